@@ -1,0 +1,199 @@
+#!/usr/bin/env python3
+"""Headline benchmark: BASELINE.json metric on config C2.
+
+  "probe+build tuples/sec at 10M⋈200M; achieved HBM GB/s vs roofline, 1/2/4/8 GPU"
+  C2: RadixCluster 2-pass (8+8 radix bits), 10M ⋈ 200M, Murmur3, Zipf s=1.05.
+
+One step = one full join over the resident relations (partition R and S,
+build, probe, count back on the host), exactly HashJoiner::Run
+(src/RadixCluster/HashJoin.hpp:190-241). Relations are generated on the
+device before the timed region (the reference also times after generation,
+src/main.cpp:254 vs :100-102).
+
+N=1:  python bench.py [--steps K --warmup W]
+N>1:  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+      Both relations are range-sharded (strong scaling: the 10M⋈200M
+      workload is fixed); the partitioned build side is all-gathered over
+      RCCL (partitionedhashjoin_amd/distributed.py).
+
+Rank 0 prints ONE JSON line. `roofline` is for the dominant kernel (longest
+per-step device time), from hipEvents on the stream the kernels run on;
+`cpu_baseline` times the oracle's restatement of the reference RadixCluster
+path (-p 1024, XXH3: its best published configuration) on this host.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
+NR, NS, ALPHA, GEN_SEED = 10_000_000, 200_000_000, 1.05, 20240601
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=["c2", "c4", "c5"],
+                    help="c2: radix 8+8 murmur3 s=1.05; c4: no-partitioning xxh3; c5: radix s=1.25")
+    ap.add_argument("--primary", type=int, default=NR)
+    ap.add_argument("--secondary", type=int, default=NS)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, cpus) - 1")
+    ap.add_argument("--verbose", action="store_true")
+    return ap.parse_args()
+
+
+def config_params(phj, name):
+    if name == "c4":
+        return phj.nopart_params(hash=phj.HASH_XXH3), ALPHA, \
+            "C4: NoPartitioning, global table in HBM, XXH3, 10M⋈200M, Zipf s=1.05"
+    if name == "c5":
+        return phj.radix_params((8, 8), hash=phj.HASH_MURMUR3), 1.25, \
+            "C5: RadixCluster 2-pass 8+8, Murmur3, 10M⋈200M, Zipf s=1.25"
+    return phj.radix_params((8, 8), hash=phj.HASH_MURMUR3), ALPHA, \
+        "C2: RadixCluster 2-pass 8+8, Murmur3, 10M⋈200M, Zipf s=1.05"
+
+
+def cpu_baseline(ctx, nR, nS, threads, verbose):
+    """The oracle's restatement of RadixCluster -p 1024 (XXH3) on this host's cores,
+    over the same device-generated relations (copied back), once."""
+    from oracle import oracle as O
+    import numpy as np
+    R = ctx.download(0)
+    S = ctx.download(1)
+    t0 = time.perf_counter()
+    res = O.join_radix(R, S, P=1024, radix=False, part_hash=O.HASH_XXH3, part_seed=1,
+                       table_hash=O.HASH_XXH3, table_seed=2, ratio=1.25, workers=threads)
+    wall = time.perf_counter() - t0
+    del R, S
+    if verbose:
+        print(f"cpu baseline: {res.as_dict()}", file=sys.stderr)
+    return {
+        "value": (nR + nS) / wall,
+        "unit": "tuples/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"full {nR // 10**6}M⋈{nS // 10**6}M workload, 1 run of the oracle's "
+                  f"RadixCluster restatement (-p 1024, XXH3, LinearProbing 3-slot 1.25x) "
+                  f"with {threads} worker threads; wall {wall * 1e3:.0f} ms "
+                  f"(partition {res.partition_ms:.0f} / build {res.build_ms:.0f} / "
+                  f"probe {res.probe_ms:.0f} ms, reference phase semantics)",
+        "matches": int(res.matches),
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    import partitionedhashjoin_amd as phj
+    from partitionedhashjoin_amd.distributed import HipShardEngine, distributed_join
+
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    nR, nS = args.primary, args.secondary
+    params, alpha, workload = config_params(phj, args.config)
+    if world > 1 and params.algo != phj.ALGO_RADIX:
+        raise SystemExit("multi-GPU bench runs the radix configs (c2, c5)")
+    engine = HipShardEngine(local_rank)
+    engine.generate(nR, nS, alpha, GEN_SEED, rank, world)
+    torch.cuda.synchronize()
+    # correctness gate at full size: every generated S key lies in [1, |R|]
+    local_inrange = engine.ctx.count_in_range(1, 1, nR)
+
+    def step():
+        if params.algo == phj.ALGO_RADIX:
+            return distributed_join(engine, params, nR, nS, rank, world, dist if world > 1 else None)
+        r = engine.ctx.join(params)
+
+        class _R:
+            matches = r.matches
+            timers = r.timers()
+        return _R
+
+    for _ in range(args.warmup):
+        step()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    acc = {}
+    matches = None
+    for _ in range(args.steps):
+        res = step()
+        matches = res.matches
+        for name, ms, nbytes in res.timers:
+            a = acc.setdefault(name, [0.0, 0, 0])
+            a[0] += ms
+            a[1] += nbytes
+            a[2] += 1
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        c = torch.tensor([local_inrange], dtype=torch.int64, device="cuda")
+        dist.all_reduce(c)
+        inrange = int(c.item())
+    else:
+        inrange = local_inrange
+
+    if rank == 0:
+        per_step = {k: (v[0] / args.steps, v[1] / args.steps) for k, v in acc.items()}
+        dom_name, (dom_ms, dom_bytes) = max(per_step.items(), key=lambda kv: kv[1][0])
+        achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+        value = (nR + nS) * args.steps / elapsed
+        out = {
+            "metric": "probe+build tuples/sec at 10M⋈200M; achieved HBM GB/s vs roofline, 1/2/4/8 GPU",
+            "value": value,
+            "unit": "tuples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "int64",
+            "data": "synthetic (device-generated Sequential R + seeded Zipf S, reference generators)",
+            "config": {"workload": workload, "primary": nR, "secondary": nS,
+                       "radix_bits": list(params.radix_bits) if params.algo == phj.ALGO_RADIX else None,
+                       "hash": "murmur3" if params.hash == phj.HASH_MURMUR3 else "xxh3",
+                       "skew": alpha, "parallelism": f"range-shard x{world}"},
+            "matches": int(matches),
+            "expected_matches": inrange,
+            "correct": int(matches) == inrange,
+            "roofline": {"bound": "hbm", "kernel": dom_name, "achieved": achieved,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": None},
+            "kernels_ms": {k: round(v[0], 4) for k, v in sorted(per_step.items())},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            threads = args.cpu_threads or max(1, min(16, os.cpu_count() or 1) - 1)
+            cb = cpu_baseline(engine.ctx, nR, nS, threads, args.verbose)
+            out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample")}
+            out["cpu_matches_gpu"] = cb["matches"] == int(matches)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,168 @@
+/*
+ * phj.h — C ABI of the MI355X-native partitioned hash join (libphj_hip.so).
+ *
+ * This is the drop-in boundary under the reference's join API. The reference
+ * (ragoragino/partitionedhashjoin, C++17, CPU only) exposes
+ *
+ *   RadixClustering::HashJoiner<HashTableFactory, HasherType>::Run(
+ *       shared_ptr<Table<Tuple>> tableA /+build+/, shared_ptr<Table<Tuple>> tableB /+probe+/,
+ *       shared_ptr<IHashJoinTimer> timer)                 src/RadixCluster/HashJoin.hpp:100-104
+ *   NoPartitioning::HashJoiner<HashTableFactory>::Run(...) src/NoPartitioning/HashJoin.hpp:23-27
+ *
+ * and reads the relations through Table<Tuple>::operator[] / GetSize()
+ * (src/Common/Table.hpp:42-46). Those entry points are kept in C++ by the
+ * host driver (partitionedhashjoin_amd/host/Gpu/HashJoin.hpp); underneath, they call
+ * only the functions below: plain pointers and sizes, no exceptions, no
+ * torch types. Conventions: 0 = PHJ_OK, negative = error (message via
+ * phj_last_error). A context owns every device buffer it allocates (grow
+ * only, allocated outside the timed phases), is bound to one HIP device and
+ * one stream, and is not thread-safe.
+ */
+#ifndef PHJ_H
+#define PHJ_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PHJ_ABI_VERSION 1
+
+/* Common::Tuple (src/Common/Table.hpp:20-25): alignas(16) {int64 id; int64 payload}. */
+typedef struct phj_tuple {
+    int64_t id;
+    int64_t payload;
+} phj_tuple;
+
+typedef struct phj_ctx phj_ctx;
+
+/* status codes */
+#define PHJ_OK 0
+#define PHJ_ERR_INVALID -1 /* bad argument (reference: std::invalid_argument) */
+#define PHJ_ERR_NOMEM -2   /* device allocation failed */
+#define PHJ_ERR_HIP -3     /* HIP runtime / kernel launch error */
+#define PHJ_ERR_STATE -4   /* call order (e.g. join before relations are bound) */
+#define PHJ_ERR_RANGE -5   /* size beyond a documented limit */
+
+/* Common::JoinAlgorithmType values (src/Common/Configuration.hpp:12-15). */
+#define PHJ_ALGO_NO_PARTITIONING 0
+#define PHJ_ALGO_RADIX 1
+
+/* hash functions: XXH3_64bits_withSeed over the 8-byte key (XXHasher.hpp:19-22)
+ * and the Murmur3 fmix64 finalizer over key ^ seed (BASELINE config C2). */
+#define PHJ_HASH_XXH3 0
+#define PHJ_HASH_MURMUR3 1
+
+/* relation sides: tableA = build (R), tableB = probe (S) (HashJoin.hpp:99) */
+#define PHJ_SIDE_BUILD 0
+#define PHJ_SIDE_PROBE 1
+
+typedef struct phj_join_params {
+    int32_t algo;            /* PHJ_ALGO_* */
+    int32_t hash;            /* PHJ_HASH_* */
+    uint64_t hash_seed;      /* XXHasher seed (random in the reference, explicit here) */
+    /* Radix partition id q(key):
+     *   num_partitions > 0 : q = hash % num_partitions  (reference `-p P`, HashJoin.hpp:349-351)
+     *   num_partitions == 0: q = hash & (2^(b0+b1) - 1) (power-of-two radix, radix_bits = {b0, b1})
+     * Partitioning takes one pass when q has <= 11 bits and two otherwise
+     * (pass digits: high bits first). Maximum 22 bits (4,194,304 partitions). */
+    uint32_t num_partitions;
+    uint8_t radix_bits[2];
+    uint8_t reserved[2];
+    /* NoPartitioning: hash-table slots per build tuple (>= 1). 0 selects the default. */
+    double table_ratio;
+} phj_join_params;
+
+#define PHJ_MAX_TIMERS 32
+#define PHJ_TIMER_NAME 24
+
+typedef struct phj_join_result {
+    uint64_t matches;            /* #probe tuples with >= 1 equal build key (semi-join count:
+                                    the "Joined N tuples" of RadixCluster/HashJoin.hpp:320-321) */
+    double partition_ms;         /* reference phase keys (Results.hpp:274-276), device time */
+    double build_ms;
+    double probe_ms;             /* probe alone (the reference's NoPartitioning probe also
+                                    counts its build, Results.hpp:202; see phj host driver) */
+    double total_ms;             /* first kernel start .. count on host */
+    uint64_t algorithmic_bytes;  /* HBM bytes the algorithm must move */
+    uint32_t num_partitions;     /* final partition count (radix) */
+    uint32_t num_timers;
+    double timer_ms[PHJ_MAX_TIMERS];        /* per-kernel device time (hipEvents on the ctx stream) */
+    uint64_t timer_bytes[PHJ_MAX_TIMERS];   /* algorithmic bytes of that launch */
+    char timer_name[PHJ_MAX_TIMERS][PHJ_TIMER_NAME];
+} phj_join_result;
+
+/* A partitioned relation on the device: SoA key/payload columns in partition
+ * order, bounds[num_partitions + 1] offsets (uint32). Views are owned by the
+ * ctx that produced them (valid until the next partition call on that side)
+ * or by the caller (gathered shards on multi-GPU). */
+typedef struct phj_partitioned {
+    const int64_t *keys;
+    const int64_t *payloads;
+    const uint32_t *bounds;
+    uint64_t n;
+    uint32_t num_partitions;
+    uint32_t reserved;
+} phj_partitioned;
+
+/* ---- context ---- */
+int phj_ctx_create(int device, phj_ctx **out);
+void phj_ctx_destroy(phj_ctx *ctx);
+const char *phj_last_error(const phj_ctx *ctx);
+/* Run on an external stream (e.g. torch.cuda.current_stream()); NULL = ctx-owned stream. */
+int phj_ctx_set_stream(phj_ctx *ctx, void *hip_stream);
+int phj_ctx_synchronize(phj_ctx *ctx);
+int phj_abi_version(void);
+
+/* ---- relations (Table<Tuple>: &(*table)[0], GetSize(), Table.hpp:42-46) ---- */
+/* Copy a host relation to ctx-owned device memory (H2D, synchronous). */
+int phj_relation_upload(phj_ctx *ctx, int side, const phj_tuple *host, uint64_t n);
+/* Borrow a device relation (caller keeps it alive while the ctx uses it). */
+int phj_relation_bind_device(phj_ctx *ctx, int side, const phj_tuple *dev, uint64_t n);
+/* Device pointer of the bound relation (NULL if none). */
+const phj_tuple *phj_relation_device_ptr(phj_ctx *ctx, int side, uint64_t *n);
+/* Copy the bound relation back to host (n tuples). */
+int phj_relation_download(phj_ctx *ctx, int side, phj_tuple *host, uint64_t n);
+/* On-device generators: Sequential::FillTable (Sequential.cpp:6-40)
+ * and Zipf::FillTable (Zipf.cpp:58-108) over [lo, hi] with LCG streams seeded
+ * per 4096-tuple batch. Rows [first_index, first_index + n) of the full
+ * relation are generated (a range shard on multi-GPU; 0 = the whole table),
+ * so shards concatenate to exactly the single-device relation. The Zipf
+ * kernel uses the device libm pow; the host generator is the parity source. */
+int phj_relation_generate_sequential(phj_ctx *ctx, int side, uint64_t n, int64_t start,
+                                     uint64_t first_index);
+int phj_relation_generate_zipf(phj_ctx *ctx, int side, uint64_t n, double alpha, int64_t lo,
+                               int64_t hi, uint64_t seed, uint64_t first_index);
+/* Count tuples of the bound relation with lo <= id <= hi (device reduction). */
+int phj_relation_count_in_range(phj_ctx *ctx, int side, int64_t lo, int64_t hi, uint64_t *count);
+
+/* ---- the join (HashJoiner::Run) ---- */
+/* Synchronous: partition (radix) / build / probe on the device, count back on the host. */
+int phj_join(phj_ctx *ctx, const phj_join_params *p, phj_join_result *r);
+
+/* ---- building blocks (multi-GPU: range-sharded relations, RCCL exchange) ---- */
+/* Radix-partition the bound relation of `side`; fills `out` with ctx-owned views.
+ * Asynchronous on the ctx stream (order later work on the same stream). */
+int phj_partition(phj_ctx *ctx, int side, const phj_join_params *p, phj_partitioned *out);
+/* Build bucket-chained tables over the union of `nbuild` partitioned build
+ * segments (e.g. every rank's shard after an all-gather) and probe the ctx's
+ * partitioned probe relation (phj_partition(PHJ_SIDE_PROBE) with the same
+ * params must precede). Synchronous; fills r (build_ms, probe_ms, matches). */
+int phj_join_partitioned(phj_ctx *ctx, const phj_join_params *p, int nbuild,
+                         const phj_partitioned *build, phj_join_result *r);
+/* Copy a partitioned view (keys, payloads: n; bounds: P+1) to host or device
+ * buffers (any may be NULL). Synchronous. */
+int phj_partitioned_download(phj_ctx *ctx, const phj_partitioned *v, int64_t *keys,
+                             int64_t *payloads, uint32_t *bounds);
+
+/* ---- hashing on the device (tests / host parity) ---- */
+/* out[i] = hash(keys[i]) for n host keys, evaluated by the device kernel. */
+int phj_hash_keys(phj_ctx *ctx, int hash, uint64_t seed, const int64_t *keys, uint64_t n,
+                  uint64_t *out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PHJ_H */

@@ -1,0 +1,159 @@
+"""partitionedhashjoin_amd — MI355X-native radix-partitioned / no-partitioning hash join.
+
+The product is the HIP library libphj_hip.so (C ABI: include/phj.h) plus the
+C++ host driver `phjoin` that keeps the reference's CLI, Configuration and
+Table<Tuple> API (ragoragino/partitionedhashjoin, src/main.cpp). This Python
+module is plumbing over the same C ABI for tests, bench.py and the
+torch.distributed multi-GPU driver. It never falls back to a CPU path:
+without the built HIP library every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _capi
+from ._capi import (ALGO_NO_PARTITIONING, ALGO_RADIX, HASH_MURMUR3, HASH_XXH3, SIDE_BUILD,
+                    SIDE_PROBE, JoinParams, JoinResult, Partitioned, PhjError)
+
+__all__ = ["Context", "radix_params", "nopart_params", "JoinParams", "JoinResult",
+           "Partitioned", "PhjError", "ALGO_RADIX", "ALGO_NO_PARTITIONING", "HASH_XXH3",
+           "HASH_MURMUR3", "SIDE_BUILD", "SIDE_PROBE", "DEFAULT_SEED"]
+
+DEFAULT_SEED = 0x9E3779B97F4A7C15
+
+
+def radix_params(bits=(8, 8), num_partitions=0, hash=HASH_MURMUR3, seed=DEFAULT_SEED) -> JoinParams:
+    """RadixCluster parameters. num_partitions > 0 reproduces the reference's
+    `hash % P` partitioning (`phjoin -p P`); otherwise q = hash & (2^(b0+b1)-1)."""
+    p = JoinParams()
+    p.algo = ALGO_RADIX
+    p.hash = hash
+    p.hash_seed = seed
+    p.num_partitions = num_partitions
+    p.radix_bits[0] = bits[0]
+    p.radix_bits[1] = bits[1] if len(bits) > 1 else 0
+    p.table_ratio = 0.0
+    return p
+
+
+def nopart_params(hash=HASH_XXH3, seed=DEFAULT_SEED, table_ratio=0.0) -> JoinParams:
+    p = JoinParams()
+    p.algo = ALGO_NO_PARTITIONING
+    p.hash = hash
+    p.hash_seed = seed
+    p.table_ratio = table_ratio
+    return p
+
+
+class Context:
+    """One HIP device + stream + workspace (phj_ctx)."""
+
+    def __init__(self, device: int = 0):
+        self._L = _capi.load()
+        h = C.c_void_p()
+        rc = self._L.phj_ctx_create(device, C.byref(h))
+        if rc != 0:
+            raise PhjError(rc, f"phj_ctx_create(device={device}) failed")
+        self._h = h
+        self.device = device
+        self._keep = {}
+
+    # -- lifecycle --
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.phj_ctx_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc != 0:
+            raise PhjError(rc, self._L.phj_last_error(self._h).decode())
+
+    def set_stream(self, stream_ptr: int | None):
+        self._check(self._L.phj_ctx_set_stream(self._h, C.c_void_p(stream_ptr or 0)))
+
+    def synchronize(self):
+        self._check(self._L.phj_ctx_synchronize(self._h))
+
+    # -- relations --
+    def upload(self, side: int, rel: np.ndarray):
+        rel = np.ascontiguousarray(rel, dtype=np.int64)
+        assert rel.ndim == 2 and rel.shape[1] == 2
+        self._check(self._L.phj_relation_upload(self._h, side, rel.ctypes.data_as(C.c_void_p),
+                                                rel.shape[0]))
+
+    def bind_device(self, side: int, ptr: int, n: int, keepalive=None):
+        self._keep[side] = keepalive
+        self._check(self._L.phj_relation_bind_device(self._h, side, C.c_void_p(ptr), n))
+
+    def relation_ptr(self, side: int):
+        n = C.c_uint64()
+        p = self._L.phj_relation_device_ptr(self._h, side, C.byref(n))
+        return p, n.value
+
+    def download(self, side: int, n: int | None = None) -> np.ndarray:
+        if n is None:
+            n = self.relation_ptr(side)[1]
+        out = np.zeros((n, 2), dtype=np.int64)
+        self._check(self._L.phj_relation_download(self._h, side, out.ctypes.data_as(C.c_void_p), n))
+        return out
+
+    def generate_sequential(self, side: int, n: int, start: int = 1, first_index: int = 0):
+        self._check(self._L.phj_relation_generate_sequential(self._h, side, n, start, first_index))
+
+    def generate_zipf(self, side: int, n: int, alpha: float, lo: int, hi: int, seed: int,
+                      first_index: int = 0):
+        self._check(self._L.phj_relation_generate_zipf(self._h, side, n, alpha, lo, hi, seed,
+                                                       first_index))
+
+    def count_in_range(self, side: int, lo: int, hi: int) -> int:
+        c = C.c_uint64()
+        self._check(self._L.phj_relation_count_in_range(self._h, side, lo, hi, C.byref(c)))
+        return c.value
+
+    # -- join --
+    def join(self, params: JoinParams) -> JoinResult:
+        r = JoinResult()
+        self._check(self._L.phj_join(self._h, C.byref(params), C.byref(r)))
+        return r
+
+    def partition(self, side: int, params: JoinParams) -> Partitioned:
+        v = Partitioned()
+        self._check(self._L.phj_partition(self._h, side, C.byref(params), C.byref(v)))
+        return v
+
+    def join_partitioned(self, params: JoinParams, segments) -> JoinResult:
+        arr = (Partitioned * len(segments))(*segments)
+        r = JoinResult()
+        self._check(self._L.phj_join_partitioned(self._h, C.byref(params), len(segments), arr,
+                                                 C.byref(r)))
+        return r
+
+    def download_partitioned(self, v: Partitioned):
+        keys = np.zeros(v.n, dtype=np.int64)
+        pays = np.zeros(v.n, dtype=np.int64)
+        bounds = np.zeros(v.num_partitions + 1, dtype=np.uint32)
+        self._check(self._L.phj_partitioned_download(
+            self._h, C.byref(v), keys.ctypes.data_as(C.c_void_p), pays.ctypes.data_as(C.c_void_p),
+            bounds.ctypes.data_as(C.c_void_p)))
+        return keys, pays, bounds
+
+    def hash_keys(self, kind: int, seed: int, keys) -> np.ndarray:
+        keys = np.ascontiguousarray(np.asarray(keys, dtype=np.int64))
+        out = np.zeros(keys.shape[0], dtype=np.uint64)
+        self._check(self._L.phj_hash_keys(self._h, kind, seed, keys.ctypes.data_as(C.c_void_p),
+                                          keys.shape[0], out.ctypes.data_as(C.c_void_p)))
+        return out

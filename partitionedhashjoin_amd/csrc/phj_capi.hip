@@ -1,0 +1,874 @@
+// phj_capi.hip — the C ABI (include/phj.h) over the gfx950 kernels.
+//
+// Orchestration of the reference's HashJoiner::Run on one MI355X:
+//   radix:          Partition(R), Partition(S)            RadixCluster/HashJoin.hpp:208-224
+//                   -> build + probe per partition        :243-331
+//   no-partitioning: Build(R) -> Probe(S)                 NoPartitioning/HashJoin.hpp:54-187
+// Every kernel is launched on the ctx stream; device buffers are allocated
+// once (grow-only) before the timed region; phases are timed with hipEvents
+// on the same stream. Errors never cross the ABI as exceptions: they become
+// negative status codes plus a message (phj_last_error).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/phj.h"
+#include "phj_join.h"
+#include "phj_partition.h"
+
+using namespace phj;
+
+namespace {
+
+constexpr int kPartItems = 8;                       // tuples per thread in a partition tile
+constexpr uint32_t kTile = kBlock * kPartItems;     // 2048 tuples per tile
+constexpr int kProbeItems = 16;                     // S keys per thread per probe item
+constexpr uint32_t kChunk = kBlock * kProbeItems;   // 4096 S tuples per probe item
+constexpr int kNPProbeItems = 4;
+constexpr double kNPDefaultRatio = 2.0;             // slots per build tuple
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+struct Plan {
+    int hk = 0;
+    uint64_t seed = 0;
+    uint32_t mode = 0;    // 0: q = h & (P-1), 1: q = h % P
+    uint64_t P = 0;       // logical partitions
+    uint32_t npass = 1;
+    uint32_t nb1 = 1, nb2 = 1;
+    uint32_t bits1 = 0, bits2 = 0;
+    uint32_t shift1 = 0, dmask1 = 0, dmask2 = 0;
+    uint32_t Ppad = 1;    // nb1 * nb2 = final bounds length - 1
+    bool operator==(const Plan& o) const {
+        return hk == o.hk && seed == o.seed && mode == o.mode && P == o.P && npass == o.npass &&
+               nb1 == o.nb1 && nb2 == o.nb2;
+    }
+};
+
+struct TimerRec {
+    std::string name;
+    uint64_t bytes;
+    hipEvent_t a, b;
+};
+
+struct SideState {
+    const phj_tuple* rel = nullptr;
+    uint64_t n = 0;
+    DevBuf owned;
+    DevBuf kA, pA, kB, pB;
+    DevBuf hist1, hist2, bounds1, tbase2, bounds;
+    phj_partitioned view{};
+    bool partitioned = false;
+    Plan plan;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
+uint32_t ceil_log2(uint64_t x) {
+    uint32_t b = 0;
+    while ((1ull << b) < x) b++;
+    return b;
+}
+
+uint32_t next_pow2_u32(uint32_t x) {
+    uint32_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+}  // namespace
+
+struct phj_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    SideState side[2];
+    DevBuf scan_partials, prep, tkeys, tpays, toffs, gcursor, items, count;
+    DevBuf np_tab, np_pays;
+    std::vector<hipEvent_t> evpool;
+    size_t evnext = 0;
+    std::vector<TimerRec> timers;
+    std::string err;
+    int max_lds = 65536;
+};
+
+namespace {
+
+int set_err(phj_ctx* c, int code, const std::string& msg) {
+    if (c) c->err = msg;
+    return code;
+}
+
+#define PHJ_HIP(ctx, expr)                                                                   \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess)                                                                \
+            return set_err(ctx, PHJ_ERR_HIP,                                                 \
+                           std::string(#expr) + ": " + hipGetErrorString(e_));               \
+    } while (0)
+
+#define PHJ_LAUNCHED(ctx, what)                                                              \
+    do {                                                                                     \
+        hipError_t e_ = hipGetLastError();                                                   \
+        if (e_ != hipSuccess)                                                                \
+            return set_err(ctx, PHJ_ERR_HIP, std::string("launch ") + what + ": " +         \
+                                                 hipGetErrorString(e_));                     \
+    } while (0)
+
+#define PHJ_TRY(expr)           \
+    do {                        \
+        int rc_ = (expr);       \
+        if (rc_ != PHJ_OK) return rc_; \
+    } while (0)
+
+int ensure(phj_ctx* c, DevBuf& b, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (b.bytes >= bytes) return PHJ_OK;
+    if (b.p) {
+        PHJ_HIP(c, hipStreamSynchronize(c->stream));
+        PHJ_HIP(c, hipFree(b.p));
+        b.p = nullptr;
+        b.bytes = 0;
+    }
+    const size_t rounded = (bytes + 4095) & ~size_t(4095);
+    hipError_t e = hipMalloc(&b.p, rounded);
+    if (e != hipSuccess) {
+        b.p = nullptr;
+        return set_err(c, PHJ_ERR_NOMEM, "hipMalloc(" + std::to_string(rounded) + "): " + hipGetErrorString(e));
+    }
+    b.bytes = rounded;
+    return PHJ_OK;
+}
+
+void free_buf(DevBuf& b) {
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+}
+
+hipEvent_t next_event(phj_ctx* c) {
+    if (c->evnext == c->evpool.size()) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        c->evpool.push_back(e);
+    }
+    return c->evpool[c->evnext++];
+}
+
+int mark(phj_ctx* c, hipEvent_t* out) {
+    *out = next_event(c);
+    if (!*out) return set_err(c, PHJ_ERR_HIP, "hipEventCreate failed");
+    PHJ_HIP(c, hipEventRecord(*out, c->stream));
+    return PHJ_OK;
+}
+
+int timer_begin(phj_ctx* c, const char* name, uint64_t bytes) {
+    TimerRec t{name, bytes, nullptr, nullptr};
+    PHJ_TRY(mark(c, &t.a));
+    c->timers.push_back(t);
+    return PHJ_OK;
+}
+
+int timer_end(phj_ctx* c) { return mark(c, &c->timers.back().b); }
+
+void reset_timers(phj_ctx* c) {
+    c->timers.clear();
+    c->evnext = 0;
+}
+
+int fill_timers(phj_ctx* c, phj_join_result* r) {
+    r->num_timers = 0;
+    for (const TimerRec& t : c->timers) {
+        if (r->num_timers >= PHJ_MAX_TIMERS) break;
+        float ms = 0;
+        PHJ_HIP(c, hipEventElapsedTime(&ms, t.a, t.b));
+        const uint32_t i = r->num_timers++;
+        r->timer_ms[i] = ms;
+        r->timer_bytes[i] = t.bytes;
+        std::snprintf(r->timer_name[i], PHJ_TIMER_NAME, "%s", t.name.c_str());
+    }
+    return PHJ_OK;
+}
+
+double elapsed(phj_ctx* c, hipEvent_t a, hipEvent_t b) {
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return -1.0;
+    (void)c;
+    return ms;
+}
+
+int make_plan(phj_ctx* c, const phj_join_params* p, Plan& pl) {
+    if (!p) return set_err(c, PHJ_ERR_INVALID, "null params");
+    if (p->hash != PHJ_HASH_XXH3 && p->hash != PHJ_HASH_MURMUR3)
+        return set_err(c, PHJ_ERR_INVALID, "unknown hash function");
+    pl = Plan{};
+    pl.hk = p->hash;
+    pl.seed = p->hash_seed;
+    if (p->num_partitions > 0) {
+        pl.mode = 1;
+        pl.P = p->num_partitions;
+        if (pl.P <= static_cast<uint64_t>(kMaxBins)) {
+            pl.npass = 1;
+            pl.nb1 = static_cast<uint32_t>(pl.P);
+            pl.bits1 = ceil_log2(pl.P);
+            pl.shift1 = 0;
+            pl.dmask1 = 0xffffffffu;
+        } else {
+            if (pl.P > (1ull << (2 * kMaxDigitBits)))
+                return set_err(c, PHJ_ERR_RANGE, "num_partitions above 2^22");
+            pl.npass = 2;
+            pl.nb2 = kMaxBins;
+            pl.bits2 = kMaxDigitBits;
+            pl.nb1 = static_cast<uint32_t>((pl.P + kMaxBins - 1) / kMaxBins);
+            pl.bits1 = ceil_log2(pl.nb1);
+            pl.shift1 = kMaxDigitBits;
+            pl.dmask1 = 0xffffffffu;
+            pl.dmask2 = kMaxBins - 1;
+        }
+    } else {
+        const uint32_t b0 = p->radix_bits[0], b1 = p->radix_bits[1];
+        if (b0 < 1 || b0 > static_cast<uint32_t>(kMaxDigitBits) || b1 > static_cast<uint32_t>(kMaxDigitBits))
+            return set_err(c, PHJ_ERR_INVALID, "radix_bits must be in [1,11] x [0,11]");
+        pl.mode = 0;
+        pl.P = 1ull << (b0 + b1);
+        pl.nb1 = 1u << b0;
+        pl.bits1 = b0;
+        pl.dmask1 = pl.nb1 - 1;
+        pl.shift1 = b1;
+        if (b1 == 0) {
+            pl.npass = 1;
+        } else {
+            pl.npass = 2;
+            pl.nb2 = 1u << b1;
+            pl.bits2 = b1;
+            pl.dmask2 = pl.nb2 - 1;
+        }
+    }
+    pl.Ppad = pl.nb1 * pl.nb2;
+    return PHJ_OK;
+}
+
+DigitFn digit_fn(const Plan& pl, int pass) {
+    DigitFn f{};
+    f.seed = pl.seed;
+    f.P = pl.P;
+    f.mode = pl.mode;
+    f.magic = pl.mode == 1 ? (~0ull) / pl.P : 0;
+    if (pass == 1) {
+        f.shift = pl.shift1;
+        f.dmask = pl.dmask1;
+    } else {
+        f.shift = 0;
+        f.dmask = pl.dmask2;
+    }
+    return f;
+}
+
+int scan_u32(phj_ctx* c, uint32_t* data, uint32_t len, uint32_t narrays, uint32_t stride) {
+    if (len == 0) return PHJ_OK;
+    ScanArgs s{};
+    s.data = data;
+    s.len = len;
+    s.stride = stride;
+    s.nblk = (len + kScanBlockElems - 1) / kScanBlockElems;
+    PHJ_TRY(ensure(c, c->scan_partials, static_cast<size_t>(s.nblk) * narrays * 4));
+    s.partials = static_cast<uint32_t*>(c->scan_partials.p);
+    hipLaunchKernelGGL(k_scan_reduce, dim3(s.nblk, narrays), dim3(kBlock), 0, c->stream, s);
+    PHJ_LAUNCHED(c, "k_scan_reduce");
+    hipLaunchKernelGGL(k_scan_partials, dim3(1, narrays), dim3(1024), 0, c->stream, s);
+    PHJ_LAUNCHED(c, "k_scan_partials");
+    hipLaunchKernelGGL(k_scan_apply, dim3(s.nblk, narrays), dim3(kBlock), 0, c->stream, s);
+    PHJ_LAUNCHED(c, "k_scan_apply");
+    return PHJ_OK;
+}
+
+template <bool AOS>
+int launch_pass(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const std::string& prefix,
+                uint64_t n, uint32_t hist_len) {
+    if (grid == 0) return PHJ_OK;
+    const size_t hist_lds = static_cast<size_t>(kWaves) * a.nbins * 4;
+    const size_t sc_lds = scatter_lds_bytes(kTile, a.nbins);
+    const std::string hname = prefix + ".hist", cname = prefix + ".scan", sname = prefix + ".scatter";
+    // algorithmic bytes: the histogram reads the key (a whole 16-B tuple when AoS);
+    // the scatter reads and writes every tuple once (16 + 16 B)
+    PHJ_TRY(timer_begin(c, hname.c_str(), n * (AOS ? 16 : 8)));
+    if (hk == kMurmur3)
+        hipLaunchKernelGGL((k_hist<kPartItems, AOS, kMurmur3>), dim3(grid), dim3(kBlock), hist_lds, c->stream, a);
+    else
+        hipLaunchKernelGGL((k_hist<kPartItems, AOS, kXXH3>), dim3(grid), dim3(kBlock), hist_lds, c->stream, a);
+    PHJ_LAUNCHED(c, hname);
+    PHJ_TRY(timer_end(c));
+    PHJ_TRY(timer_begin(c, cname.c_str(), static_cast<uint64_t>(hist_len) * 12));
+    PHJ_TRY(scan_u32(c, a.hist, hist_len, 1, hist_len));
+    PHJ_TRY(timer_end(c));
+    PHJ_TRY(timer_begin(c, sname.c_str(), n * 32));
+    if (hk == kMurmur3)
+        hipLaunchKernelGGL((k_scatter<kPartItems, AOS, kMurmur3>), dim3(grid), dim3(kBlock), sc_lds, c->stream, a);
+    else
+        hipLaunchKernelGGL((k_scatter<kPartItems, AOS, kXXH3>), dim3(grid), dim3(kBlock), sc_lds, c->stream, a);
+    PHJ_LAUNCHED(c, sname);
+    PHJ_TRY(timer_end(c));
+    return PHJ_OK;
+}
+
+int partition_side(phj_ctx* c, int s, const Plan& pl) {
+    SideState& S = c->side[s];
+    if (!S.rel && S.n > 0) return set_err(c, PHJ_ERR_STATE, "relation not bound");
+    const uint64_t n64 = S.n;
+    if (n64 >= (1ull << 32) - 2 * kTile) return set_err(c, PHJ_ERR_RANGE, "relation above 2^32 tuples per device");
+    const uint32_t n = static_cast<uint32_t>(n64);
+    const uint32_t nt1 = (n + kTile - 1) / kTile;
+    const char* tag = s == PHJ_SIDE_BUILD ? "R" : "S";
+    // workspace (grow-only; allocation is outside the timed phases on reuse)
+    PHJ_TRY(ensure(c, S.kA, static_cast<size_t>(n) * 8));
+    PHJ_TRY(ensure(c, S.pA, static_cast<size_t>(n) * 8));
+    PHJ_TRY(ensure(c, S.hist1, static_cast<size_t>(nt1) * pl.nb1 * 4));
+    PHJ_TRY(ensure(c, S.bounds1, (static_cast<size_t>(pl.nb1) + 1) * 4));
+    if (pl.npass == 2) {
+        PHJ_TRY(ensure(c, S.kB, static_cast<size_t>(n) * 8));
+        PHJ_TRY(ensure(c, S.pB, static_cast<size_t>(n) * 8));
+        PHJ_TRY(ensure(c, S.tbase2, (static_cast<size_t>(pl.nb1) + 1) * 4));
+        PHJ_TRY(ensure(c, S.hist2, (static_cast<size_t>(nt1) + pl.nb1) * pl.nb2 * 4));
+        PHJ_TRY(ensure(c, S.bounds, (static_cast<size_t>(pl.Ppad) + 1) * 4));
+    }
+    // pass 1: AoS relation -> SoA columns A
+    PassArgs a{};
+    a.in_keys = reinterpret_cast<const int64_t*>(S.rel);
+    a.out_keys = static_cast<int64_t*>(S.kA.p);
+    a.out_pays = static_cast<int64_t*>(S.pA.p);
+    a.hist = static_cast<uint32_t*>(S.hist1.p);
+    a.seg_bounds = nullptr;
+    a.tile_base = nullptr;
+    a.nseg = 1;
+    a.n = n;
+    a.ntiles1 = nt1;
+    a.nbins = pl.nb1;
+    a.nbits = pl.bits1;
+    a.f = digit_fn(pl, 1);
+    PHJ_TRY(launch_pass<true>(c, pl.hk, a, nt1, std::string(tag) + ".p1", n, nt1 * pl.nb1));
+    uint32_t* tb2 = pl.npass == 2 ? static_cast<uint32_t*>(S.tbase2.p) : nullptr;
+    hipLaunchKernelGGL(k_pass1_finish, dim3(1), dim3(1024), 0, c->stream, a.hist, nt1, pl.nb1, n,
+                       kTile, static_cast<uint32_t*>(S.bounds1.p), tb2);
+    PHJ_LAUNCHED(c, "k_pass1_finish");
+    if (pl.npass == 1) {
+        S.view.keys = static_cast<const int64_t*>(S.kA.p);
+        S.view.payloads = static_cast<const int64_t*>(S.pA.p);
+        S.view.bounds = static_cast<const uint32_t*>(S.bounds1.p);
+    } else {
+        PassArgs b{};
+        b.in_keys = static_cast<const int64_t*>(S.kA.p);
+        b.in_pays = static_cast<const int64_t*>(S.pA.p);
+        b.out_keys = static_cast<int64_t*>(S.kB.p);
+        b.out_pays = static_cast<int64_t*>(S.pB.p);
+        b.hist = static_cast<uint32_t*>(S.hist2.p);
+        b.seg_bounds = static_cast<const uint32_t*>(S.bounds1.p);
+        b.tile_base = tb2;
+        b.nseg = pl.nb1;
+        b.n = n;
+        b.ntiles1 = 0;
+        b.nbins = pl.nb2;
+        b.nbits = pl.bits2;
+        b.f = digit_fn(pl, 2);
+        const uint32_t grid2 = n ? nt1 + pl.nb1 : 0;
+        PHJ_TRY(launch_pass<false>(c, pl.hk, b, grid2, std::string(tag) + ".p2", n, grid2 * pl.nb2));
+        const uint32_t nbnd = pl.Ppad + 1;
+        hipLaunchKernelGGL(k_pass2_bounds, dim3((nbnd + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream,
+                           b.hist, tb2, b.seg_bounds, pl.nb1, pl.nb2, n, static_cast<uint32_t*>(S.bounds.p));
+        PHJ_LAUNCHED(c, "k_pass2_bounds");
+        S.view.keys = static_cast<const int64_t*>(S.kB.p);
+        S.view.payloads = static_cast<const int64_t*>(S.pB.p);
+        S.view.bounds = static_cast<const uint32_t*>(S.bounds.p);
+    }
+    S.view.n = n;
+    S.view.num_partitions = pl.Ppad;
+    S.partitioned = true;
+    S.plan = pl;
+    return PHJ_OK;
+}
+
+// Build over `nseg` partitioned build segments and probe the ctx's partitioned
+// probe side. Records "build" and "probe" timers; returns events bracketing them.
+int build_and_probe(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned* segs,
+                    hipEvent_t* e_build0, hipEvent_t* e_build1, hipEvent_t* e_probe1) {
+    SideState& PS = c->side[PHJ_SIDE_PROBE];
+    if (!PS.partitioned || !(PS.plan == pl))
+        return set_err(c, PHJ_ERR_STATE, "probe relation not partitioned with these params");
+    if (nseg < 1 || nseg > kMaxSegs) return set_err(c, PHJ_ERR_INVALID, "nbuild must be in [1,16]");
+    const uint32_t P = pl.Ppad;
+    SegList L{};
+    L.nseg = static_cast<uint32_t>(nseg);
+    L.P = P;
+    uint64_t nR = 0;
+    for (int g = 0; g < nseg; g++) {
+        if (segs[g].num_partitions != P)
+            return set_err(c, PHJ_ERR_INVALID, "build segment partition count mismatch");
+        L.seg[g].keys = segs[g].keys;
+        L.seg[g].pays = segs[g].payloads;
+        L.seg[g].bounds = segs[g].bounds;
+        nR += segs[g].n;
+    }
+    if (nR >= (1ull << 32) - 1) return set_err(c, PHJ_ERR_RANGE, "build side above 2^32 tuples");
+    const uint64_t nS = PS.view.n;
+    const size_t stride = static_cast<size_t>(P) + 1;
+    PHJ_TRY(ensure(c, c->prep, stride * 3 * 4));
+    PHJ_TRY(ensure(c, c->tkeys, nR * 8));
+    PHJ_TRY(ensure(c, c->tpays, nR * 8));
+    const size_t noffs = nR + 2 * static_cast<size_t>(P) + 1;
+    PHJ_TRY(ensure(c, c->toffs, noffs * 4));
+    PHJ_TRY(ensure(c, c->gcursor, noffs * 4));
+    const size_t item_bound = P + (nS + kChunk - 1) / kChunk;
+    PHJ_TRY(ensure(c, c->items, item_bound * 8));
+    PHJ_TRY(ensure(c, c->count, 8));
+    uint32_t* prep = static_cast<uint32_t*>(c->prep.p);
+    // LDS capacities from the expected partition size (larger partitions take
+    // the global-memory path; results are identical).
+    const uint64_t expect = (nR + P - 1) / P;
+    const uint32_t kcap = expect * 2 > 8192 ? 256u : std::max<uint32_t>(256, next_pow2_u32(static_cast<uint32_t>(expect * 2)));
+    const uint32_t ocap_probe = kcap / 2 + 1;
+    const uint32_t ocap_build = std::min<uint32_t>(16384, std::max<uint32_t>(256, kcap));
+
+    PHJ_TRY(mark(c, e_build0));
+    PHJ_TRY(timer_begin(c, "build", nR * 32));
+    hipLaunchKernelGGL(k_join_prep, dim3((P + 1 + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream, L,
+                       PS.view.bounds, kChunk, prep);
+    PHJ_LAUNCHED(c, "k_join_prep");
+    PHJ_TRY(scan_u32(c, prep, P + 1, 3, static_cast<uint32_t>(stride)));
+    const uint32_t* tkb = prep;
+    const uint32_t* tob = prep + stride;
+    const uint32_t* itb = prep + 2 * stride;
+    hipLaunchKernelGGL(k_items_expand, dim3((P + kWaves - 1) / kWaves), dim3(kBlock), 0, c->stream, itb, P,
+                       static_cast<uint2*>(c->items.p));
+    PHJ_LAUNCHED(c, "k_items_expand");
+    BuildArgs ba{};
+    ba.L = L;
+    ba.tkb = tkb;
+    ba.tob = tob;
+    ba.tkeys = static_cast<int64_t*>(c->tkeys.p);
+    ba.tpays = static_cast<int64_t*>(c->tpays.p);
+    ba.toffs = static_cast<uint32_t*>(c->toffs.p);
+    ba.gcursor = static_cast<uint32_t*>(c->gcursor.p);
+    ba.ocap = ocap_build;
+    ba.seed = pl.seed;
+    const uint32_t bgrid = std::min<uint32_t>(P, 8192);
+    const size_t blds = 64 + static_cast<size_t>(ocap_build) * 4;
+    if (pl.hk == kMurmur3)
+        hipLaunchKernelGGL((k_build<kMurmur3>), dim3(bgrid), dim3(kBlock), blds, c->stream, ba);
+    else
+        hipLaunchKernelGGL((k_build<kXXH3>), dim3(bgrid), dim3(kBlock), blds, c->stream, ba);
+    PHJ_LAUNCHED(c, "k_build");
+    PHJ_TRY(timer_end(c));
+    PHJ_TRY(mark(c, e_build1));
+
+    PHJ_HIP(c, hipMemsetAsync(c->count.p, 0, 8, c->stream));
+    ProbeArgs pa{};
+    pa.skeys = PS.view.keys;
+    pa.sbounds = PS.view.bounds;
+    pa.tkb = tkb;
+    pa.tob = tob;
+    pa.tkeys = static_cast<const int64_t*>(c->tkeys.p);
+    pa.toffs = static_cast<const uint32_t*>(c->toffs.p);
+    pa.items = static_cast<const uint2*>(c->items.p);
+    pa.nitems = itb + P;
+    pa.count = static_cast<unsigned long long*>(c->count.p);
+    pa.kcap = kcap;
+    pa.ocap = ocap_probe;
+    pa.seed = pl.seed;
+    const size_t plds = static_cast<size_t>(kcap) * 8 + static_cast<size_t>(ocap_probe) * 4 + 16;
+    const uint32_t pgrid = static_cast<uint32_t>(std::max<size_t>(1, std::min<size_t>(item_bound, 2048)));
+    PHJ_TRY(timer_begin(c, "probe", nS * 8 + nR * 8));
+    if (pl.hk == kMurmur3)
+        hipLaunchKernelGGL((k_probe<kMurmur3, kProbeItems>), dim3(pgrid), dim3(kBlock), plds, c->stream, pa);
+    else
+        hipLaunchKernelGGL((k_probe<kXXH3, kProbeItems>), dim3(pgrid), dim3(kBlock), plds, c->stream, pa);
+    PHJ_LAUNCHED(c, "k_probe");
+    PHJ_TRY(timer_end(c));
+    PHJ_TRY(mark(c, e_probe1));
+    return PHJ_OK;
+}
+
+int get_count(phj_ctx* c, uint64_t* out) {
+    unsigned long long h = 0;
+    PHJ_HIP(c, hipMemcpyAsync(&h, c->count.p, 8, hipMemcpyDeviceToHost, c->stream));
+    PHJ_HIP(c, hipStreamSynchronize(c->stream));
+    *out = h;
+    return PHJ_OK;
+}
+
+int join_nopart(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
+    SideState& R = c->side[PHJ_SIDE_BUILD];
+    SideState& S = c->side[PHJ_SIDE_PROBE];
+    if (p->hash != PHJ_HASH_XXH3 && p->hash != PHJ_HASH_MURMUR3)
+        return set_err(c, PHJ_ERR_INVALID, "unknown hash function");
+    if (R.n == 0)  // LinearProbing.hpp:295-299
+        return set_err(c, PHJ_ERR_INVALID,
+                       "LinearProbingHashTable::LinearProbingHashTable: numberOfObjects must be greater than zero.");
+    if (R.n >= (1ull << 32)) return set_err(c, PHJ_ERR_RANGE, "build side above 2^32 tuples");
+    const double ratio = p->table_ratio > 0 ? p->table_ratio : kNPDefaultRatio;
+    if (ratio < 1.0) return set_err(c, PHJ_ERR_INVALID, "table_ratio must be >= 1");
+    const double nbd = std::ceil(static_cast<double>(R.n) * ratio / kNPSlots);
+    if (nbd >= 4294967295.0) return set_err(c, PHJ_ERR_RANGE, "table too large");
+    const uint32_t nb = std::max<uint32_t>(1, static_cast<uint32_t>(nbd));
+    PHJ_TRY(ensure(c, c->np_tab, static_cast<size_t>(nb) * sizeof(NPBucket)));
+    PHJ_TRY(ensure(c, c->np_pays, static_cast<size_t>(nb) * kNPSlots * 8));
+    PHJ_TRY(ensure(c, c->count, 8));
+    hipEvent_t e0, e1, e2;
+    const uint32_t nR = static_cast<uint32_t>(R.n);
+    PHJ_TRY(mark(c, &e0));
+    PHJ_TRY(timer_begin(c, "np.build", static_cast<uint64_t>(nR) * 32 + static_cast<uint64_t>(nb) * 64));
+    PHJ_HIP(c, hipMemsetAsync(c->np_tab.p, 0, static_cast<size_t>(nb) * sizeof(NPBucket), c->stream));
+    const uint32_t bg = (nR + kBlock - 1) / kBlock;
+    if (p->hash == PHJ_HASH_MURMUR3)
+        hipLaunchKernelGGL((k_np_build<kMurmur3>), dim3(bg), dim3(kBlock), 0, c->stream,
+                           reinterpret_cast<const longlong2*>(R.rel), nR, static_cast<NPBucket*>(c->np_tab.p),
+                           static_cast<int64_t*>(c->np_pays.p), nb, p->hash_seed);
+    else
+        hipLaunchKernelGGL((k_np_build<kXXH3>), dim3(bg), dim3(kBlock), 0, c->stream,
+                           reinterpret_cast<const longlong2*>(R.rel), nR, static_cast<NPBucket*>(c->np_tab.p),
+                           static_cast<int64_t*>(c->np_pays.p), nb, p->hash_seed);
+    PHJ_LAUNCHED(c, "k_np_build");
+    PHJ_TRY(timer_end(c));
+    PHJ_TRY(mark(c, &e1));
+    PHJ_HIP(c, hipMemsetAsync(c->count.p, 0, 8, c->stream));
+    if (S.n > 0) {
+        const uint64_t per = static_cast<uint64_t>(kBlock) * kNPProbeItems;
+        const uint32_t pg = static_cast<uint32_t>(std::min<uint64_t>((S.n + per - 1) / per, 8192));
+        PHJ_TRY(timer_begin(c, "np.probe", S.n * 16 + static_cast<uint64_t>(nb) * 64));
+        if (p->hash == PHJ_HASH_MURMUR3)
+            hipLaunchKernelGGL((k_np_probe<kMurmur3, kNPProbeItems>), dim3(pg), dim3(kBlock), 0, c->stream,
+                               reinterpret_cast<const longlong2*>(S.rel), S.n,
+                               static_cast<const NPBucket*>(c->np_tab.p), nb, p->hash_seed,
+                               static_cast<unsigned long long*>(c->count.p));
+        else
+            hipLaunchKernelGGL((k_np_probe<kXXH3, kNPProbeItems>), dim3(pg), dim3(kBlock), 0, c->stream,
+                               reinterpret_cast<const longlong2*>(S.rel), S.n,
+                               static_cast<const NPBucket*>(c->np_tab.p), nb, p->hash_seed,
+                               static_cast<unsigned long long*>(c->count.p));
+        PHJ_LAUNCHED(c, "k_np_probe");
+        PHJ_TRY(timer_end(c));
+    }
+    PHJ_TRY(mark(c, &e2));
+    uint64_t m = 0;
+    PHJ_TRY(get_count(c, &m));
+    r->matches = m;
+    r->partition_ms = 0;
+    r->build_ms = elapsed(c, e0, e1);
+    r->probe_ms = elapsed(c, e1, e2);
+    r->total_ms = elapsed(c, e0, e2);
+    r->num_partitions = 0;
+    r->algorithmic_bytes = R.n * 32 + S.n * 16 + static_cast<uint64_t>(nb) * 64;
+    return fill_timers(c, r);
+}
+
+int check_side(phj_ctx* c, int side) {
+    if (!c) return PHJ_ERR_INVALID;
+    (void)hipGetLastError();  // drop a stale error left by code outside this library
+    if (side != PHJ_SIDE_BUILD && side != PHJ_SIDE_PROBE)
+        return set_err(c, PHJ_ERR_INVALID, "side must be PHJ_SIDE_BUILD or PHJ_SIDE_PROBE");
+    return PHJ_OK;
+}
+
+void drop_relation(phj_ctx* c, int side) {
+    SideState& S = c->side[side];
+    S.rel = nullptr;
+    S.n = 0;
+    S.partitioned = false;
+}
+
+uint64_t partition_bytes(const Plan& pl, uint64_t n) {
+    // hist (16 B AoS read) + scatter (16 read + 16 write); pass 2: hist 8 + scatter 32
+    return n * (16 + 32) + (pl.npass == 2 ? n * (8 + 32) : 0);
+}
+
+}  // namespace
+
+extern "C" {
+
+int phj_abi_version(void) { return PHJ_ABI_VERSION; }
+
+int phj_ctx_create(int device, phj_ctx** out) {
+    if (!out) return PHJ_ERR_INVALID;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return PHJ_ERR_HIP;
+    if (device < 0 || device >= ndev) return PHJ_ERR_INVALID;
+    if (hipSetDevice(device) != hipSuccess) return PHJ_ERR_HIP;
+    phj_ctx* c = new phj_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return PHJ_ERR_HIP;
+    }
+    c->own_stream = true;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->max_lds = static_cast<int>(prop.sharedMemPerBlock);
+    // gfx950 launches accept dynamic LDS up to the 160 KiB per workgroup without an
+    // opt-in attribute; clear any error a probe of the runtime left behind
+    (void)hipGetLastError();
+    *out = c;
+    return PHJ_OK;
+}
+
+void phj_ctx_destroy(phj_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    for (SideState& S : c->side) {
+        for (DevBuf* b : {&S.owned, &S.kA, &S.pA, &S.kB, &S.pB, &S.hist1, &S.hist2, &S.bounds1, &S.tbase2, &S.bounds})
+            free_buf(*b);
+    }
+    for (DevBuf* b : {&c->scan_partials, &c->prep, &c->tkeys, &c->tpays, &c->toffs, &c->gcursor, &c->items,
+                      &c->count, &c->np_tab, &c->np_pays})
+        free_buf(*b);
+    for (hipEvent_t e : c->evpool) (void)hipEventDestroy(e);
+    if (c->own_stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char* phj_last_error(const phj_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int phj_ctx_set_stream(phj_ctx* c, void* stream) {
+    if (!c) return PHJ_ERR_INVALID;
+    PHJ_HIP(c, hipSetDevice(c->device));
+    PHJ_HIP(c, hipStreamSynchronize(c->stream));
+    if (c->own_stream) {
+        PHJ_HIP(c, hipStreamDestroy(c->stream));
+        c->own_stream = false;
+    }
+    if (stream) {
+        c->stream = static_cast<hipStream_t>(stream);
+    } else {
+        PHJ_HIP(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        c->own_stream = true;
+    }
+    return PHJ_OK;
+}
+
+int phj_ctx_synchronize(phj_ctx* c) {
+    if (!c) return PHJ_ERR_INVALID;
+    PHJ_HIP(c, hipStreamSynchronize(c->stream));
+    return PHJ_OK;
+}
+
+int phj_relation_upload(phj_ctx* c, int side, const phj_tuple* host, uint64_t n) {
+    PHJ_TRY(check_side(c, side));
+    if (n && !host) return set_err(c, PHJ_ERR_INVALID, "null host relation");
+    PHJ_HIP(c, hipSetDevice(c->device));
+    SideState& S = c->side[side];
+    drop_relation(c, side);
+    PHJ_TRY(ensure(c, S.owned, n * sizeof(phj_tuple)));
+    if (n) {
+        PHJ_HIP(c, hipMemcpyAsync(S.owned.p, host, n * sizeof(phj_tuple), hipMemcpyHostToDevice, c->stream));
+        PHJ_HIP(c, hipStreamSynchronize(c->stream));
+    }
+    S.rel = static_cast<const phj_tuple*>(S.owned.p);
+    S.n = n;
+    return PHJ_OK;
+}
+
+int phj_relation_bind_device(phj_ctx* c, int side, const phj_tuple* dev, uint64_t n) {
+    PHJ_TRY(check_side(c, side));
+    if (n && !dev) return set_err(c, PHJ_ERR_INVALID, "null device relation");
+    if (reinterpret_cast<uintptr_t>(dev) % 16) return set_err(c, PHJ_ERR_INVALID, "relation must be 16-byte aligned");
+    drop_relation(c, side);
+    c->side[side].rel = dev;
+    c->side[side].n = n;
+    return PHJ_OK;
+}
+
+const phj_tuple* phj_relation_device_ptr(phj_ctx* c, int side, uint64_t* n) {
+    if (!c || (side != 0 && side != 1)) return nullptr;
+    if (n) *n = c->side[side].n;
+    return c->side[side].rel;
+}
+
+int phj_relation_download(phj_ctx* c, int side, phj_tuple* host, uint64_t n) {
+    PHJ_TRY(check_side(c, side));
+    SideState& S = c->side[side];
+    if (n > S.n) return set_err(c, PHJ_ERR_INVALID, "download larger than the relation");
+    PHJ_HIP(c, hipSetDevice(c->device));
+    if (n) {
+        PHJ_HIP(c, hipMemcpyAsync(host, S.rel, n * sizeof(phj_tuple), hipMemcpyDeviceToHost, c->stream));
+        PHJ_HIP(c, hipStreamSynchronize(c->stream));
+    }
+    return PHJ_OK;
+}
+
+int phj_relation_generate_sequential(phj_ctx* c, int side, uint64_t n, int64_t start, uint64_t first_index) {
+    PHJ_TRY(check_side(c, side));
+    PHJ_HIP(c, hipSetDevice(c->device));
+    SideState& S = c->side[side];
+    drop_relation(c, side);
+    PHJ_TRY(ensure(c, S.owned, n * sizeof(phj_tuple)));
+    if (n) {
+        const uint32_t g = static_cast<uint32_t>(std::min<uint64_t>((n + kBlock - 1) / kBlock, 65536));
+        hipLaunchKernelGGL(k_gen_sequential, dim3(g), dim3(kBlock), 0, c->stream, static_cast<longlong2*>(S.owned.p), n, start,
+                           first_index);
+        PHJ_LAUNCHED(c, "k_gen_sequential");
+        PHJ_HIP(c, hipStreamSynchronize(c->stream));
+    }
+    S.rel = static_cast<const phj_tuple*>(S.owned.p);
+    S.n = n;
+    return PHJ_OK;
+}
+
+int phj_relation_generate_zipf(phj_ctx* c, int side, uint64_t n, double alpha, int64_t lo, int64_t hi,
+                               uint64_t seed, uint64_t first_index) {
+    PHJ_TRY(check_side(c, side));
+    if (lo >= hi) return set_err(c, PHJ_ERR_INVALID, "Range for Zipf generation is incorrectly specified");
+    if (alpha < 0.01) return set_err(c, PHJ_ERR_INVALID, "Skew parameter must be greater than 0.01.");
+    PHJ_HIP(c, hipSetDevice(c->device));
+    SideState& S = c->side[side];
+    drop_relation(c, side);
+    PHJ_TRY(ensure(c, S.owned, n * sizeof(phj_tuple)));
+    if (n) {
+        const uint64_t b0 = first_index / kGenBatch, b1 = (first_index + n + kGenBatch - 1) / kGenBatch;
+        const uint32_t g = static_cast<uint32_t>((b1 - b0 + kBlock - 1) / kBlock);
+        hipLaunchKernelGGL(k_gen_zipf, dim3(g), dim3(kBlock), 0, c->stream, static_cast<longlong2*>(S.owned.p), n,
+                           alpha, static_cast<uint64_t>(hi - lo + 1), lo - 1, seed, first_index);
+        PHJ_LAUNCHED(c, "k_gen_zipf");
+        PHJ_HIP(c, hipStreamSynchronize(c->stream));
+    }
+    S.rel = static_cast<const phj_tuple*>(S.owned.p);
+    S.n = n;
+    return PHJ_OK;
+}
+
+int phj_relation_count_in_range(phj_ctx* c, int side, int64_t lo, int64_t hi, uint64_t* count) {
+    PHJ_TRY(check_side(c, side));
+    if (!count) return set_err(c, PHJ_ERR_INVALID, "null count");
+    PHJ_HIP(c, hipSetDevice(c->device));
+    SideState& S = c->side[side];
+    PHJ_TRY(ensure(c, c->count, 8));
+    PHJ_HIP(c, hipMemsetAsync(c->count.p, 0, 8, c->stream));
+    if (S.n) {
+        const uint32_t g = static_cast<uint32_t>(std::min<uint64_t>((S.n + kBlock - 1) / kBlock, 8192));
+        hipLaunchKernelGGL(k_count_range, dim3(g), dim3(kBlock), 0, c->stream, reinterpret_cast<const longlong2*>(S.rel),
+                           S.n, lo, hi, static_cast<unsigned long long*>(c->count.p));
+        PHJ_LAUNCHED(c, "k_count_range");
+    }
+    return get_count(c, count);
+}
+
+int phj_partition(phj_ctx* c, int side, const phj_join_params* p, phj_partitioned* out) {
+    PHJ_TRY(check_side(c, side));
+    (void)hipGetLastError();
+    if (p && p->algo != PHJ_ALGO_RADIX) return set_err(c, PHJ_ERR_INVALID, "phj_partition needs PHJ_ALGO_RADIX");
+    Plan pl;
+    PHJ_TRY(make_plan(c, p, pl));
+    PHJ_HIP(c, hipSetDevice(c->device));
+    // timers accumulate until the next phj_join / phj_join_partitioned reports them
+    if (c->timers.size() > PHJ_MAX_TIMERS) reset_timers(c);
+    PHJ_TRY(partition_side(c, side, pl));
+    if (out) *out = c->side[side].view;
+    return PHJ_OK;
+}
+
+int phj_join_partitioned(phj_ctx* c, const phj_join_params* p, int nbuild, const phj_partitioned* build,
+                         phj_join_result* r) {
+    if (!c || !r) return PHJ_ERR_INVALID;
+    if (!build) return set_err(c, PHJ_ERR_INVALID, "null build segments");
+    if (p && p->algo != PHJ_ALGO_RADIX) return set_err(c, PHJ_ERR_INVALID, "phj_join_partitioned needs PHJ_ALGO_RADIX");
+    (void)hipGetLastError();
+    Plan pl;
+    PHJ_TRY(make_plan(c, p, pl));
+    PHJ_HIP(c, hipSetDevice(c->device));
+    std::memset(r, 0, sizeof(*r));
+    hipEvent_t b0, b1, p1;
+    PHJ_TRY(build_and_probe(c, pl, nbuild, build, &b0, &b1, &p1));
+    uint64_t m = 0;
+    PHJ_TRY(get_count(c, &m));
+    r->matches = m;
+    r->build_ms = elapsed(c, b0, b1);
+    r->probe_ms = elapsed(c, b1, p1);
+    r->total_ms = elapsed(c, b0, p1);
+    r->num_partitions = pl.Ppad;
+    uint64_t nR = 0;
+    for (int g = 0; g < nbuild; g++) nR += build[g].n;
+    r->algorithmic_bytes = nR * 32 + c->side[PHJ_SIDE_PROBE].view.n * 8 + nR * 8;
+    const int rc = fill_timers(c, r);  // includes the phj_partition launches since the last report
+    reset_timers(c);
+    return rc;
+}
+
+int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
+    if (!c || !r) return PHJ_ERR_INVALID;
+    (void)hipGetLastError();
+    if (!p) return set_err(c, PHJ_ERR_INVALID, "null params");
+    PHJ_HIP(c, hipSetDevice(c->device));
+    std::memset(r, 0, sizeof(*r));
+    reset_timers(c);
+    if (p->algo == PHJ_ALGO_NO_PARTITIONING) return join_nopart(c, p, r);
+    if (p->algo != PHJ_ALGO_RADIX) return set_err(c, PHJ_ERR_INVALID, "Unrecognized join algorithm");
+    Plan pl;
+    PHJ_TRY(make_plan(c, p, pl));
+    SideState& R = c->side[PHJ_SIDE_BUILD];
+    SideState& S = c->side[PHJ_SIDE_PROBE];
+    hipEvent_t t0, t1, b0, b1, p1;
+    PHJ_TRY(mark(c, &t0));
+    PHJ_TRY(partition_side(c, PHJ_SIDE_BUILD, pl));
+    PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, pl));
+    PHJ_TRY(mark(c, &t1));
+    PHJ_TRY(build_and_probe(c, pl, 1, &R.view, &b0, &b1, &p1));
+    uint64_t m = 0;
+    PHJ_TRY(get_count(c, &m));
+    r->matches = m;
+    r->partition_ms = elapsed(c, t0, t1);
+    r->build_ms = elapsed(c, b0, b1);
+    r->probe_ms = elapsed(c, b1, p1);
+    r->total_ms = elapsed(c, t0, p1);
+    r->num_partitions = pl.Ppad;
+    r->algorithmic_bytes = partition_bytes(pl, R.n) + partition_bytes(pl, S.n) + R.n * 32 + S.n * 8 + R.n * 8;
+    return fill_timers(c, r);
+}
+
+int phj_partitioned_download(phj_ctx* c, const phj_partitioned* v, int64_t* keys, int64_t* payloads,
+                             uint32_t* bounds) {
+    if (!c || !v) return PHJ_ERR_INVALID;
+    PHJ_HIP(c, hipSetDevice(c->device));
+    if (v->n && keys) PHJ_HIP(c, hipMemcpyAsync(keys, v->keys, v->n * 8, hipMemcpyDefault, c->stream));
+    if (v->n && payloads) PHJ_HIP(c, hipMemcpyAsync(payloads, v->payloads, v->n * 8, hipMemcpyDefault, c->stream));
+    if (bounds)
+        PHJ_HIP(c, hipMemcpyAsync(bounds, v->bounds, (static_cast<size_t>(v->num_partitions) + 1) * 4,
+                                  hipMemcpyDefault, c->stream));
+    PHJ_HIP(c, hipStreamSynchronize(c->stream));
+    return PHJ_OK;
+}
+
+int phj_hash_keys(phj_ctx* c, int hash, uint64_t seed, const int64_t* keys, uint64_t n, uint64_t* out) {
+    if (!c) return PHJ_ERR_INVALID;
+    if (hash != PHJ_HASH_XXH3 && hash != PHJ_HASH_MURMUR3) return set_err(c, PHJ_ERR_INVALID, "unknown hash function");
+    if (n == 0) return PHJ_OK;
+    (void)hipGetLastError();
+    PHJ_HIP(c, hipSetDevice(c->device));
+    void *dk = nullptr, *dout = nullptr;
+    PHJ_HIP(c, hipMalloc(&dk, n * 8));
+    hipError_t e = hipMalloc(&dout, n * 8);
+    if (e != hipSuccess) {
+        (void)hipFree(dk);
+        return set_err(c, PHJ_ERR_NOMEM, "hipMalloc failed");
+    }
+    int rc = PHJ_OK;
+    do {
+        if (hipMemcpy(dk, keys, n * 8, hipMemcpyHostToDevice) != hipSuccess) { rc = set_err(c, PHJ_ERR_HIP, "H2D"); break; }
+        const uint32_t g = static_cast<uint32_t>((n + kBlock - 1) / kBlock);
+        if (hash == PHJ_HASH_MURMUR3)
+            hipLaunchKernelGGL((k_hash_keys<kMurmur3>), dim3(g), dim3(kBlock), 0, c->stream, static_cast<int64_t*>(dk), n, seed, static_cast<uint64_t*>(dout));
+        else
+            hipLaunchKernelGGL((k_hash_keys<kXXH3>), dim3(g), dim3(kBlock), 0, c->stream, static_cast<int64_t*>(dk), n, seed, static_cast<uint64_t*>(dout));
+        if (hipGetLastError() != hipSuccess) { rc = set_err(c, PHJ_ERR_HIP, "k_hash_keys launch"); break; }
+        if (hipStreamSynchronize(c->stream) != hipSuccess) { rc = set_err(c, PHJ_ERR_HIP, "sync"); break; }
+        if (hipMemcpy(out, dout, n * 8, hipMemcpyDeviceToHost) != hipSuccess) { rc = set_err(c, PHJ_ERR_HIP, "D2H"); break; }
+    } while (0);
+    (void)hipFree(dk);
+    (void)hipFree(dout);
+    return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,454 @@
+// phj_join.h — build / probe / count kernels for gfx950.
+//
+// Radix path (src/RadixCluster/HashJoin.hpp:243-331, Join()):
+//   k_join_prep + batched scan : per-partition table sizes and probe work items
+//   k_build                    : one workgroup per partition builds a
+//                                bucket-chained table in compacted (CSR) form:
+//                                bucket b of partition p holds the keys
+//                                tkeys[tkb[p] + toffs[tob[p]+b] .. +toffs[..+b+1]).
+//                                LDS counting sort for small partitions, global
+//                                atomics for partitions past the LDS capacity.
+//   k_probe                    : persistent workgroups walk (partition, S-chunk)
+//                                items; a partition's table is staged into LDS
+//                                once per item, every S key probes it and the
+//                                first equal key counts (Get() returns the first
+//                                match, LinearProbing.hpp:160-180).
+// Skew is handled by the item split: a hot partition becomes many S chunks.
+//
+// NoPartitioning path (src/NoPartitioning/HashJoin.hpp:76-187):
+//   k_np_build / k_np_probe    : one global bucketized linear-probing table in
+//                                HBM, 64-B buckets {7 keys, fill count}. As in
+//                                LinearProbing.hpp:22-83 occupancy is a
+//                                per-bucket fill counter (no sentinel key: every
+//                                int64 is a valid key), inserts claim a slot
+//                                with an atomic on the counter and move to the
+//                                next bucket when full, and a lookup stops at
+//                                the first non-full bucket.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "phj_hash.h"
+#include "phj_partition.h"
+
+namespace phj {
+
+constexpr int kMaxSegs = 16;
+
+struct Seg {
+    const int64_t* keys;
+    const int64_t* pays;
+    const uint32_t* bounds;
+};
+
+struct SegList {
+    Seg seg[kMaxSegs];
+    uint32_t nseg;
+    uint32_t P;
+};
+
+__host__ __device__ __forceinline__ uint32_t table_buckets(uint32_t m) {
+    if (m <= 1) return 1u;
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t np2 = 1u << (32 - __clz(m - 1));
+#else
+    uint32_t np2 = 1;
+    while (np2 < m) np2 <<= 1;
+#endif
+    return np2 >> 1;
+}
+
+__device__ __forceinline__ uint32_t bucket_of(uint64_t h, uint32_t nbk) {
+    return static_cast<uint32_t>(h >> 32) & (nbk - 1u);
+}
+
+// arr: 3 arrays of P+1 entries: m_p, NB_p + 1, items_p (last entry 0).
+__global__ __launch_bounds__(kBlock) void k_join_prep(SegList L, const uint32_t* sbounds,
+                                                      uint32_t chunk, uint32_t* arr) {
+    const uint32_t P = L.P;
+    const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+    if (p > P) return;
+    const size_t stride = static_cast<size_t>(P) + 1;
+    if (p == P) {
+        arr[P] = 0;
+        arr[stride + P] = 0;
+        arr[2 * stride + P] = 0;
+        return;
+    }
+    uint32_t m = 0;
+    for (uint32_t g = 0; g < L.nseg; g++) m += L.seg[g].bounds[p + 1] - L.seg[g].bounds[p];
+    const uint32_t s = sbounds[p + 1] - sbounds[p];
+    arr[p] = m;
+    arr[stride + p] = table_buckets(m) + 1;
+    arr[2 * stride + p] = (m && s) ? (s + chunk - 1) / chunk : 0u;
+}
+
+// One wave per partition writes its (partition, chunk) work items.
+__global__ __launch_bounds__(kBlock) void k_items_expand(const uint32_t* itb, uint32_t P,
+                                                         uint2* items) {
+    const uint32_t p = blockIdx.x * kWaves + (threadIdx.x >> 6);
+    if (p >= P) return;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t lo = itb[p], hi = itb[p + 1];
+    for (uint32_t i = lo + lane; i < hi; i += 64) items[i] = make_uint2(p, i - lo);
+}
+
+struct BuildArgs {
+    SegList L;
+    const uint32_t* tkb;   // P+1: table key base (exclusive scan of m_p)
+    const uint32_t* tob;   // P+1: table offset base (exclusive scan of NB_p + 1)
+    int64_t* tkeys;
+    int64_t* tpays;
+    uint32_t* toffs;
+    uint32_t* gcursor;     // global cursors for partitions beyond the LDS capacity
+    uint32_t ocap;         // LDS bucket-counter capacity
+    uint32_t pad;
+    uint64_t seed;
+};
+
+// Block-wide in-place exclusive scan of arr[0..len) (LDS or global via pointer
+// kind); also writes the result to out[0..len) and out[len] = total.
+template <typename LoadF, typename StoreF>
+__device__ __forceinline__ void block_scan_array(uint32_t len, LoadF ld, StoreF st, uint32_t* tmp) {
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < len; base += kBlock) {
+        const uint32_t i = base + threadIdx.x;
+        const uint32_t v = i < len ? ld(i) : 0u;
+        uint32_t total;
+        const uint32_t ex = block_exclusive_scan(v, tmp, total);
+        if (i < len) st(i, carry + ex);
+        carry += total;
+    }
+}
+
+template <int HK>
+__global__ __launch_bounds__(kBlock) void k_build(BuildArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint32_t* tmp = reinterpret_cast<uint32_t*>(smem);        // 16 words
+    uint32_t* lcnt = tmp + 16;                                // ocap words
+    const uint32_t P = a.L.P;
+    for (uint32_t p = blockIdx.x; p < P; p += gridDim.x) {
+        const uint32_t kb = a.tkb[p], m = a.tkb[p + 1] - kb;
+        const uint32_t ob = a.tob[p], nbk = a.tob[p + 1] - ob - 1;
+        uint32_t* offs = a.toffs + ob;
+        if (m == 0) {
+            for (uint32_t i = threadIdx.x; i <= nbk; i += kBlock) offs[i] = 0;
+            continue;
+        }
+        const bool in_lds = (nbk <= a.ocap);
+        uint32_t* cnt = in_lds ? lcnt : (a.gcursor + ob);
+        for (uint32_t i = threadIdx.x; i < nbk; i += kBlock) {
+            if (in_lds) cnt[i] = 0;
+            else __hip_atomic_store(&cnt[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        // count
+        for (uint32_t g = 0; g < a.L.nseg; g++) {
+            const Seg& S = a.L.seg[g];
+            const uint32_t lo = S.bounds[p], c = S.bounds[p + 1] - lo;
+            for (uint32_t i = threadIdx.x; i < c; i += kBlock) {
+                const uint32_t b = bucket_of(hash64<HK>(static_cast<uint64_t>(S.keys[lo + i]), a.seed), nbk);
+                if (in_lds) atomicAdd(&cnt[b], 1u);
+                else __hip_atomic_fetch_add(&cnt[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        __syncthreads();
+        // bucket offsets (exclusive), cursors = offsets
+        if (in_lds) {
+            block_scan_array(
+                nbk, [&](uint32_t i) { return cnt[i]; },
+                [&](uint32_t i, uint32_t v) {
+                    cnt[i] = v;
+                    offs[i] = v;
+                },
+                tmp);
+        } else {
+            block_scan_array(
+                nbk,
+                [&](uint32_t i) {
+                    return __hip_atomic_load(&cnt[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                },
+                [&](uint32_t i, uint32_t v) {
+                    __hip_atomic_store(&cnt[i], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    offs[i] = v;
+                },
+                tmp);
+        }
+        if (threadIdx.x == 0) offs[nbk] = m;
+        __syncthreads();
+        // scatter into bucket order
+        for (uint32_t g = 0; g < a.L.nseg; g++) {
+            const Seg& S = a.L.seg[g];
+            const uint32_t lo = S.bounds[p], c = S.bounds[p + 1] - lo;
+            for (uint32_t i = threadIdx.x; i < c; i += kBlock) {
+                const int64_t key = S.keys[lo + i];
+                const int64_t pay = S.pays[lo + i];
+                const uint32_t b = bucket_of(hash64<HK>(static_cast<uint64_t>(key), a.seed), nbk);
+                uint32_t pos;
+                if (in_lds) pos = atomicAdd(&cnt[b], 1u);
+                else pos = __hip_atomic_fetch_add(&cnt[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                a.tkeys[kb + pos] = key;
+                a.tpays[kb + pos] = pay;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+struct ProbeArgs {
+    const int64_t* skeys;
+    const uint32_t* sbounds;
+    const uint32_t* tkb;
+    const uint32_t* tob;
+    const int64_t* tkeys;
+    const uint32_t* toffs;
+    const uint2* items;
+    const uint32_t* nitems;   // device scalar (itb[P])
+    unsigned long long* count;
+    uint32_t kcap;            // LDS staging capacity: keys
+    uint32_t ocap;            // LDS staging capacity: bucket offsets (NB + 1)
+    uint64_t seed;
+};
+
+template <int HK, int ITEMS, typename KP, typename OP>
+__device__ __forceinline__ uint32_t probe_keys(const int64_t (&k)[ITEMS], uint32_t valid_n,
+                                               KP K, OP O, uint32_t nbk, uint64_t seed) {
+    uint32_t hits = 0;
+#pragma unroll
+    for (int j = 0; j < ITEMS; j++) {
+        if (static_cast<uint32_t>(j * kBlock) + threadIdx.x < valid_n) {
+            const uint64_t h = hash64<HK>(static_cast<uint64_t>(k[j]), seed);
+            const uint32_t b = bucket_of(h, nbk);
+            uint32_t t = O[b];
+            const uint32_t e = O[b + 1];
+            for (; t < e; t++) {
+                if (K[t] == k[j]) {
+                    hits++;
+                    break;
+                }
+            }
+        }
+    }
+    return hits;
+}
+
+template <int HK, int ITEMS>
+__global__ __launch_bounds__(kBlock) void k_probe(ProbeArgs a) {
+    constexpr uint32_t C = kBlock * ITEMS;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    int64_t* lk = reinterpret_cast<int64_t*>(smem);
+    uint32_t* lo = reinterpret_cast<uint32_t*>(lk + a.kcap);
+    __shared__ uint32_t red[kWaves];
+    const uint32_t nitems = *a.nitems;
+    uint32_t hits = 0;
+    for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
+        const uint2 it = a.items[item];
+        const uint32_t p = it.x;
+        const uint32_t kb = a.tkb[p], m = a.tkb[p + 1] - kb;
+        const uint32_t ob = a.tob[p], nbk = a.tob[p + 1] - ob - 1;
+        const uint32_t s_lo = a.sbounds[p] + it.y * C;
+        const uint32_t s_hi = min(a.sbounds[p + 1], s_lo + C);
+        const uint32_t valid_n = s_hi - s_lo;
+        int64_t k[ITEMS];
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const uint32_t off = j * kBlock + threadIdx.x;
+            k[j] = off < valid_n ? a.skeys[s_lo + off] : 0;
+        }
+        if (m <= a.kcap && nbk + 1 <= a.ocap) {
+            for (uint32_t i = threadIdx.x; i < m; i += kBlock) lk[i] = a.tkeys[kb + i];
+            for (uint32_t i = threadIdx.x; i <= nbk; i += kBlock) lo[i] = a.toffs[ob + i];
+            __syncthreads();
+            hits += probe_keys<HK, ITEMS>(k, valid_n, lk, lo, nbk, a.seed);
+            __syncthreads();
+        } else {
+            hits += probe_keys<HK, ITEMS>(k, valid_n, a.tkeys + kb, a.toffs + ob, nbk, a.seed);
+        }
+    }
+    // block reduce -> one atomic per workgroup
+    uint32_t x = hits;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_down(x, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (int w = 0; w < kWaves; w++) t += red[w];
+        if (t) atomicAdd(a.count, t);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// NoPartitioning: global bucketized linear probing.
+// ---------------------------------------------------------------------------
+constexpr int kNPSlots = 7;
+
+struct alignas(64) NPBucket {
+    int64_t key[kNPSlots];
+    uint32_t fill;   // claimed slots; > 7 once full (readers clamp)
+    uint32_t pad;
+};
+
+__device__ __forceinline__ uint32_t np_home(uint64_t h, uint32_t nb) {
+    return static_cast<uint32_t>(((h >> 32) * static_cast<uint64_t>(nb)) >> 32);
+}
+
+template <int HK>
+__global__ __launch_bounds__(kBlock) void k_np_build(const longlong2* R, uint32_t nR,
+                                                     NPBucket* tab, int64_t* pays, uint32_t nb,
+                                                     uint64_t seed) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= nR) return;
+    const longlong2 t = R[i];
+    uint32_t b = np_home(hash64<HK>(static_cast<uint64_t>(t.x), seed), nb);
+    for (uint32_t step = 0; step < nb; step++) {
+        const uint32_t slot = atomicAdd(&tab[b].fill, 1u);
+        if (slot < kNPSlots) {
+            tab[b].key[slot] = t.x;
+            pays[static_cast<size_t>(b) * kNPSlots + slot] = t.y;
+            return;
+        }
+        b = (b + 1 == nb) ? 0 : b + 1;
+    }
+}
+
+template <int HK, int ITEMS>
+__global__ __launch_bounds__(kBlock) void k_np_probe(const longlong2* S, uint64_t nS,
+                                                     const NPBucket* tab, uint32_t nb,
+                                                     uint64_t seed, unsigned long long* count) {
+    __shared__ uint32_t red[kWaves];
+    uint32_t hits = 0;
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kBlock * ITEMS;
+    for (uint64_t base = static_cast<uint64_t>(blockIdx.x) * kBlock * ITEMS; base < nS; base += stride) {
+        int64_t k[ITEMS];
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const uint64_t idx = base + static_cast<uint64_t>(j) * kBlock + threadIdx.x;
+            k[j] = idx < nS ? S[idx].x : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const uint64_t idx = base + static_cast<uint64_t>(j) * kBlock + threadIdx.x;
+            if (idx < nS) {
+                const int64_t key = k[j];
+                uint32_t b = np_home(hash64<HK>(static_cast<uint64_t>(key), seed), nb);
+                for (uint32_t step = 0; step < nb; step++) {
+                    const longlong2* bp = reinterpret_cast<const longlong2*>(tab + b);
+                    const longlong2 q0 = bp[0], q1 = bp[1], q2 = bp[2], q3 = bp[3];
+                    const uint32_t fill = static_cast<uint32_t>(q3.y);
+                    const uint32_t c = fill < kNPSlots ? fill : kNPSlots;
+                    const bool hit = (c > 0 && q0.x == key) || (c > 1 && q0.y == key) ||
+                                     (c > 2 && q1.x == key) || (c > 3 && q1.y == key) ||
+                                     (c > 4 && q2.x == key) || (c > 5 && q2.y == key) ||
+                                     (c > 6 && q3.x == key);
+                    if (hit) {
+                        hits++;
+                        break;
+                    }
+                    if (fill < kNPSlots) break;
+                    b = (b + 1 == nb) ? 0 : b + 1;
+                }
+            }
+        }
+    }
+    uint32_t x = hits;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_down(x, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (int w = 0; w < kWaves; w++) t += red[w];
+        if (t) atomicAdd(count, t);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Generators and utilities.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kGenBatch = 4096;
+
+// Rows [first, first + n) of Sequential::FillTable: id = start + i, payload = i (global i).
+__global__ __launch_bounds__(kBlock) void k_gen_sequential(longlong2* out, uint64_t n, int64_t start,
+                                                           uint64_t first) {
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kBlock;
+    for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) {
+        const int64_t g = static_cast<int64_t>(first + i);
+        out[i] = make_longlong2(start + g, g);
+    }
+}
+
+__device__ __forceinline__ double lcg_next(int64_t& st) {
+    const int64_t a = 16807, q = 127773, r = 2836, m = 2147483647LL;
+    const int64_t xn = a * (st % q) - r * (st / q);
+    st = xn > 0 ? xn : xn + m;
+    return static_cast<double>(st) / static_cast<double>(m);
+}
+
+// Thread per 4096-tuple batch; Zipf::generate (Zipf.cpp:14-56) per sample.
+// Writes global rows [first, first + n) to out[0, n).
+__global__ __launch_bounds__(kBlock) void k_gen_zipf(longlong2* out, uint64_t n, double alpha,
+                                                     uint64_t card, int64_t correction,
+                                                     uint64_t seed, uint64_t first) {
+    const uint64_t b = first / kGenBatch + static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    const uint64_t lo = b * kGenBatch;
+    const uint64_t end = first + n;
+    if (lo >= end) return;
+    const uint64_t hi = lo + kGenBatch < end ? lo + kGenBatch : end;
+    const uint64_t M = 2147483646ULL;
+    int64_t st = static_cast<int64_t>(1 + (((seed % M) * 1000003ULL + b) % M));
+    double skew = 1.001 - alpha;
+    const double diff = 1.0 - alpha;
+    if (fabs(diff) < 0.01) {
+        skew = 0.01 * ((diff < 0) ? 1 : -1);
+        alpha = 1.0 - skew;
+    }
+    const double norm = (pow(static_cast<double>(card), skew) - alpha) / skew;
+    for (uint64_t i = lo; i < hi; i++) {
+        double sample;
+        for (;;) {
+            const double u1 = lcg_next(st);
+            const double u2 = lcg_next(st);
+            double inv;
+            if (u1 * norm <= 1.0) inv = u1 * norm;
+            else inv = pow((u1 * norm) * skew + alpha, 1.0 / skew);
+            sample = floor(inv + 1);
+            const double d_orig = pow(sample, -alpha);
+            const double d_samp = sample <= 1.0 ? 1.0 / norm : pow(inv, -alpha) / norm;
+            if (u2 < d_orig / (d_samp * norm)) break;
+        }
+        if (i >= first)
+            out[i - first] = make_longlong2(static_cast<int64_t>(static_cast<uint64_t>(sample)) + correction,
+                                            static_cast<int64_t>(i));
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_count_range(const longlong2* rel, uint64_t n, int64_t lo,
+                                                        int64_t hi, unsigned long long* count) {
+    __shared__ uint32_t red[kWaves];
+    uint32_t c = 0;
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kBlock;
+    for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) {
+        const int64_t k = rel[i].x;
+        c += (k >= lo && k <= hi) ? 1u : 0u;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (int w = 0; w < kWaves; w++) t += red[w];
+        if (t) atomicAdd(count, t);
+    }
+}
+
+template <int HK>
+__global__ __launch_bounds__(kBlock) void k_hash_keys(const int64_t* keys, uint64_t n, uint64_t seed,
+                                                      uint64_t* out) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (i < n) out[i] = hash64<HK>(static_cast<uint64_t>(keys[i]), seed);
+}
+
+}  // namespace phj

@@ -1,0 +1,462 @@
+// phj_partition.h — radix partition pass kernels for gfx950.
+//
+// One pass = histogram -> flat exclusive scan -> scatter, per tile of
+// T = 256 * ITEMS tuples. This restates, for the GPU, the reference's
+// Partition() pipeline (src/RadixCluster/HashJoin.hpp:333-440): scanTable
+// (per-worker histogram, :343-357), createPrefixSumTable (exclusive scan
+// across workers, :360-390) and partitionTable (stable scatter, :394-412),
+// with "worker" = tile. The output is a STABLE partition: partition-major,
+// then tile order, then input order inside the tile — the reference's layout.
+//
+// Segmented passes (pass 2 of a 2-pass radix) partition every pass-1
+// partition ("segment") independently: tiles never straddle a segment, and
+// the histogram is laid out [segment][digit][tile-in-segment] so one flat
+// exclusive scan yields every tile's output offset per digit directly.
+//
+// Memory shape: input tuples are read once per kernel with 16-B (AoS) or 8-B
+// (SoA) per-lane coalesced loads; the scatter sorts the tile locally in LDS
+// (wave-level match ranking, stable) and then writes key and payload
+// columns with consecutive lanes on consecutive output slots of a digit run.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "phj_hash.h"
+
+namespace phj {
+
+constexpr int kBlock = 256;   // 4 waves of 64
+constexpr int kWaves = kBlock / 64;
+constexpr int kMaxDigitBits = 11;
+constexpr int kMaxBins = 1 << kMaxDigitBits;
+
+// q(key) -> this pass's digit. mode 0: q = h & (P - 1); mode 1: q = h % P
+// (Barrett: magic = floor((2^64 - 1) / P), one correction step).
+struct DigitFn {
+    uint64_t seed;
+    uint64_t P;
+    uint64_t magic;
+    uint32_t mode;
+    uint32_t shift;
+    uint32_t dmask;
+    uint32_t pad;
+};
+
+template <int HK>
+__device__ __forceinline__ uint64_t partition_q(uint64_t key, const DigitFn& f) {
+    const uint64_t h = hash64<HK>(key, f.seed);
+    if (f.mode == 0) return h & (f.P - 1);
+    const uint64_t qt = __umul64hi(h, f.magic);
+    uint64_t r = h - qt * f.P;
+    if (r >= f.P) r -= f.P;
+    return r;
+}
+
+template <int HK>
+__device__ __forceinline__ uint32_t digit_of(uint64_t key, const DigitFn& f) {
+    return static_cast<uint32_t>(partition_q<HK>(key, f) >> f.shift) & f.dmask;
+}
+
+struct PassArgs {
+    const int64_t* in_keys;     // AoS: tuple base ({id,payload} pairs); SoA: key column
+    const int64_t* in_pays;     // SoA payload column (unused for AoS)
+    int64_t* out_keys;
+    int64_t* out_pays;
+    uint32_t* hist;             // [seg][digit][tile]; scanned in place between the kernels
+    const uint32_t* seg_bounds; // nseg+1 input offsets; nullptr = one segment [0, n)
+    const uint32_t* tile_base;  // nseg+1 cumulative tile counts (segmented passes)
+    uint32_t nseg;
+    uint32_t n;
+    uint32_t ntiles1;           // tiles of the single-segment case
+    uint32_t nbins;
+    uint32_t nbits;
+    uint32_t pad;
+    DigitFn f;
+};
+
+struct TileLoc {
+    uint32_t tseg, ntiles_s, tb_s, lo, hi;
+};
+
+template <int T>
+__device__ __forceinline__ bool locate_tile(const PassArgs& a, uint32_t tile, TileLoc& L) {
+    if (a.seg_bounds == nullptr) {
+        if (tile >= a.ntiles1) return false;
+        L.tseg = tile;
+        L.ntiles_s = a.ntiles1;
+        L.tb_s = 0;
+        L.lo = tile * T;
+        L.hi = min(a.n, L.lo + T);
+        return true;
+    }
+    const uint32_t total = a.tile_base[a.nseg];
+    if (tile >= total) return false;
+    uint32_t l = 0, r = a.nseg;  // tile_base[l] <= tile < tile_base[r]
+    while (r - l > 1) {
+        const uint32_t m = (l + r) >> 1;
+        if (a.tile_base[m] <= tile) l = m;
+        else r = m;
+    }
+    L.tb_s = a.tile_base[l];
+    L.tseg = tile - L.tb_s;
+    L.ntiles_s = a.tile_base[l + 1] - L.tb_s;
+    L.lo = a.seg_bounds[l] + L.tseg * T;
+    L.hi = min(a.seg_bounds[l + 1], L.lo + T);
+    return true;
+}
+
+__device__ __forceinline__ uint64_t lanemask_lt() {
+    const uint32_t lane = threadIdx.x & 63;
+    return (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
+}
+
+// Lanes of this wave holding the same digit (valid lanes only).
+__device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid, uint32_t nbits) {
+    uint64_t m = __ballot(valid);
+    for (uint32_t b = 0; b < nbits; b++) {
+        const bool bit = (d >> b) & 1u;
+        const uint64_t bb = __ballot(bit);
+        m &= bit ? bb : ~bb;
+    }
+    return m;
+}
+
+// Exclusive scan of one value per thread across the 256-thread block.
+__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* tmp,
+                                                         uint32_t& total) {
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) tmp[wave] = x;
+    __syncthreads();
+    uint32_t before = 0, all = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; w++) {
+        const uint32_t s = tmp[w];
+        if (w < (int)wave) before += s;
+        all += s;
+    }
+    __syncthreads();
+    total = all;
+    return before + x - v;
+}
+
+template <bool AOS>
+__device__ __forceinline__ void load_tuple(const PassArgs& a, uint32_t idx, int64_t& k, int64_t& p) {
+    if constexpr (AOS) {
+        const longlong2 t = reinterpret_cast<const longlong2*>(a.in_keys)[idx];
+        k = t.x;
+        p = t.y;
+    } else {
+        k = a.in_keys[idx];
+        p = a.in_pays[idx];
+    }
+}
+
+// Per-tile digit histogram -> hist[(tb_s * nbins) + d * ntiles_s + tseg].
+template <int ITEMS, bool AOS, int HK>
+__global__ __launch_bounds__(kBlock) void k_hist(PassArgs a) {
+    constexpr int T = kBlock * ITEMS;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint32_t* wcnt = reinterpret_cast<uint32_t*>(smem);  // [kWaves][nbins]
+    TileLoc L;
+    if (!locate_tile<T>(a, blockIdx.x, L)) return;
+    const uint32_t nb = a.nbins;
+    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    for (uint32_t i = tid; i < kWaves * nb; i += kBlock) wcnt[i] = 0;
+    const uint32_t cnt = L.hi - L.lo;
+    int64_t key[ITEMS];
+    const uint32_t wbase = wave * 64 * ITEMS;
+#pragma unroll
+    for (int i = 0; i < ITEMS; i++) {
+        const uint32_t e = wbase + i * 64 + lane;
+        key[i] = 0;
+        if (e < cnt) {
+            if constexpr (AOS) {
+                key[i] = reinterpret_cast<const longlong2*>(a.in_keys)[L.lo + e].x;
+            } else {
+                key[i] = a.in_keys[L.lo + e];
+            }
+        }
+    }
+    __syncthreads();
+    uint32_t* my = wcnt + wave * nb;
+#pragma unroll
+    for (int i = 0; i < ITEMS; i++) {
+        const uint32_t e = wbase + i * 64 + lane;
+        const bool valid = e < cnt;
+        const uint32_t d = valid ? digit_of<HK>(static_cast<uint64_t>(key[i]), a.f) : 0u;
+        const uint64_t peers = match_digit(d, valid, a.nbits);
+        if (valid && (peers & lanemask_lt()) == 0) my[d] += __popcll(peers);
+    }
+    __syncthreads();
+    uint32_t* out = a.hist + static_cast<size_t>(L.tb_s) * nb + L.tseg;
+    for (uint32_t d = tid; d < nb; d += kBlock) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; w++) c += wcnt[w * nb + d];
+        out[static_cast<size_t>(d) * L.ntiles_s] = c;
+    }
+}
+
+// LDS bytes of k_scatter for a tile of T tuples and nb digits.
+__host__ __device__ constexpr size_t scatter_lds_bytes(int T, uint32_t nb) {
+    return static_cast<size_t>(T) * 18 + static_cast<size_t>(nb) * 4 * (kWaves + 2) + 64;
+}
+
+// Stable scatter of one tile using the scanned offsets.
+template <int ITEMS, bool AOS, int HK>
+__global__ __launch_bounds__(kBlock) void k_scatter(PassArgs a) {
+    constexpr int T = kBlock * ITEMS;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t nb = a.nbins;
+    int64_t* skey = reinterpret_cast<int64_t*>(smem);
+    int64_t* spay = skey + T;
+    uint32_t* wcnt = reinterpret_cast<uint32_t*>(spay + T);  // [kWaves][nb]
+    uint32_t* gofs = wcnt + kWaves * nb;
+    uint32_t* dstart = gofs + nb;
+    uint32_t* tmp = dstart + nb;                              // 16 words
+    uint16_t* sdig = reinterpret_cast<uint16_t*>(tmp + 16);   // [T]
+
+    TileLoc L;
+    if (!locate_tile<T>(a, blockIdx.x, L)) return;
+    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const uint32_t cnt = L.hi - L.lo;
+    for (uint32_t i = tid; i < kWaves * nb; i += kBlock) wcnt[i] = 0;
+    {
+        const uint32_t* h = a.hist + static_cast<size_t>(L.tb_s) * nb + L.tseg;
+        for (uint32_t d = tid; d < nb; d += kBlock) gofs[d] = h[static_cast<size_t>(d) * L.ntiles_s];
+    }
+    int64_t key[ITEMS], pay[ITEMS];
+    uint32_t dig[ITEMS], rank[ITEMS];
+    const uint32_t wbase = wave * 64 * ITEMS;
+#pragma unroll
+    for (int i = 0; i < ITEMS; i++) {
+        const uint32_t e = wbase + i * 64 + lane;
+        key[i] = 0;
+        pay[i] = 0;
+        if (e < cnt) load_tuple<AOS>(a, L.lo + e, key[i], pay[i]);
+    }
+    __syncthreads();
+    // stable ranking: wave-major, then round i, then lane
+    uint32_t* my = wcnt + wave * nb;
+#pragma unroll
+    for (int i = 0; i < ITEMS; i++) {
+        const uint32_t e = wbase + i * 64 + lane;
+        const bool valid = e < cnt;
+        const uint32_t d = valid ? digit_of<HK>(static_cast<uint64_t>(key[i]), a.f) : 0u;
+        const uint64_t peers = match_digit(d, valid, a.nbits);
+        dig[i] = d;
+        rank[i] = 0;
+        if (valid) {
+            const uint32_t before = my[d];
+            const uint64_t lt = peers & lanemask_lt();
+            rank[i] = before + __popcll(lt);
+            if (lt == 0) my[d] = before + __popcll(peers);
+        }
+    }
+    __syncthreads();
+    // digit totals -> tile-local digit starts and per-wave starts
+    {
+        const uint32_t dpt = (nb + kBlock - 1) / kBlock;
+        const uint32_t d0 = tid * dpt;
+        uint32_t local = 0;
+        for (uint32_t j = 0; j < dpt; j++) {
+            const uint32_t d = d0 + j;
+            if (d < nb) {
+#pragma unroll
+                for (int w = 0; w < kWaves; w++) local += wcnt[w * nb + d];
+            }
+        }
+        uint32_t total;
+        uint32_t run = block_exclusive_scan(local, tmp, total);
+        for (uint32_t j = 0; j < dpt; j++) {
+            const uint32_t d = d0 + j;
+            if (d < nb) {
+                dstart[d] = run;
+#pragma unroll
+                for (int w = 0; w < kWaves; w++) {
+                    const uint32_t c = wcnt[w * nb + d];
+                    wcnt[w * nb + d] = run;
+                    run += c;
+                }
+            }
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < ITEMS; i++) {
+        const uint32_t e = wbase + i * 64 + lane;
+        if (e < cnt) {
+            const uint32_t pos = my[dig[i]] + rank[i];
+            skey[pos] = key[i];
+            spay[pos] = pay[i];
+            sdig[pos] = static_cast<uint16_t>(dig[i]);
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < ITEMS; i++) {
+        const uint32_t k = i * kBlock + tid;
+        if (k < cnt) {
+            const uint32_t d = sdig[k];
+            const uint32_t o = gofs[d] + (k - dstart[d]);
+            a.out_keys[o] = skey[k];
+            a.out_pays[o] = spay[k];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Flat exclusive scan of uint32 arrays (batched: blockIdx.y selects array).
+// ---------------------------------------------------------------------------
+constexpr int kScanItems = 16;
+constexpr int kScanBlockElems = kBlock * kScanItems;  // 4096
+
+struct ScanArgs {
+    uint32_t* data;       // narrays arrays at stride `stride`
+    uint32_t* partials;   // narrays * nblk
+    uint32_t len;
+    uint32_t stride;
+    uint32_t nblk;
+    uint32_t pad;
+};
+
+__global__ __launch_bounds__(kBlock) void k_scan_reduce(ScanArgs s) {
+    __shared__ uint32_t tmp[16];
+    const uint32_t* d = s.data + static_cast<size_t>(blockIdx.y) * s.stride;
+    const uint32_t base = blockIdx.x * kScanBlockElems;
+    uint32_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < kScanItems; i++) {
+        const uint32_t idx = base + i * kBlock + threadIdx.x;
+        if (idx < s.len) acc += d[idx];
+    }
+    uint32_t total;
+    block_exclusive_scan(acc, tmp, total);
+    if (threadIdx.x == 0) s.partials[blockIdx.y * s.nblk + blockIdx.x] = total;
+}
+
+// One block per array: exclusive scan of the block partials.
+__global__ __launch_bounds__(1024) void k_scan_partials(ScanArgs s) {
+    __shared__ uint32_t wsum[16];
+    __shared__ uint32_t carry;
+    uint32_t* p = s.partials + blockIdx.y * s.nblk;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid == 0) carry = 0;
+    __syncthreads();
+    for (uint32_t base = 0; base < s.nblk; base += 1024) {
+        const uint32_t idx = base + tid;
+        const uint32_t v = idx < s.nblk ? p[idx] : 0u;
+        uint32_t x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= (uint32_t)o) x += y;
+        }
+        if (lane == 63) wsum[wave] = x;
+        __syncthreads();
+        uint32_t before = 0, all = 0;
+        for (int w = 0; w < 16; w++) {
+            const uint32_t t = wsum[w];
+            if (w < (int)wave) before += t;
+            all += t;
+        }
+        const uint32_t c = carry;
+        if (idx < s.nblk) p[idx] = c + before + x - v;
+        __syncthreads();
+        if (tid == 0) carry = c + all;
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_scan_apply(ScanArgs s) {
+    __shared__ uint32_t tmp[16];
+    uint32_t* d = s.data + static_cast<size_t>(blockIdx.y) * s.stride;
+    const uint32_t base = blockIdx.x * kScanBlockElems + threadIdx.x * kScanItems;
+    uint32_t v[kScanItems];
+    uint32_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < kScanItems; i++) {
+        const uint32_t idx = base + i;
+        v[i] = idx < s.len ? d[idx] : 0u;
+        acc += v[i];
+    }
+    uint32_t total;
+    uint32_t run = block_exclusive_scan(acc, tmp, total) + s.partials[blockIdx.y * s.nblk + blockIdx.x];
+#pragma unroll
+    for (int i = 0; i < kScanItems; i++) {
+        const uint32_t idx = base + i;
+        if (idx < s.len) d[idx] = run;
+        run += v[i];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Pass bookkeeping.
+// ---------------------------------------------------------------------------
+// After pass 1 (single segment): bounds1[d] for d <= nb1 and, for a second
+// pass, the per-segment cumulative tile counts.
+__global__ __launch_bounds__(1024) void k_pass1_finish(const uint32_t* hist, uint32_t ntiles,
+                                                       uint32_t nb, uint32_t n, uint32_t T,
+                                                       uint32_t* bounds1, uint32_t* tile_base2) {
+    __shared__ uint32_t wsum[16];
+    __shared__ uint32_t carry;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (uint32_t d = tid; d < nb; d += 1024) bounds1[d] = ntiles ? hist[static_cast<size_t>(d) * ntiles] : 0u;
+    if (tid == 0) {
+        bounds1[nb] = n;
+        carry = 0;
+    }
+    __syncthreads();
+    if (tile_base2 == nullptr) return;
+    for (uint32_t base = 0; base < nb; base += 1024) {
+        const uint32_t d = base + tid;
+        const uint32_t v = d < nb ? (bounds1[d + 1] - bounds1[d] + T - 1) / T : 0u;
+        uint32_t x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= (uint32_t)o) x += y;
+        }
+        if (lane == 63) wsum[wave] = x;
+        __syncthreads();
+        uint32_t before = 0, all = 0;
+        for (int w = 0; w < 16; w++) {
+            const uint32_t t = wsum[w];
+            if (w < (int)wave) before += t;
+            all += t;
+        }
+        const uint32_t c = carry;
+        if (d < nb) tile_base2[d] = c + before + x - v;
+        __syncthreads();
+        if (tid == 0) carry = c + all;
+        __syncthreads();
+    }
+    if (tid == 0) tile_base2[nb] = carry;
+}
+
+// Final bounds after a segmented pass 2: bounds[s * nb2 + d].
+__global__ __launch_bounds__(kBlock) void k_pass2_bounds(const uint32_t* hist2,
+                                                         const uint32_t* tile_base2,
+                                                         const uint32_t* bounds1, uint32_t nb1,
+                                                         uint32_t nb2, uint32_t n,
+                                                         uint32_t* bounds) {
+    const uint32_t P = nb1 * nb2;
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i > P) return;
+    if (i == P) {
+        bounds[P] = n;
+        return;
+    }
+    const uint32_t s = i / nb2, d = i - s * nb2;
+    const uint32_t tb = tile_base2[s], nt = tile_base2[s + 1] - tb;
+    bounds[i] = nt ? hist2[static_cast<size_t>(tb) * nb2 + static_cast<size_t>(d) * nt] : bounds1[s];
+}
+
+}  // namespace phj

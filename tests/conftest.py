@@ -1,0 +1,38 @@
+"""Test configuration.
+
+`-m "not gpu"` runs here (no GPU): oracle vs golden vectors, host logic, the C
+ABI library's exports, the C++ host driver and the multi-rank orchestration
+over gloo. `-m gpu` runs on an MI355X and checks the HIP path against the
+oracle through the C ABI.
+"""
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP kernels)")
+
+
+def _gpu_available():
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+@pytest.fixture(scope="session")
+def ctx():
+    """One HIP context for the whole GPU session (one process on the card)."""
+    if not _gpu_available():
+        pytest.fail("GPU test selected but no GPU is visible")
+    import partitionedhashjoin_amd as phj
+    c = phj.Context(0)
+    yield c
+    c.close()
