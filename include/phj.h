@@ -151,6 +151,9 @@ int phj_partition(phj_ctx *ctx, int side, const phj_join_params *p, phj_partitio
  * params must precede). Synchronous; fills r (build_ms, probe_ms, matches). */
 int phj_join_partitioned(phj_ctx *ctx, const phj_join_params *p, int nbuild,
                          const phj_partitioned *build, phj_join_result *r);
+/* Per-kernel device timers recorded since the last report (e.g. after
+ * phj_partition calls); synchronizes the ctx stream, then resets. */
+int phj_timers_report(phj_ctx *ctx, phj_join_result *r);
 /* Copy a partitioned view (keys, payloads: n; bounds: P+1) to host or device
  * buffers (any may be NULL). Synchronous. */
 int phj_partitioned_download(phj_ctx *ctx, const phj_partitioned *v, int64_t *keys,

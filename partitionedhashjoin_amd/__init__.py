@@ -142,6 +142,11 @@ class Context:
                                                  C.byref(r)))
         return r
 
+    def timers_report(self) -> JoinResult:
+        r = JoinResult()
+        self._check(self._L.phj_timers_report(self._h, C.byref(r)))
+        return r
+
     def download_partitioned(self, v: Partitioned):
         keys = np.zeros(v.n, dtype=np.int64)
         pays = np.zeros(v.n, dtype=np.int64)

@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -20,13 +21,12 @@
 #include "../../include/phj.h"
 #include "phj_join.h"
 #include "phj_partition.h"
+#include "phj_partition_wc.h"
 
 using namespace phj;
 
 namespace {
 
-constexpr int kPartItems = 8;                       // tuples per thread in a partition tile
-constexpr uint32_t kTile = kBlock * kPartItems;     // 2048 tuples per tile
 constexpr int kProbeItems = 16;                     // S keys per thread per probe item
 constexpr uint32_t kChunk = kBlock * kProbeItems;   // 4096 S tuples per probe item
 constexpr int kNPProbeItems = 4;
@@ -36,6 +36,23 @@ struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
 };
+
+// Launch-shape knobs (results never depend on them). Defaults are the tuned
+// values; PHJ_TILE_ITEMS / PHJ_P1_AOS / PHJ_XCD_REMAP override them for sweeps.
+struct Tuning {
+    int tile = 4096;      // tile kernels: tuples per tile (2048, 4096 or 8192)
+    bool p1_aos = false;  // tile kernels, 2-pass: pass-1 output as 16-B tuples
+    bool xcd_remap = true;
+    bool wc = false;      // write-combining super-tile kernels (slower on MI355X: DESIGN.md)
+    int wc_items = 8;     // WC sub-tile = 256 * wc_items tuples (4 or 8)
+    int wc_lw = 8;        // WC line: elements per column (8 = 64 B, 16 = 128 B)
+    int wc_wgs = 1024;    // target workgroups per WC pass (super-tile size follows)
+};
+
+int env_int(const char* name, int dflt) {
+    const char* v = std::getenv(name);
+    return (v && *v) ? std::atoi(v) : dflt;
+}
 
 struct Plan {
     int hk = 0;
@@ -96,7 +113,7 @@ struct phj_ctx {
     size_t evnext = 0;
     std::vector<TimerRec> timers;
     std::string err;
-    int max_lds = 65536;
+    Tuning tune;
 };
 
 namespace {
@@ -289,20 +306,21 @@ int scan_u32(phj_ctx* c, uint32_t* data, uint32_t len, uint32_t narrays, uint32_
     return PHJ_OK;
 }
 
-template <bool AOS>
-int launch_pass(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const std::string& prefix,
-                uint64_t n, uint32_t hist_len) {
-    if (grid == 0) return PHJ_OK;
-    const size_t hist_lds = static_cast<size_t>(kWaves) * a.nbins * 4;
-    const size_t sc_lds = scatter_lds_bytes(kTile, a.nbins);
+template <int BLOCK, int ITEMS, bool IN_AOS, bool OUT_AOS>
+int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const std::string& prefix,
+                  uint64_t n, uint32_t hist_len) {
+    constexpr int T = BLOCK * ITEMS;
+    constexpr int NW = BLOCK / 64;
+    const size_t hist_lds = static_cast<size_t>(NW) * a.nbins * 4;
+    const size_t sc_lds = scatter_lds_bytes(T, a.nbins, NW);
     const std::string hname = prefix + ".hist", cname = prefix + ".scan", sname = prefix + ".scatter";
     // algorithmic bytes: the histogram reads the key (a whole 16-B tuple when AoS);
     // the scatter reads and writes every tuple once (16 + 16 B)
-    PHJ_TRY(timer_begin(c, hname.c_str(), n * (AOS ? 16 : 8)));
+    PHJ_TRY(timer_begin(c, hname.c_str(), n * (IN_AOS ? 16 : 8)));
     if (hk == kMurmur3)
-        hipLaunchKernelGGL((k_hist<kPartItems, AOS, kMurmur3>), dim3(grid), dim3(kBlock), hist_lds, c->stream, a);
+        hipLaunchKernelGGL((k_hist<BLOCK, ITEMS, IN_AOS, kMurmur3>), dim3(grid), dim3(BLOCK), hist_lds, c->stream, a);
     else
-        hipLaunchKernelGGL((k_hist<kPartItems, AOS, kXXH3>), dim3(grid), dim3(kBlock), hist_lds, c->stream, a);
+        hipLaunchKernelGGL((k_hist<BLOCK, ITEMS, IN_AOS, kXXH3>), dim3(grid), dim3(BLOCK), hist_lds, c->stream, a);
     PHJ_LAUNCHED(c, hname);
     PHJ_TRY(timer_end(c));
     PHJ_TRY(timer_begin(c, cname.c_str(), static_cast<uint64_t>(hist_len) * 12));
@@ -310,32 +328,127 @@ int launch_pass(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const std:
     PHJ_TRY(timer_end(c));
     PHJ_TRY(timer_begin(c, sname.c_str(), n * 32));
     if (hk == kMurmur3)
-        hipLaunchKernelGGL((k_scatter<kPartItems, AOS, kMurmur3>), dim3(grid), dim3(kBlock), sc_lds, c->stream, a);
+        hipLaunchKernelGGL((k_scatter<BLOCK, ITEMS, IN_AOS, OUT_AOS, kMurmur3>), dim3(grid), dim3(BLOCK), sc_lds, c->stream, a);
     else
-        hipLaunchKernelGGL((k_scatter<kPartItems, AOS, kXXH3>), dim3(grid), dim3(kBlock), sc_lds, c->stream, a);
+        hipLaunchKernelGGL((k_scatter<BLOCK, ITEMS, IN_AOS, OUT_AOS, kXXH3>), dim3(grid), dim3(BLOCK), sc_lds, c->stream, a);
     PHJ_LAUNCHED(c, sname);
     PHJ_TRY(timer_end(c));
     return PHJ_OK;
+}
+
+// One partition pass over `ntiles` tiles (an upper bound for segmented passes).
+int launch_pass(phj_ctx* c, int hk, bool in_aos, bool out_aos, PassArgs a, uint32_t ntiles,
+                const std::string& prefix, uint64_t n, uint32_t hist_len) {
+    if (ntiles == 0) return PHJ_OK;
+    uint32_t grid = ntiles;
+    a.xcd_remap = 0;
+    if (c->tune.xcd_remap) {
+        grid = (ntiles + 7) & ~7u;
+        a.xcd_remap = 1;
+    }
+    int tile = c->tune.tile;
+    if (tile == 8192 && scatter_lds_bytes(8192, a.nbins, 8) > 160 * 1024) tile = 4096;
+    const int io = (in_aos ? 2 : 0) + (out_aos ? 1 : 0);
+#define PHJ_PASS_CASES(B, I)                                                        \
+    switch (io) {                                                                   \
+        case 0: return launch_pass_t<B, I, false, false>(c, hk, a, grid, prefix, n, hist_len); \
+        case 2: return launch_pass_t<B, I, true, false>(c, hk, a, grid, prefix, n, hist_len);  \
+        case 3: return launch_pass_t<B, I, true, true>(c, hk, a, grid, prefix, n, hist_len);   \
+        default: return set_err(c, PHJ_ERR_INVALID, "unsupported pass layout");     \
+    }
+    if (tile == 2048) PHJ_PASS_CASES(256, 8)
+    if (tile == 8192) PHJ_PASS_CASES(512, 16)
+    PHJ_PASS_CASES(256, 16)
+#undef PHJ_PASS_CASES
+}
+
+template <int ITEMS, bool IN_AOS, int LW>
+int launch_pass_wc_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, uint32_t tsz,
+                     const std::string& prefix, uint64_t n, uint32_t hist_len) {
+    const size_t hist_lds = static_cast<size_t>(kWaves) * a.nbins * 4;
+    const size_t sc_lds = scatter_wc_lds_bytes(kBlock * ITEMS, LW);
+    const std::string hname = prefix + ".hist", cname = prefix + ".scan", sname = prefix + ".scatter";
+    PHJ_TRY(timer_begin(c, hname.c_str(), n * (IN_AOS ? 16 : 8)));
+    if (hk == kMurmur3)
+        hipLaunchKernelGGL((k_hist_super<ITEMS, IN_AOS, kMurmur3>), dim3(grid), dim3(kBlock), hist_lds, c->stream, a, tsz);
+    else
+        hipLaunchKernelGGL((k_hist_super<ITEMS, IN_AOS, kXXH3>), dim3(grid), dim3(kBlock), hist_lds, c->stream, a, tsz);
+    PHJ_LAUNCHED(c, hname);
+    PHJ_TRY(timer_end(c));
+    PHJ_TRY(timer_begin(c, cname.c_str(), static_cast<uint64_t>(hist_len) * 12));
+    PHJ_TRY(scan_u32(c, a.hist, hist_len, 1, hist_len));
+    PHJ_TRY(timer_end(c));
+    PHJ_TRY(timer_begin(c, sname.c_str(), n * 32));
+    if (hk == kMurmur3)
+        hipLaunchKernelGGL((k_scatter_wc<ITEMS, IN_AOS, kMurmur3, LW>), dim3(grid), dim3(kBlock), sc_lds, c->stream, a, tsz);
+    else
+        hipLaunchKernelGGL((k_scatter_wc<ITEMS, IN_AOS, kXXH3, LW>), dim3(grid), dim3(kBlock), sc_lds, c->stream, a, tsz);
+    PHJ_LAUNCHED(c, sname);
+    PHJ_TRY(timer_end(c));
+    return PHJ_OK;
+}
+
+int launch_pass_wc(phj_ctx* c, int hk, bool in_aos, PassArgs a, uint32_t ntiles, uint32_t tsz,
+                   const std::string& prefix, uint64_t n, uint32_t hist_len) {
+    if (ntiles == 0) return PHJ_OK;
+    uint32_t grid = ntiles;
+    a.xcd_remap = 0;
+    if (c->tune.xcd_remap) {
+        grid = (ntiles + 7) & ~7u;
+        a.xcd_remap = 1;
+    }
+    const int key = (c->tune.wc_lw == 16 ? 2 : 0) + (in_aos ? 1 : 0);
+    if (c->tune.wc_items == 4) {
+        switch (key) {
+            case 0: return launch_pass_wc_t<4, false, 8>(c, hk, a, grid, tsz, prefix, n, hist_len);
+            case 1: return launch_pass_wc_t<4, true, 8>(c, hk, a, grid, tsz, prefix, n, hist_len);
+            case 2: return launch_pass_wc_t<4, false, 16>(c, hk, a, grid, tsz, prefix, n, hist_len);
+            default: return launch_pass_wc_t<4, true, 16>(c, hk, a, grid, tsz, prefix, n, hist_len);
+        }
+    }
+    switch (key) {
+        case 0: return launch_pass_wc_t<8, false, 8>(c, hk, a, grid, tsz, prefix, n, hist_len);
+        case 1: return launch_pass_wc_t<8, true, 8>(c, hk, a, grid, tsz, prefix, n, hist_len);
+        default: return set_err(c, PHJ_ERR_INVALID, "unsupported WC shape");
+    }
+}
+
+// Tuples per (super-)tile of a pass over n tuples with nb digits.
+uint32_t pass_tile(const phj_ctx* c, uint32_t n, uint32_t nb, bool* wc) {
+    *wc = c->tune.wc && nb <= static_cast<uint32_t>(kWcMaxBins);
+    if (!*wc) {
+        if (c->tune.tile == 8192 && scatter_lds_bytes(8192, nb, 8) > 160 * 1024) return 4096;
+        return static_cast<uint32_t>(c->tune.tile);
+    }
+    const uint32_t sub = kBlock * static_cast<uint32_t>(c->tune.wc_items);
+    const uint64_t subs = (static_cast<uint64_t>(n) + sub - 1) / sub;
+    const uint64_t k = std::min<uint64_t>(64, std::max<uint64_t>(1, (subs + c->tune.wc_wgs - 1) / c->tune.wc_wgs));
+    return static_cast<uint32_t>(sub * k);
 }
 
 int partition_side(phj_ctx* c, int s, const Plan& pl) {
     SideState& S = c->side[s];
     if (!S.rel && S.n > 0) return set_err(c, PHJ_ERR_STATE, "relation not bound");
     const uint64_t n64 = S.n;
-    if (n64 >= (1ull << 32) - 2 * kTile) return set_err(c, PHJ_ERR_RANGE, "relation above 2^32 tuples per device");
+    if (n64 >= (1ull << 32) - 2 * 4096) return set_err(c, PHJ_ERR_RANGE, "relation above 2^32 tuples per device");
     const uint32_t n = static_cast<uint32_t>(n64);
-    const uint32_t nt1 = (n + kTile - 1) / kTile;
+    bool wc1 = false, wc2 = false;
+    const uint32_t tile = pass_tile(c, n, pl.nb1, &wc1);
+    const uint32_t tile2 = pl.npass == 2 ? pass_tile(c, n, pl.nb2, &wc2) : 0;
+    const uint32_t nt1 = (n + tile - 1) / tile;
+    const uint32_t nt2 = pl.npass == 2 ? (n + tile2 - 1) / tile2 + pl.nb1 : 0;  // bound
+    const bool p1_aos = pl.npass == 2 && c->tune.p1_aos && !wc1;
     const char* tag = s == PHJ_SIDE_BUILD ? "R" : "S";
     // workspace (grow-only; allocation is outside the timed phases on reuse)
-    PHJ_TRY(ensure(c, S.kA, static_cast<size_t>(n) * 8));
-    PHJ_TRY(ensure(c, S.pA, static_cast<size_t>(n) * 8));
+    PHJ_TRY(ensure(c, S.kA, static_cast<size_t>(n) * (p1_aos ? 16 : 8)));
+    if (!p1_aos) PHJ_TRY(ensure(c, S.pA, static_cast<size_t>(n) * 8));
     PHJ_TRY(ensure(c, S.hist1, static_cast<size_t>(nt1) * pl.nb1 * 4));
     PHJ_TRY(ensure(c, S.bounds1, (static_cast<size_t>(pl.nb1) + 1) * 4));
     if (pl.npass == 2) {
         PHJ_TRY(ensure(c, S.kB, static_cast<size_t>(n) * 8));
         PHJ_TRY(ensure(c, S.pB, static_cast<size_t>(n) * 8));
         PHJ_TRY(ensure(c, S.tbase2, (static_cast<size_t>(pl.nb1) + 1) * 4));
-        PHJ_TRY(ensure(c, S.hist2, (static_cast<size_t>(nt1) + pl.nb1) * pl.nb2 * 4));
+        PHJ_TRY(ensure(c, S.hist2, (static_cast<size_t>(nt2) + 8) * pl.nb2 * 4));
         PHJ_TRY(ensure(c, S.bounds, (static_cast<size_t>(pl.Ppad) + 1) * 4));
     }
     // pass 1: AoS relation -> SoA columns A
@@ -352,10 +465,13 @@ int partition_side(phj_ctx* c, int s, const Plan& pl) {
     a.nbins = pl.nb1;
     a.nbits = pl.bits1;
     a.f = digit_fn(pl, 1);
-    PHJ_TRY(launch_pass<true>(c, pl.hk, a, nt1, std::string(tag) + ".p1", n, nt1 * pl.nb1));
+    if (wc1)
+        PHJ_TRY(launch_pass_wc(c, pl.hk, true, a, nt1, tile, std::string(tag) + ".p1", n, nt1 * pl.nb1));
+    else
+        PHJ_TRY(launch_pass(c, pl.hk, true, p1_aos, a, nt1, std::string(tag) + ".p1", n, nt1 * pl.nb1));
     uint32_t* tb2 = pl.npass == 2 ? static_cast<uint32_t*>(S.tbase2.p) : nullptr;
     hipLaunchKernelGGL(k_pass1_finish, dim3(1), dim3(1024), 0, c->stream, a.hist, nt1, pl.nb1, n,
-                       kTile, static_cast<uint32_t*>(S.bounds1.p), tb2);
+                       pl.npass == 2 ? tile2 : tile, static_cast<uint32_t*>(S.bounds1.p), tb2);
     PHJ_LAUNCHED(c, "k_pass1_finish");
     if (pl.npass == 1) {
         S.view.keys = static_cast<const int64_t*>(S.kA.p);
@@ -364,7 +480,7 @@ int partition_side(phj_ctx* c, int s, const Plan& pl) {
     } else {
         PassArgs b{};
         b.in_keys = static_cast<const int64_t*>(S.kA.p);
-        b.in_pays = static_cast<const int64_t*>(S.pA.p);
+        b.in_pays = p1_aos ? nullptr : static_cast<const int64_t*>(S.pA.p);
         b.out_keys = static_cast<int64_t*>(S.kB.p);
         b.out_pays = static_cast<int64_t*>(S.pB.p);
         b.hist = static_cast<uint32_t*>(S.hist2.p);
@@ -376,8 +492,11 @@ int partition_side(phj_ctx* c, int s, const Plan& pl) {
         b.nbins = pl.nb2;
         b.nbits = pl.bits2;
         b.f = digit_fn(pl, 2);
-        const uint32_t grid2 = n ? nt1 + pl.nb1 : 0;
-        PHJ_TRY(launch_pass<false>(c, pl.hk, b, grid2, std::string(tag) + ".p2", n, grid2 * pl.nb2));
+        const uint32_t grid2 = n ? nt2 : 0;
+        if (wc2)
+            PHJ_TRY(launch_pass_wc(c, pl.hk, false, b, grid2, tile2, std::string(tag) + ".p2", n, grid2 * pl.nb2));
+        else
+            PHJ_TRY(launch_pass(c, pl.hk, p1_aos, false, b, grid2, std::string(tag) + ".p2", n, grid2 * pl.nb2));
         const uint32_t nbnd = pl.Ppad + 1;
         hipLaunchKernelGGL(k_pass2_bounds, dim3((nbnd + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream,
                            b.hist, tb2, b.seg_bounds, pl.nb1, pl.nb2, n, static_cast<uint32_t*>(S.bounds.p));
@@ -606,8 +725,17 @@ int phj_ctx_create(int device, phj_ctx** out) {
         return PHJ_ERR_HIP;
     }
     c->own_stream = true;
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->max_lds = static_cast<int>(prop.sharedMemPerBlock);
+    {
+        const int t = env_int("PHJ_TILE", 4096);
+        c->tune.tile = (t == 2048 || t == 8192) ? t : 4096;
+    }
+    c->tune.p1_aos = env_int("PHJ_P1_AOS", 0) != 0;
+    c->tune.xcd_remap = env_int("PHJ_XCD_REMAP", 1) != 0;
+    c->tune.wc = env_int("PHJ_WC", 0) != 0;
+    c->tune.wc_items = env_int("PHJ_WC_ITEMS", 8) == 4 ? 4 : 8;
+    c->tune.wc_lw = env_int("PHJ_WC_LW", 8) == 16 ? 16 : 8;
+    c->tune.wc_wgs = std::max(64, env_int("PHJ_WC_WGS", 1024));
+    if (c->tune.wc_items == 8 && c->tune.wc_lw == 16) c->tune.wc_items = 4;  // LDS budget
     // gfx950 launches accept dynamic LDS up to the 160 KiB per workgroup without an
     // opt-in attribute; clear any error a probe of the runtime left behind
     (void)hipGetLastError();
@@ -826,6 +954,16 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
     r->num_partitions = pl.Ppad;
     r->algorithmic_bytes = partition_bytes(pl, R.n) + partition_bytes(pl, S.n) + R.n * 32 + S.n * 8 + R.n * 8;
     return fill_timers(c, r);
+}
+
+int phj_timers_report(phj_ctx* c, phj_join_result* r) {
+    if (!c || !r) return PHJ_ERR_INVALID;
+    PHJ_HIP(c, hipSetDevice(c->device));
+    PHJ_HIP(c, hipStreamSynchronize(c->stream));
+    std::memset(r, 0, sizeof(*r));
+    const int rc = fill_timers(c, r);
+    reset_timers(c);
+    return rc;
 }
 
 int phj_partitioned_download(phj_ctx* c, const phj_partitioned* v, int64_t* keys, int64_t* payloads,

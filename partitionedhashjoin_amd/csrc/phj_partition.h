@@ -71,16 +71,26 @@ struct PassArgs {
     uint32_t ntiles1;           // tiles of the single-segment case
     uint32_t nbins;
     uint32_t nbits;
-    uint32_t pad;
+    uint32_t xcd_remap;         // 1: give each XCD a contiguous run of tiles (grid % 8 == 0)
     DigitFn f;
 };
+
+// Workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md,
+// "Workgroup dispatch"); with xcd_remap each XCD instead walks a contiguous
+// run of tiles, so the partial output lines of neighbouring tiles meet in one
+// L2. Placement only changes speed, never results.
+__device__ __forceinline__ uint32_t tile_id(const PassArgs& a) {
+    if (!a.xcd_remap) return blockIdx.x;
+    const uint32_t per = gridDim.x >> 3;
+    return (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
+}
 
 struct TileLoc {
     uint32_t tseg, ntiles_s, tb_s, lo, hi;
 };
 
-template <int T>
-__device__ __forceinline__ bool locate_tile(const PassArgs& a, uint32_t tile, TileLoc& L) {
+__device__ __forceinline__ bool locate_tile_rt(const PassArgs& a, uint32_t tile, uint32_t T,
+                                               TileLoc& L) {
     if (a.seg_bounds == nullptr) {
         if (tile >= a.ntiles1) return false;
         L.tseg = tile;
@@ -106,6 +116,11 @@ __device__ __forceinline__ bool locate_tile(const PassArgs& a, uint32_t tile, Ti
     return true;
 }
 
+template <int T>
+__device__ __forceinline__ bool locate_tile(const PassArgs& a, uint32_t tile, TileLoc& L) {
+    return locate_tile_rt(a, tile, T, L);
+}
+
 __device__ __forceinline__ uint64_t lanemask_lt() {
     const uint32_t lane = threadIdx.x & 63;
     return (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
@@ -122,9 +137,10 @@ __device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid, uint32_t
     return m;
 }
 
-// Exclusive scan of one value per thread across the 256-thread block.
-__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* tmp,
-                                                         uint32_t& total) {
+// Exclusive scan of one value per thread across a block of NW waves.
+template <int NW>
+__device__ __forceinline__ uint32_t block_exclusive_scan_t(uint32_t v, uint32_t* tmp,
+                                                           uint32_t& total) {
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t x = v;
 #pragma unroll
@@ -136,7 +152,7 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* t
     __syncthreads();
     uint32_t before = 0, all = 0;
 #pragma unroll
-    for (int w = 0; w < kWaves; w++) {
+    for (int w = 0; w < NW; w++) {
         const uint32_t s = tmp[w];
         if (w < (int)wave) before += s;
         all += s;
@@ -144,6 +160,11 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* t
     __syncthreads();
     total = all;
     return before + x - v;
+}
+
+__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* tmp,
+                                                         uint32_t& total) {
+    return block_exclusive_scan_t<kWaves>(v, tmp, total);
 }
 
 template <bool AOS>
@@ -159,16 +180,17 @@ __device__ __forceinline__ void load_tuple(const PassArgs& a, uint32_t idx, int6
 }
 
 // Per-tile digit histogram -> hist[(tb_s * nbins) + d * ntiles_s + tseg].
-template <int ITEMS, bool AOS, int HK>
-__global__ __launch_bounds__(kBlock) void k_hist(PassArgs a) {
-    constexpr int T = kBlock * ITEMS;
+template <int BLOCK, int ITEMS, bool AOS, int HK>
+__global__ __launch_bounds__(BLOCK) void k_hist(PassArgs a) {
+    constexpr int NW = BLOCK / 64;
+    constexpr int T = BLOCK * ITEMS;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    uint32_t* wcnt = reinterpret_cast<uint32_t*>(smem);  // [kWaves][nbins]
+    uint32_t* wcnt = reinterpret_cast<uint32_t*>(smem);  // [NW][nbins]
     TileLoc L;
-    if (!locate_tile<T>(a, blockIdx.x, L)) return;
+    if (!locate_tile<T>(a, tile_id(a), L)) return;
     const uint32_t nb = a.nbins;
     const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    for (uint32_t i = tid; i < kWaves * nb; i += kBlock) wcnt[i] = 0;
+    for (uint32_t i = tid; i < NW * nb; i += BLOCK) wcnt[i] = 0;
     const uint32_t cnt = L.hi - L.lo;
     int64_t key[ITEMS];
     const uint32_t wbase = wave * 64 * ITEMS;
@@ -196,41 +218,42 @@ __global__ __launch_bounds__(kBlock) void k_hist(PassArgs a) {
     }
     __syncthreads();
     uint32_t* out = a.hist + static_cast<size_t>(L.tb_s) * nb + L.tseg;
-    for (uint32_t d = tid; d < nb; d += kBlock) {
+    for (uint32_t d = tid; d < nb; d += BLOCK) {
         uint32_t c = 0;
 #pragma unroll
-        for (int w = 0; w < kWaves; w++) c += wcnt[w * nb + d];
+        for (int w = 0; w < NW; w++) c += wcnt[w * nb + d];
         out[static_cast<size_t>(d) * L.ntiles_s] = c;
     }
 }
 
-// LDS bytes of k_scatter for a tile of T tuples and nb digits.
-__host__ __device__ constexpr size_t scatter_lds_bytes(int T, uint32_t nb) {
-    return static_cast<size_t>(T) * 18 + static_cast<size_t>(nb) * 4 * (kWaves + 2) + 64;
+// LDS bytes of k_scatter for a tile of T tuples, nb digits, NW waves.
+__host__ __device__ constexpr size_t scatter_lds_bytes(int T, uint32_t nb, int NW = kWaves) {
+    return static_cast<size_t>(T) * 18 + static_cast<size_t>(nb) * 4 * (NW + 2) + 64;
 }
 
 // Stable scatter of one tile using the scanned offsets.
-template <int ITEMS, bool AOS, int HK>
-__global__ __launch_bounds__(kBlock) void k_scatter(PassArgs a) {
-    constexpr int T = kBlock * ITEMS;
+template <int BLOCK, int ITEMS, bool AOS, bool OUT_AOS, int HK>
+__global__ __launch_bounds__(BLOCK) void k_scatter(PassArgs a) {
+    constexpr int NW = BLOCK / 64;
+    constexpr int T = BLOCK * ITEMS;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t nb = a.nbins;
     int64_t* skey = reinterpret_cast<int64_t*>(smem);
     int64_t* spay = skey + T;
-    uint32_t* wcnt = reinterpret_cast<uint32_t*>(spay + T);  // [kWaves][nb]
-    uint32_t* gofs = wcnt + kWaves * nb;
+    uint32_t* wcnt = reinterpret_cast<uint32_t*>(spay + T);  // [NW][nb]
+    uint32_t* gofs = wcnt + NW * nb;
     uint32_t* dstart = gofs + nb;
     uint32_t* tmp = dstart + nb;                              // 16 words
     uint16_t* sdig = reinterpret_cast<uint16_t*>(tmp + 16);   // [T]
 
     TileLoc L;
-    if (!locate_tile<T>(a, blockIdx.x, L)) return;
+    if (!locate_tile<T>(a, tile_id(a), L)) return;
     const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const uint32_t cnt = L.hi - L.lo;
-    for (uint32_t i = tid; i < kWaves * nb; i += kBlock) wcnt[i] = 0;
+    for (uint32_t i = tid; i < NW * nb; i += BLOCK) wcnt[i] = 0;
     {
         const uint32_t* h = a.hist + static_cast<size_t>(L.tb_s) * nb + L.tseg;
-        for (uint32_t d = tid; d < nb; d += kBlock) gofs[d] = h[static_cast<size_t>(d) * L.ntiles_s];
+        for (uint32_t d = tid; d < nb; d += BLOCK) gofs[d] = h[static_cast<size_t>(d) * L.ntiles_s];
     }
     int64_t key[ITEMS], pay[ITEMS];
     uint32_t dig[ITEMS], rank[ITEMS];
@@ -263,24 +286,24 @@ __global__ __launch_bounds__(kBlock) void k_scatter(PassArgs a) {
     __syncthreads();
     // digit totals -> tile-local digit starts and per-wave starts
     {
-        const uint32_t dpt = (nb + kBlock - 1) / kBlock;
+        const uint32_t dpt = (nb + BLOCK - 1) / BLOCK;
         const uint32_t d0 = tid * dpt;
         uint32_t local = 0;
         for (uint32_t j = 0; j < dpt; j++) {
             const uint32_t d = d0 + j;
             if (d < nb) {
 #pragma unroll
-                for (int w = 0; w < kWaves; w++) local += wcnt[w * nb + d];
+                for (int w = 0; w < NW; w++) local += wcnt[w * nb + d];
             }
         }
         uint32_t total;
-        uint32_t run = block_exclusive_scan(local, tmp, total);
+        uint32_t run = block_exclusive_scan_t<NW>(local, tmp, total);
         for (uint32_t j = 0; j < dpt; j++) {
             const uint32_t d = d0 + j;
             if (d < nb) {
                 dstart[d] = run;
 #pragma unroll
-                for (int w = 0; w < kWaves; w++) {
+                for (int w = 0; w < NW; w++) {
                     const uint32_t c = wcnt[w * nb + d];
                     wcnt[w * nb + d] = run;
                     run += c;
@@ -302,12 +325,16 @@ __global__ __launch_bounds__(kBlock) void k_scatter(PassArgs a) {
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < ITEMS; i++) {
-        const uint32_t k = i * kBlock + tid;
+        const uint32_t k = i * BLOCK + tid;
         if (k < cnt) {
             const uint32_t d = sdig[k];
             const uint32_t o = gofs[d] + (k - dstart[d]);
-            a.out_keys[o] = skey[k];
-            a.out_pays[o] = spay[k];
+            if constexpr (OUT_AOS) {
+                reinterpret_cast<longlong2*>(a.out_keys)[o] = make_longlong2(skey[k], spay[k]);
+            } else {
+                a.out_keys[o] = skey[k];
+                a.out_pays[o] = spay[k];
+            }
         }
     }
 }
