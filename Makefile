@@ -16,7 +16,7 @@ CLI := $(PKG)/phjoin
 HIP_SRC := $(PKG)/csrc/phj_capi.hip
 HIP_HDR := $(PKG)/csrc/phj_partition.h $(PKG)/csrc/phj_partition_wc.h $(PKG)/csrc/phj_join.h $(PKG)/csrc/phj_hash.h include/phj.h
 HOST_SRC := $(wildcard $(PKG)/host/*.cpp $(PKG)/host/*/*.cpp)
-HOST_HDR := $(wildcard $(PKG)/host/*.hpp $(PKG)/host/*/*.hpp)
+HOST_HDR := $(wildcard $(PKG)/host/*.hpp $(PKG)/host/*/*.hpp) $(PKG)/csrc/phj_hash.h
 
 ifneq ($(HOST_SRC),)
 all: $(LIB) $(CLI) oracle
@@ -28,7 +28,7 @@ $(LIB): $(HIP_SRC) $(HIP_HDR)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(HIP_SRC)
 
 $(CLI): $(HOST_SRC) $(HOST_HDR) include/phj.h $(LIB)
-	$(CXX) $(CXXFLAGS) -Iinclude -I$(PKG)/host -o $@ $(HOST_SRC) -L$(PKG) -lphj_hip -Wl,-rpath,'$$ORIGIN'
+	$(CXX) $(CXXFLAGS) -Iinclude -I$(PKG)/host -I$(PKG)/csrc -o $@ $(HOST_SRC) -L$(PKG) -lphj_hip -Wl,-rpath,'$$ORIGIN'
 
 oracle:
 	$(MAKE) -s -C oracle liboracle.so

@@ -27,8 +27,6 @@ using namespace phj;
 
 namespace {
 
-constexpr int kProbeItems = 16;                     // S keys per thread per probe item
-constexpr uint32_t kChunk = kBlock * kProbeItems;   // 4096 S tuples per probe item
 constexpr int kNPProbeItems = 4;
 constexpr double kNPDefaultRatio = 2.0;             // slots per build tuple
 
@@ -47,6 +45,8 @@ struct Tuning {
     int wc_items = 8;     // WC sub-tile = 256 * wc_items tuples (4 or 8)
     int wc_lw = 8;        // WC line: elements per column (8 = 64 B, 16 = 128 B)
     int wc_wgs = 1024;    // target workgroups per WC pass (super-tile size follows)
+    bool r_aux = false;   // partition R on the aux stream (no gain measured: DESIGN.md)
+    int probe_items = 8;  // S keys per lane per probe work item (8 or 16)
 };
 
 int env_int(const char* name, int dflt) {
@@ -81,7 +81,7 @@ struct SideState {
     uint64_t n = 0;
     DevBuf owned;
     DevBuf kA, pA, kB, pB;
-    DevBuf hist1, hist2, bounds1, tbase2, bounds;
+    DevBuf hist1, hist2, bounds1, tbase2, tseg2, bounds, partials;
     phj_partitioned view{};
     bool partitioned = false;
     Plan plan;
@@ -104,10 +104,14 @@ uint32_t next_pow2_u32(uint32_t x) {
 
 struct phj_ctx {
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;  // the ctx stream (own or borrowed)
+    hipStream_t aux = nullptr;     // ctx-owned: R-side partitioning runs here beside S
+    hipStream_t ks = nullptr;      // stream the current launches go to (stream or aux)
+    DevBuf* scan_scratch = nullptr; // scan partials of the side being partitioned
+    int num_cus = 256;
     bool own_stream = false;
     SideState side[2];
-    DevBuf scan_partials, prep, tkeys, tpays, toffs, gcursor, items, count;
+    DevBuf scan_partials, prep, tkeys, tpays, toffs, gcursor, items, count, biglist;
     DevBuf np_tab, np_pays;
     std::vector<hipEvent_t> evpool;
     size_t evnext = 0;
@@ -150,6 +154,7 @@ int ensure(phj_ctx* c, DevBuf& b, size_t bytes) {
     if (b.bytes >= bytes) return PHJ_OK;
     if (b.p) {
         PHJ_HIP(c, hipStreamSynchronize(c->stream));
+        PHJ_HIP(c, hipStreamSynchronize(c->aux));
         PHJ_HIP(c, hipFree(b.p));
         b.p = nullptr;
         b.bytes = 0;
@@ -182,7 +187,7 @@ hipEvent_t next_event(phj_ctx* c) {
 int mark(phj_ctx* c, hipEvent_t* out) {
     *out = next_event(c);
     if (!*out) return set_err(c, PHJ_ERR_HIP, "hipEventCreate failed");
-    PHJ_HIP(c, hipEventRecord(*out, c->stream));
+    PHJ_HIP(c, hipEventRecord(*out, c->ks));
     return PHJ_OK;
 }
 
@@ -288,20 +293,20 @@ DigitFn digit_fn(const Plan& pl, int pass) {
     return f;
 }
 
-int scan_u32(phj_ctx* c, uint32_t* data, uint32_t len, uint32_t narrays, uint32_t stride) {
+int scan_u32(phj_ctx* c, uint32_t* data, uint32_t len, uint32_t narrays, uint32_t stride,
+             DevBuf* scratch = nullptr) {
     if (len == 0) return PHJ_OK;
     ScanArgs s{};
     s.data = data;
     s.len = len;
     s.stride = stride;
     s.nblk = (len + kScanBlockElems - 1) / kScanBlockElems;
-    PHJ_TRY(ensure(c, c->scan_partials, static_cast<size_t>(s.nblk) * narrays * 4));
-    s.partials = static_cast<uint32_t*>(c->scan_partials.p);
-    hipLaunchKernelGGL(k_scan_reduce, dim3(s.nblk, narrays), dim3(kBlock), 0, c->stream, s);
+    DevBuf& part = scratch ? *scratch : c->scan_partials;
+    PHJ_TRY(ensure(c, part, static_cast<size_t>(s.nblk) * narrays * 4));
+    s.partials = static_cast<uint32_t*>(part.p);
+    hipLaunchKernelGGL(k_scan_reduce, dim3(s.nblk, narrays), dim3(kBlock), 0, c->ks, s);
     PHJ_LAUNCHED(c, "k_scan_reduce");
-    hipLaunchKernelGGL(k_scan_partials, dim3(1, narrays), dim3(1024), 0, c->stream, s);
-    PHJ_LAUNCHED(c, "k_scan_partials");
-    hipLaunchKernelGGL(k_scan_apply, dim3(s.nblk, narrays), dim3(kBlock), 0, c->stream, s);
+    hipLaunchKernelGGL(k_scan_apply, dim3(s.nblk, narrays), dim3(kBlock), 0, c->ks, s);
     PHJ_LAUNCHED(c, "k_scan_apply");
     return PHJ_OK;
 }
@@ -318,19 +323,19 @@ int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const st
     // the scatter reads and writes every tuple once (16 + 16 B)
     PHJ_TRY(timer_begin(c, hname.c_str(), n * (IN_AOS ? 16 : 8)));
     if (hk == kMurmur3)
-        hipLaunchKernelGGL((k_hist<BLOCK, ITEMS, IN_AOS, kMurmur3>), dim3(grid), dim3(BLOCK), hist_lds, c->stream, a);
+        hipLaunchKernelGGL((k_hist<BLOCK, ITEMS, IN_AOS, kMurmur3>), dim3(grid), dim3(BLOCK), hist_lds, c->ks, a);
     else
-        hipLaunchKernelGGL((k_hist<BLOCK, ITEMS, IN_AOS, kXXH3>), dim3(grid), dim3(BLOCK), hist_lds, c->stream, a);
+        hipLaunchKernelGGL((k_hist<BLOCK, ITEMS, IN_AOS, kXXH3>), dim3(grid), dim3(BLOCK), hist_lds, c->ks, a);
     PHJ_LAUNCHED(c, hname);
     PHJ_TRY(timer_end(c));
     PHJ_TRY(timer_begin(c, cname.c_str(), static_cast<uint64_t>(hist_len) * 12));
-    PHJ_TRY(scan_u32(c, a.hist, hist_len, 1, hist_len));
+    PHJ_TRY(scan_u32(c, a.hist, hist_len, 1, hist_len, c->scan_scratch));
     PHJ_TRY(timer_end(c));
     PHJ_TRY(timer_begin(c, sname.c_str(), n * 32));
     if (hk == kMurmur3)
-        hipLaunchKernelGGL((k_scatter<BLOCK, ITEMS, IN_AOS, OUT_AOS, kMurmur3>), dim3(grid), dim3(BLOCK), sc_lds, c->stream, a);
+        hipLaunchKernelGGL((k_scatter<BLOCK, ITEMS, IN_AOS, OUT_AOS, kMurmur3>), dim3(grid), dim3(BLOCK), sc_lds, c->ks, a);
     else
-        hipLaunchKernelGGL((k_scatter<BLOCK, ITEMS, IN_AOS, OUT_AOS, kXXH3>), dim3(grid), dim3(BLOCK), sc_lds, c->stream, a);
+        hipLaunchKernelGGL((k_scatter<BLOCK, ITEMS, IN_AOS, OUT_AOS, kXXH3>), dim3(grid), dim3(BLOCK), sc_lds, c->ks, a);
     PHJ_LAUNCHED(c, sname);
     PHJ_TRY(timer_end(c));
     return PHJ_OK;
@@ -370,19 +375,19 @@ int launch_pass_wc_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, uint3
     const std::string hname = prefix + ".hist", cname = prefix + ".scan", sname = prefix + ".scatter";
     PHJ_TRY(timer_begin(c, hname.c_str(), n * (IN_AOS ? 16 : 8)));
     if (hk == kMurmur3)
-        hipLaunchKernelGGL((k_hist_super<ITEMS, IN_AOS, kMurmur3>), dim3(grid), dim3(kBlock), hist_lds, c->stream, a, tsz);
+        hipLaunchKernelGGL((k_hist_super<ITEMS, IN_AOS, kMurmur3>), dim3(grid), dim3(kBlock), hist_lds, c->ks, a, tsz);
     else
-        hipLaunchKernelGGL((k_hist_super<ITEMS, IN_AOS, kXXH3>), dim3(grid), dim3(kBlock), hist_lds, c->stream, a, tsz);
+        hipLaunchKernelGGL((k_hist_super<ITEMS, IN_AOS, kXXH3>), dim3(grid), dim3(kBlock), hist_lds, c->ks, a, tsz);
     PHJ_LAUNCHED(c, hname);
     PHJ_TRY(timer_end(c));
     PHJ_TRY(timer_begin(c, cname.c_str(), static_cast<uint64_t>(hist_len) * 12));
-    PHJ_TRY(scan_u32(c, a.hist, hist_len, 1, hist_len));
+    PHJ_TRY(scan_u32(c, a.hist, hist_len, 1, hist_len, c->scan_scratch));
     PHJ_TRY(timer_end(c));
     PHJ_TRY(timer_begin(c, sname.c_str(), n * 32));
     if (hk == kMurmur3)
-        hipLaunchKernelGGL((k_scatter_wc<ITEMS, IN_AOS, kMurmur3, LW>), dim3(grid), dim3(kBlock), sc_lds, c->stream, a, tsz);
+        hipLaunchKernelGGL((k_scatter_wc<ITEMS, IN_AOS, kMurmur3, LW>), dim3(grid), dim3(kBlock), sc_lds, c->ks, a, tsz);
     else
-        hipLaunchKernelGGL((k_scatter_wc<ITEMS, IN_AOS, kXXH3, LW>), dim3(grid), dim3(kBlock), sc_lds, c->stream, a, tsz);
+        hipLaunchKernelGGL((k_scatter_wc<ITEMS, IN_AOS, kXXH3, LW>), dim3(grid), dim3(kBlock), sc_lds, c->ks, a, tsz);
     PHJ_LAUNCHED(c, sname);
     PHJ_TRY(timer_end(c));
     return PHJ_OK;
@@ -428,6 +433,7 @@ uint32_t pass_tile(const phj_ctx* c, uint32_t n, uint32_t nb, bool* wc) {
 
 int partition_side(phj_ctx* c, int s, const Plan& pl) {
     SideState& S = c->side[s];
+    c->scan_scratch = &S.partials;
     if (!S.rel && S.n > 0) return set_err(c, PHJ_ERR_STATE, "relation not bound");
     const uint64_t n64 = S.n;
     if (n64 >= (1ull << 32) - 2 * 4096) return set_err(c, PHJ_ERR_RANGE, "relation above 2^32 tuples per device");
@@ -449,6 +455,7 @@ int partition_side(phj_ctx* c, int s, const Plan& pl) {
         PHJ_TRY(ensure(c, S.pB, static_cast<size_t>(n) * 8));
         PHJ_TRY(ensure(c, S.tbase2, (static_cast<size_t>(pl.nb1) + 1) * 4));
         PHJ_TRY(ensure(c, S.hist2, (static_cast<size_t>(nt2) + 8) * pl.nb2 * 4));
+        PHJ_TRY(ensure(c, S.tseg2, (static_cast<size_t>(nt2) + 8) * 4));
         PHJ_TRY(ensure(c, S.bounds, (static_cast<size_t>(pl.Ppad) + 1) * 4));
     }
     // pass 1: AoS relation -> SoA columns A
@@ -470,7 +477,7 @@ int partition_side(phj_ctx* c, int s, const Plan& pl) {
     else
         PHJ_TRY(launch_pass(c, pl.hk, true, p1_aos, a, nt1, std::string(tag) + ".p1", n, nt1 * pl.nb1));
     uint32_t* tb2 = pl.npass == 2 ? static_cast<uint32_t*>(S.tbase2.p) : nullptr;
-    hipLaunchKernelGGL(k_pass1_finish, dim3(1), dim3(1024), 0, c->stream, a.hist, nt1, pl.nb1, n,
+    hipLaunchKernelGGL(k_pass1_finish, dim3(1), dim3(1024), 0, c->ks, a.hist, nt1, pl.nb1, n,
                        pl.npass == 2 ? tile2 : tile, static_cast<uint32_t*>(S.bounds1.p), tb2);
     PHJ_LAUNCHED(c, "k_pass1_finish");
     if (pl.npass == 1) {
@@ -486,7 +493,13 @@ int partition_side(phj_ctx* c, int s, const Plan& pl) {
         b.hist = static_cast<uint32_t*>(S.hist2.p);
         b.seg_bounds = static_cast<const uint32_t*>(S.bounds1.p);
         b.tile_base = tb2;
+        b.tile_seg = static_cast<const uint32_t*>(S.tseg2.p);
         b.nseg = pl.nb1;
+        if (n) {
+            hipLaunchKernelGGL(k_tile_seg, dim3((pl.nb1 + kWaves - 1) / kWaves), dim3(kBlock), 0, c->ks, tb2,
+                               pl.nb1, static_cast<uint32_t*>(S.tseg2.p));
+            PHJ_LAUNCHED(c, "k_tile_seg");
+        }
         b.n = n;
         b.ntiles1 = 0;
         b.nbins = pl.nb2;
@@ -498,7 +511,7 @@ int partition_side(phj_ctx* c, int s, const Plan& pl) {
         else
             PHJ_TRY(launch_pass(c, pl.hk, p1_aos, false, b, grid2, std::string(tag) + ".p2", n, grid2 * pl.nb2));
         const uint32_t nbnd = pl.Ppad + 1;
-        hipLaunchKernelGGL(k_pass2_bounds, dim3((nbnd + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream,
+        hipLaunchKernelGGL(k_pass2_bounds, dim3((nbnd + kBlock - 1) / kBlock), dim3(kBlock), 0, c->ks,
                            b.hist, tb2, b.seg_bounds, pl.nb1, pl.nb2, n, static_cast<uint32_t*>(S.bounds.p));
         PHJ_LAUNCHED(c, "k_pass2_bounds");
         S.view.keys = static_cast<const int64_t*>(S.kB.p);
@@ -542,28 +555,30 @@ int build_and_probe(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned*
     const size_t noffs = nR + 2 * static_cast<size_t>(P) + 1;
     PHJ_TRY(ensure(c, c->toffs, noffs * 4));
     PHJ_TRY(ensure(c, c->gcursor, noffs * 4));
+    const uint32_t kChunk = kBlock * static_cast<uint32_t>(c->tune.probe_items);
     const size_t item_bound = P + (nS + kChunk - 1) / kChunk;
-    PHJ_TRY(ensure(c, c->items, item_bound * 8));
-    PHJ_TRY(ensure(c, c->count, 8));
+    PHJ_TRY(ensure(c, c->items, item_bound * sizeof(ProbeItem)));
+    PHJ_TRY(ensure(c, c->count, 16));
+    PHJ_TRY(ensure(c, c->biglist, static_cast<size_t>(P) * 4));
     uint32_t* prep = static_cast<uint32_t*>(c->prep.p);
     // LDS capacities from the expected partition size (larger partitions take
     // the global-memory path; results are identical).
     const uint64_t expect = (nR + P - 1) / P;
     const uint32_t kcap = expect * 2 > 8192 ? 256u : std::max<uint32_t>(256, next_pow2_u32(static_cast<uint32_t>(expect * 2)));
-    const uint32_t ocap_probe = kcap / 2 + 1;
-    const uint32_t ocap_build = std::min<uint32_t>(16384, std::max<uint32_t>(256, kcap));
+    const uint32_t ocap_build = 16384;
+    const uint32_t ocap_wave = std::min<uint32_t>(2048, std::max<uint32_t>(64, kcap));
 
     PHJ_TRY(mark(c, e_build0));
     PHJ_TRY(timer_begin(c, "build", nR * 32));
-    hipLaunchKernelGGL(k_join_prep, dim3((P + 1 + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream, L,
+    hipLaunchKernelGGL(k_join_prep, dim3((P + 1 + kBlock - 1) / kBlock), dim3(kBlock), 0, c->ks, L,
                        PS.view.bounds, kChunk, prep);
     PHJ_LAUNCHED(c, "k_join_prep");
     PHJ_TRY(scan_u32(c, prep, P + 1, 3, static_cast<uint32_t>(stride)));
     const uint32_t* tkb = prep;
     const uint32_t* tob = prep + stride;
     const uint32_t* itb = prep + 2 * stride;
-    hipLaunchKernelGGL(k_items_expand, dim3((P + kWaves - 1) / kWaves), dim3(kBlock), 0, c->stream, itb, P,
-                       static_cast<uint2*>(c->items.p));
+    hipLaunchKernelGGL(k_items_expand, dim3((P + kWaves - 1) / kWaves), dim3(kBlock), 0, c->ks, itb, tkb, tob,
+                       PS.view.bounds, P, kChunk, static_cast<ProbeItem*>(c->items.p));
     PHJ_LAUNCHED(c, "k_items_expand");
     BuildArgs ba{};
     ba.L = L;
@@ -575,37 +590,57 @@ int build_and_probe(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned*
     ba.gcursor = static_cast<uint32_t*>(c->gcursor.p);
     ba.ocap = ocap_build;
     ba.seed = pl.seed;
-    const uint32_t bgrid = std::min<uint32_t>(P, 8192);
+    // wave-per-partition build; partitions past a wave's LDS slice go to k_build_big
+    ba.biglist = static_cast<uint32_t*>(c->biglist.p);
+    ba.bigcount = static_cast<uint32_t*>(c->count.p) + 2;
+    PHJ_HIP(c, hipMemsetAsync(ba.bigcount, 0, 4, c->ks));
+    ba.ocap = ocap_wave;
+    const uint32_t sgrid = std::min<uint32_t>((P + kWaves - 1) / kWaves, 4096);
+    const size_t slds = static_cast<size_t>(ocap_wave) * 4 * kWaves;
+    if (pl.hk == kMurmur3)
+        hipLaunchKernelGGL((k_build_small<kMurmur3>), dim3(sgrid), dim3(kBlock), slds, c->ks, ba);
+    else
+        hipLaunchKernelGGL((k_build_small<kXXH3>), dim3(sgrid), dim3(kBlock), slds, c->ks, ba);
+    PHJ_LAUNCHED(c, "k_build_small");
+    ba.ocap = ocap_build;
     const size_t blds = 64 + static_cast<size_t>(ocap_build) * 4;
     if (pl.hk == kMurmur3)
-        hipLaunchKernelGGL((k_build<kMurmur3>), dim3(bgrid), dim3(kBlock), blds, c->stream, ba);
+        hipLaunchKernelGGL((k_build_big<kMurmur3>), dim3(256), dim3(kBlock), blds, c->ks, ba);
     else
-        hipLaunchKernelGGL((k_build<kXXH3>), dim3(bgrid), dim3(kBlock), blds, c->stream, ba);
-    PHJ_LAUNCHED(c, "k_build");
+        hipLaunchKernelGGL((k_build_big<kXXH3>), dim3(256), dim3(kBlock), blds, c->ks, ba);
+    PHJ_LAUNCHED(c, "k_build_big");
     PHJ_TRY(timer_end(c));
     PHJ_TRY(mark(c, e_build1));
 
-    PHJ_HIP(c, hipMemsetAsync(c->count.p, 0, 8, c->stream));
+    PHJ_HIP(c, hipMemsetAsync(c->count.p, 0, 8, c->ks));
     ProbeArgs pa{};
     pa.skeys = PS.view.keys;
-    pa.sbounds = PS.view.bounds;
-    pa.tkb = tkb;
-    pa.tob = tob;
     pa.tkeys = static_cast<const int64_t*>(c->tkeys.p);
     pa.toffs = static_cast<const uint32_t*>(c->toffs.p);
-    pa.items = static_cast<const uint2*>(c->items.p);
+    pa.items = static_cast<const ProbeItem*>(c->items.p);
     pa.nitems = itb + P;
     pa.count = static_cast<unsigned long long*>(c->count.p);
-    pa.kcap = kcap;
-    pa.ocap = ocap_probe;
     pa.seed = pl.seed;
-    const size_t plds = static_cast<size_t>(kcap) * 8 + static_cast<size_t>(ocap_probe) * 4 + 16;
-    const uint32_t pgrid = static_cast<uint32_t>(std::max<size_t>(1, std::min<size_t>(item_bound, 2048)));
     PHJ_TRY(timer_begin(c, "probe", nS * 8 + nR * 8));
-    if (pl.hk == kMurmur3)
-        hipLaunchKernelGGL((k_probe<kMurmur3, kProbeItems>), dim3(pgrid), dim3(kBlock), plds, c->stream, pa);
-    else
-        hipLaunchKernelGGL((k_probe<kXXH3, kProbeItems>), dim3(pgrid), dim3(kBlock), plds, c->stream, pa);
+    // staged table slice per item: 512 keys (2 per lane) covers |R|/P up to ~300
+    // (P = 65536 at 10M); larger per-partition tables stage 2048 keys or probe in place
+    const bool small = expect * 2 <= 512;
+    const void* kfn = nullptr;
+#define PHJ_PROBE_PICK(HK_, IT_, KPT_) kfn = reinterpret_cast<const void*>(&k_probe<HK_, IT_, KPT_>)
+    if (c->tune.probe_items == 8) {
+        if (pl.hk == kMurmur3) { if (small) PHJ_PROBE_PICK(kMurmur3, 8, 2); else PHJ_PROBE_PICK(kMurmur3, 8, 8); }
+        else { if (small) PHJ_PROBE_PICK(kXXH3, 8, 2); else PHJ_PROBE_PICK(kXXH3, 8, 8); }
+    } else {
+        if (pl.hk == kMurmur3) { if (small) PHJ_PROBE_PICK(kMurmur3, 16, 2); else PHJ_PROBE_PICK(kMurmur3, 16, 8); }
+        else { if (small) PHJ_PROBE_PICK(kXXH3, 16, 2); else PHJ_PROBE_PICK(kXXH3, 16, 8); }
+    }
+#undef PHJ_PROBE_PICK
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, kBlock, 0) != hipSuccess || per_cu < 1) per_cu = 2;
+    const uint32_t pgrid = static_cast<uint32_t>(
+        std::max<size_t>(1, std::min<size_t>(item_bound, static_cast<size_t>(per_cu) * c->num_cus)));
+    void* kargs[] = {&pa};
+    PHJ_HIP(c, hipLaunchKernel(kfn, dim3(pgrid), dim3(kBlock), kargs, 0, c->ks));
     PHJ_LAUNCHED(c, "k_probe");
     PHJ_TRY(timer_end(c));
     PHJ_TRY(mark(c, e_probe1));
@@ -614,8 +649,8 @@ int build_and_probe(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned*
 
 int get_count(phj_ctx* c, uint64_t* out) {
     unsigned long long h = 0;
-    PHJ_HIP(c, hipMemcpyAsync(&h, c->count.p, 8, hipMemcpyDeviceToHost, c->stream));
-    PHJ_HIP(c, hipStreamSynchronize(c->stream));
+    PHJ_HIP(c, hipMemcpyAsync(&h, c->count.p, 8, hipMemcpyDeviceToHost, c->ks));
+    PHJ_HIP(c, hipStreamSynchronize(c->ks));
     *out = h;
     return PHJ_OK;
 }
@@ -641,31 +676,31 @@ int join_nopart(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
     const uint32_t nR = static_cast<uint32_t>(R.n);
     PHJ_TRY(mark(c, &e0));
     PHJ_TRY(timer_begin(c, "np.build", static_cast<uint64_t>(nR) * 32 + static_cast<uint64_t>(nb) * 64));
-    PHJ_HIP(c, hipMemsetAsync(c->np_tab.p, 0, static_cast<size_t>(nb) * sizeof(NPBucket), c->stream));
+    PHJ_HIP(c, hipMemsetAsync(c->np_tab.p, 0, static_cast<size_t>(nb) * sizeof(NPBucket), c->ks));
     const uint32_t bg = (nR + kBlock - 1) / kBlock;
     if (p->hash == PHJ_HASH_MURMUR3)
-        hipLaunchKernelGGL((k_np_build<kMurmur3>), dim3(bg), dim3(kBlock), 0, c->stream,
+        hipLaunchKernelGGL((k_np_build<kMurmur3>), dim3(bg), dim3(kBlock), 0, c->ks,
                            reinterpret_cast<const longlong2*>(R.rel), nR, static_cast<NPBucket*>(c->np_tab.p),
                            static_cast<int64_t*>(c->np_pays.p), nb, p->hash_seed);
     else
-        hipLaunchKernelGGL((k_np_build<kXXH3>), dim3(bg), dim3(kBlock), 0, c->stream,
+        hipLaunchKernelGGL((k_np_build<kXXH3>), dim3(bg), dim3(kBlock), 0, c->ks,
                            reinterpret_cast<const longlong2*>(R.rel), nR, static_cast<NPBucket*>(c->np_tab.p),
                            static_cast<int64_t*>(c->np_pays.p), nb, p->hash_seed);
     PHJ_LAUNCHED(c, "k_np_build");
     PHJ_TRY(timer_end(c));
     PHJ_TRY(mark(c, &e1));
-    PHJ_HIP(c, hipMemsetAsync(c->count.p, 0, 8, c->stream));
+    PHJ_HIP(c, hipMemsetAsync(c->count.p, 0, 8, c->ks));
     if (S.n > 0) {
         const uint64_t per = static_cast<uint64_t>(kBlock) * kNPProbeItems;
         const uint32_t pg = static_cast<uint32_t>(std::min<uint64_t>((S.n + per - 1) / per, 8192));
         PHJ_TRY(timer_begin(c, "np.probe", S.n * 16 + static_cast<uint64_t>(nb) * 64));
         if (p->hash == PHJ_HASH_MURMUR3)
-            hipLaunchKernelGGL((k_np_probe<kMurmur3, kNPProbeItems>), dim3(pg), dim3(kBlock), 0, c->stream,
+            hipLaunchKernelGGL((k_np_probe<kMurmur3, kNPProbeItems>), dim3(pg), dim3(kBlock), 0, c->ks,
                                reinterpret_cast<const longlong2*>(S.rel), S.n,
                                static_cast<const NPBucket*>(c->np_tab.p), nb, p->hash_seed,
                                static_cast<unsigned long long*>(c->count.p));
         else
-            hipLaunchKernelGGL((k_np_probe<kXXH3, kNPProbeItems>), dim3(pg), dim3(kBlock), 0, c->stream,
+            hipLaunchKernelGGL((k_np_probe<kXXH3, kNPProbeItems>), dim3(pg), dim3(kBlock), 0, c->ks,
                                reinterpret_cast<const longlong2*>(S.rel), S.n,
                                static_cast<const NPBucket*>(c->np_tab.p), nb, p->hash_seed,
                                static_cast<unsigned long long*>(c->count.p));
@@ -724,6 +759,12 @@ int phj_ctx_create(int device, phj_ctx** out) {
         delete c;
         return PHJ_ERR_HIP;
     }
+    if (hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess) {
+        (void)hipStreamDestroy(c->stream);
+        delete c;
+        return PHJ_ERR_HIP;
+    }
+    c->ks = c->stream;
     c->own_stream = true;
     {
         const int t = env_int("PHJ_TILE", 4096);
@@ -732,6 +773,12 @@ int phj_ctx_create(int device, phj_ctx** out) {
     c->tune.p1_aos = env_int("PHJ_P1_AOS", 0) != 0;
     c->tune.xcd_remap = env_int("PHJ_XCD_REMAP", 1) != 0;
     c->tune.wc = env_int("PHJ_WC", 0) != 0;
+    c->tune.r_aux = env_int("PHJ_R_AUX", 0) != 0;
+    c->tune.probe_items = env_int("PHJ_PROBE_ITEMS", 8) == 16 ? 16 : 8;
+    {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
+    }
     c->tune.wc_items = env_int("PHJ_WC_ITEMS", 8) == 4 ? 4 : 8;
     c->tune.wc_lw = env_int("PHJ_WC_LW", 8) == 16 ? 16 : 8;
     c->tune.wc_wgs = std::max(64, env_int("PHJ_WC_WGS", 1024));
@@ -747,15 +794,18 @@ void phj_ctx_destroy(phj_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamSynchronize(c->aux);
     for (SideState& S : c->side) {
-        for (DevBuf* b : {&S.owned, &S.kA, &S.pA, &S.kB, &S.pB, &S.hist1, &S.hist2, &S.bounds1, &S.tbase2, &S.bounds})
+        for (DevBuf* b : {&S.owned, &S.kA, &S.pA, &S.kB, &S.pB, &S.hist1, &S.hist2, &S.bounds1, &S.tbase2,
+                          &S.bounds, &S.partials, &S.tseg2})
             free_buf(*b);
     }
-    for (DevBuf* b : {&c->scan_partials, &c->prep, &c->tkeys, &c->tpays, &c->toffs, &c->gcursor, &c->items,
+    for (DevBuf* b : {&c->scan_partials, &c->prep, &c->tkeys, &c->tpays, &c->toffs, &c->gcursor, &c->items, &c->biglist,
                       &c->count, &c->np_tab, &c->np_pays})
         free_buf(*b);
     for (hipEvent_t e : c->evpool) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->stream);
+    (void)hipStreamDestroy(c->aux);
     delete c;
 }
 
@@ -765,6 +815,7 @@ int phj_ctx_set_stream(phj_ctx* c, void* stream) {
     if (!c) return PHJ_ERR_INVALID;
     PHJ_HIP(c, hipSetDevice(c->device));
     PHJ_HIP(c, hipStreamSynchronize(c->stream));
+    PHJ_HIP(c, hipStreamSynchronize(c->aux));
     if (c->own_stream) {
         PHJ_HIP(c, hipStreamDestroy(c->stream));
         c->own_stream = false;
@@ -775,11 +826,13 @@ int phj_ctx_set_stream(phj_ctx* c, void* stream) {
         PHJ_HIP(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
         c->own_stream = true;
     }
+    c->ks = c->stream;
     return PHJ_OK;
 }
 
 int phj_ctx_synchronize(phj_ctx* c) {
     if (!c) return PHJ_ERR_INVALID;
+    PHJ_HIP(c, hipStreamSynchronize(c->aux));
     PHJ_HIP(c, hipStreamSynchronize(c->stream));
     return PHJ_OK;
 }
@@ -792,8 +845,8 @@ int phj_relation_upload(phj_ctx* c, int side, const phj_tuple* host, uint64_t n)
     drop_relation(c, side);
     PHJ_TRY(ensure(c, S.owned, n * sizeof(phj_tuple)));
     if (n) {
-        PHJ_HIP(c, hipMemcpyAsync(S.owned.p, host, n * sizeof(phj_tuple), hipMemcpyHostToDevice, c->stream));
-        PHJ_HIP(c, hipStreamSynchronize(c->stream));
+        PHJ_HIP(c, hipMemcpyAsync(S.owned.p, host, n * sizeof(phj_tuple), hipMemcpyHostToDevice, c->ks));
+        PHJ_HIP(c, hipStreamSynchronize(c->ks));
     }
     S.rel = static_cast<const phj_tuple*>(S.owned.p);
     S.n = n;
@@ -822,8 +875,8 @@ int phj_relation_download(phj_ctx* c, int side, phj_tuple* host, uint64_t n) {
     if (n > S.n) return set_err(c, PHJ_ERR_INVALID, "download larger than the relation");
     PHJ_HIP(c, hipSetDevice(c->device));
     if (n) {
-        PHJ_HIP(c, hipMemcpyAsync(host, S.rel, n * sizeof(phj_tuple), hipMemcpyDeviceToHost, c->stream));
-        PHJ_HIP(c, hipStreamSynchronize(c->stream));
+        PHJ_HIP(c, hipMemcpyAsync(host, S.rel, n * sizeof(phj_tuple), hipMemcpyDeviceToHost, c->ks));
+        PHJ_HIP(c, hipStreamSynchronize(c->ks));
     }
     return PHJ_OK;
 }
@@ -836,10 +889,10 @@ int phj_relation_generate_sequential(phj_ctx* c, int side, uint64_t n, int64_t s
     PHJ_TRY(ensure(c, S.owned, n * sizeof(phj_tuple)));
     if (n) {
         const uint32_t g = static_cast<uint32_t>(std::min<uint64_t>((n + kBlock - 1) / kBlock, 65536));
-        hipLaunchKernelGGL(k_gen_sequential, dim3(g), dim3(kBlock), 0, c->stream, static_cast<longlong2*>(S.owned.p), n, start,
+        hipLaunchKernelGGL(k_gen_sequential, dim3(g), dim3(kBlock), 0, c->ks, static_cast<longlong2*>(S.owned.p), n, start,
                            first_index);
         PHJ_LAUNCHED(c, "k_gen_sequential");
-        PHJ_HIP(c, hipStreamSynchronize(c->stream));
+        PHJ_HIP(c, hipStreamSynchronize(c->ks));
     }
     S.rel = static_cast<const phj_tuple*>(S.owned.p);
     S.n = n;
@@ -858,10 +911,10 @@ int phj_relation_generate_zipf(phj_ctx* c, int side, uint64_t n, double alpha, i
     if (n) {
         const uint64_t b0 = first_index / kGenBatch, b1 = (first_index + n + kGenBatch - 1) / kGenBatch;
         const uint32_t g = static_cast<uint32_t>((b1 - b0 + kBlock - 1) / kBlock);
-        hipLaunchKernelGGL(k_gen_zipf, dim3(g), dim3(kBlock), 0, c->stream, static_cast<longlong2*>(S.owned.p), n,
+        hipLaunchKernelGGL(k_gen_zipf, dim3(g), dim3(kBlock), 0, c->ks, static_cast<longlong2*>(S.owned.p), n,
                            alpha, static_cast<uint64_t>(hi - lo + 1), lo - 1, seed, first_index);
         PHJ_LAUNCHED(c, "k_gen_zipf");
-        PHJ_HIP(c, hipStreamSynchronize(c->stream));
+        PHJ_HIP(c, hipStreamSynchronize(c->ks));
     }
     S.rel = static_cast<const phj_tuple*>(S.owned.p);
     S.n = n;
@@ -874,10 +927,10 @@ int phj_relation_count_in_range(phj_ctx* c, int side, int64_t lo, int64_t hi, ui
     PHJ_HIP(c, hipSetDevice(c->device));
     SideState& S = c->side[side];
     PHJ_TRY(ensure(c, c->count, 8));
-    PHJ_HIP(c, hipMemsetAsync(c->count.p, 0, 8, c->stream));
+    PHJ_HIP(c, hipMemsetAsync(c->count.p, 0, 8, c->ks));
     if (S.n) {
         const uint32_t g = static_cast<uint32_t>(std::min<uint64_t>((S.n + kBlock - 1) / kBlock, 8192));
-        hipLaunchKernelGGL(k_count_range, dim3(g), dim3(kBlock), 0, c->stream, reinterpret_cast<const longlong2*>(S.rel),
+        hipLaunchKernelGGL(k_count_range, dim3(g), dim3(kBlock), 0, c->ks, reinterpret_cast<const longlong2*>(S.rel),
                            S.n, lo, hi, static_cast<unsigned long long*>(c->count.p));
         PHJ_LAUNCHED(c, "k_count_range");
     }
@@ -938,10 +991,17 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
     PHJ_TRY(make_plan(c, p, pl));
     SideState& R = c->side[PHJ_SIDE_BUILD];
     SideState& S = c->side[PHJ_SIDE_PROBE];
-    hipEvent_t t0, t1, b0, b1, p1;
+    hipEvent_t t0, t1, tr, b0, b1, p1;
+    // Partition(R) || Partition(S) (HashJoin.hpp:210-216): R on the aux stream
     PHJ_TRY(mark(c, &t0));
-    PHJ_TRY(partition_side(c, PHJ_SIDE_BUILD, pl));
+    PHJ_HIP(c, hipStreamWaitEvent(c->aux, t0, 0));
+    c->ks = c->tune.r_aux ? c->aux : c->stream;
+    int rc = partition_side(c, PHJ_SIDE_BUILD, pl);
+    if (rc == PHJ_OK) rc = mark(c, &tr);
+    c->ks = c->stream;
+    PHJ_TRY(rc);
     PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, pl));
+    PHJ_HIP(c, hipStreamWaitEvent(c->stream, tr, 0));
     PHJ_TRY(mark(c, &t1));
     PHJ_TRY(build_and_probe(c, pl, 1, &R.view, &b0, &b1, &p1));
     uint64_t m = 0;
@@ -959,7 +1019,7 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
 int phj_timers_report(phj_ctx* c, phj_join_result* r) {
     if (!c || !r) return PHJ_ERR_INVALID;
     PHJ_HIP(c, hipSetDevice(c->device));
-    PHJ_HIP(c, hipStreamSynchronize(c->stream));
+    PHJ_HIP(c, hipStreamSynchronize(c->ks));
     std::memset(r, 0, sizeof(*r));
     const int rc = fill_timers(c, r);
     reset_timers(c);
@@ -970,12 +1030,12 @@ int phj_partitioned_download(phj_ctx* c, const phj_partitioned* v, int64_t* keys
                              uint32_t* bounds) {
     if (!c || !v) return PHJ_ERR_INVALID;
     PHJ_HIP(c, hipSetDevice(c->device));
-    if (v->n && keys) PHJ_HIP(c, hipMemcpyAsync(keys, v->keys, v->n * 8, hipMemcpyDefault, c->stream));
-    if (v->n && payloads) PHJ_HIP(c, hipMemcpyAsync(payloads, v->payloads, v->n * 8, hipMemcpyDefault, c->stream));
+    if (v->n && keys) PHJ_HIP(c, hipMemcpyAsync(keys, v->keys, v->n * 8, hipMemcpyDefault, c->ks));
+    if (v->n && payloads) PHJ_HIP(c, hipMemcpyAsync(payloads, v->payloads, v->n * 8, hipMemcpyDefault, c->ks));
     if (bounds)
         PHJ_HIP(c, hipMemcpyAsync(bounds, v->bounds, (static_cast<size_t>(v->num_partitions) + 1) * 4,
-                                  hipMemcpyDefault, c->stream));
-    PHJ_HIP(c, hipStreamSynchronize(c->stream));
+                                  hipMemcpyDefault, c->ks));
+    PHJ_HIP(c, hipStreamSynchronize(c->ks));
     return PHJ_OK;
 }
 
@@ -997,11 +1057,11 @@ int phj_hash_keys(phj_ctx* c, int hash, uint64_t seed, const int64_t* keys, uint
         if (hipMemcpy(dk, keys, n * 8, hipMemcpyHostToDevice) != hipSuccess) { rc = set_err(c, PHJ_ERR_HIP, "H2D"); break; }
         const uint32_t g = static_cast<uint32_t>((n + kBlock - 1) / kBlock);
         if (hash == PHJ_HASH_MURMUR3)
-            hipLaunchKernelGGL((k_hash_keys<kMurmur3>), dim3(g), dim3(kBlock), 0, c->stream, static_cast<int64_t*>(dk), n, seed, static_cast<uint64_t*>(dout));
+            hipLaunchKernelGGL((k_hash_keys<kMurmur3>), dim3(g), dim3(kBlock), 0, c->ks, static_cast<int64_t*>(dk), n, seed, static_cast<uint64_t*>(dout));
         else
-            hipLaunchKernelGGL((k_hash_keys<kXXH3>), dim3(g), dim3(kBlock), 0, c->stream, static_cast<int64_t*>(dk), n, seed, static_cast<uint64_t*>(dout));
+            hipLaunchKernelGGL((k_hash_keys<kXXH3>), dim3(g), dim3(kBlock), 0, c->ks, static_cast<int64_t*>(dk), n, seed, static_cast<uint64_t*>(dout));
         if (hipGetLastError() != hipSuccess) { rc = set_err(c, PHJ_ERR_HIP, "k_hash_keys launch"); break; }
-        if (hipStreamSynchronize(c->stream) != hipSuccess) { rc = set_err(c, PHJ_ERR_HIP, "sync"); break; }
+        if (hipStreamSynchronize(c->ks) != hipSuccess) { rc = set_err(c, PHJ_ERR_HIP, "sync"); break; }
         if (hipMemcpy(out, dout, n * 8, hipMemcpyDeviceToHost) != hipSuccess) { rc = set_err(c, PHJ_ERR_HIP, "D2H"); break; }
     } while (0);
     (void)hipFree(dk);

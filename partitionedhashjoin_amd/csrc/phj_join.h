@@ -84,14 +84,38 @@ __global__ __launch_bounds__(kBlock) void k_join_prep(SegList L, const uint32_t*
     arr[2 * stride + p] = (m && s) ? (s + chunk - 1) / chunk : 0u;
 }
 
+// A probe work item: one S chunk of one partition plus where that partition's
+// table lives, so a probing workgroup needs a single 32-B descriptor load.
+struct ProbeItem {
+    uint32_t s_lo, s_cnt;   // S keys [s_lo, s_lo + s_cnt)
+    uint32_t kb, m;         // table keys [kb, kb + m)
+    uint32_t ob, nbk;       // bucket offsets [ob, ob + nbk]
+    uint32_t pad0, pad1;
+};
+
 // One wave per partition writes its (partition, chunk) work items.
-__global__ __launch_bounds__(kBlock) void k_items_expand(const uint32_t* itb, uint32_t P,
-                                                         uint2* items) {
+__global__ __launch_bounds__(kBlock) void k_items_expand(const uint32_t* itb, const uint32_t* tkb,
+                                                         const uint32_t* tob, const uint32_t* sbounds,
+                                                         uint32_t P, uint32_t chunk, ProbeItem* items) {
     const uint32_t p = blockIdx.x * kWaves + (threadIdx.x >> 6);
     if (p >= P) return;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t lo = itb[p], hi = itb[p + 1];
-    for (uint32_t i = lo + lane; i < hi; i += 64) items[i] = make_uint2(p, i - lo);
+    if (lo == hi) return;
+    const uint32_t kb = tkb[p], m = tkb[p + 1] - kb;
+    const uint32_t ob = tob[p], nbk = tob[p + 1] - ob - 1;
+    const uint32_t sb = sbounds[p], se = sbounds[p + 1];
+    for (uint32_t i = lo + lane; i < hi; i += 64) {
+        ProbeItem it;
+        it.s_lo = sb + (i - lo) * chunk;
+        it.s_cnt = min(chunk, se - it.s_lo);
+        it.kb = kb;
+        it.m = m;
+        it.ob = ob;
+        it.nbk = nbk;
+        it.pad0 = it.pad1 = 0;
+        items[i] = it;
+    }
 }
 
 struct BuildArgs {
@@ -102,10 +126,82 @@ struct BuildArgs {
     int64_t* tpays;
     uint32_t* toffs;
     uint32_t* gcursor;     // global cursors for partitions beyond the LDS capacity
-    uint32_t ocap;         // LDS bucket-counter capacity
+    uint32_t* biglist;     // partitions left to k_build_big
+    uint32_t* bigcount;    // (zeroed before k_build_small)
+    uint32_t ocap;         // LDS bucket-counter capacity (per wave in k_build_small)
     uint32_t pad;
     uint64_t seed;
 };
+
+// LDS ordering between lanes of one wave (stores before loads of other lanes).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// One wave per partition: bucket counting sort of R_p in the wave's LDS slice
+// (the common case: R_p ~ |R| / P tuples). Partitions whose bucket array does
+// not fit are appended to biglist for k_build_big.
+template <int HK>
+__global__ __launch_bounds__(kBlock) void k_build_small(BuildArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(smem) + wave * a.ocap;
+    const uint32_t P = a.L.P;
+    const uint32_t nw = gridDim.x * kWaves;
+    for (uint32_t p = blockIdx.x * kWaves + wave; p < P; p += nw) {
+        const uint32_t kb = a.tkb[p], m = a.tkb[p + 1] - kb;
+        const uint32_t ob = a.tob[p], nbk = a.tob[p + 1] - ob - 1;
+        uint32_t* offs = a.toffs + ob;
+        if (m == 0) {
+            for (uint32_t i = lane; i <= nbk; i += 64) offs[i] = 0;
+            continue;
+        }
+        if (nbk > a.ocap) {
+            if (lane == 0) a.biglist[atomicAdd(a.bigcount, 1u)] = p;
+            continue;
+        }
+        for (uint32_t i = lane; i < nbk; i += 64) cnt[i] = 0;
+        wave_lds_sync();
+        for (uint32_t g = 0; g < a.L.nseg; g++) {
+            const Seg& S = a.L.seg[g];
+            const uint32_t lo = S.bounds[p], c = S.bounds[p + 1] - lo;
+            for (uint32_t i = lane; i < c; i += 64)
+                atomicAdd(&cnt[bucket_of(hash64<HK>(static_cast<uint64_t>(S.keys[lo + i]), a.seed), nbk)], 1u);
+        }
+        wave_lds_sync();
+        uint32_t carry = 0;
+        for (uint32_t base = 0; base < nbk; base += 64) {
+            const uint32_t i = base + lane;
+            const uint32_t v = i < nbk ? cnt[i] : 0u;
+            uint32_t x = v;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(x, o, 64);
+                if (lane >= (uint32_t)o) x += y;
+            }
+            if (i < nbk) {
+                cnt[i] = carry + x - v;
+                offs[i] = carry + x - v;
+            }
+            carry += __shfl(x, 63, 64);
+        }
+        if (lane == 0) offs[nbk] = m;
+        wave_lds_sync();
+        for (uint32_t g = 0; g < a.L.nseg; g++) {
+            const Seg& S = a.L.seg[g];
+            const uint32_t lo = S.bounds[p], c = S.bounds[p + 1] - lo;
+            for (uint32_t i = lane; i < c; i += 64) {
+                const int64_t key = S.keys[lo + i];
+                const uint32_t b = bucket_of(hash64<HK>(static_cast<uint64_t>(key), a.seed), nbk);
+                const uint32_t pos = atomicAdd(&cnt[b], 1u);
+                a.tkeys[kb + pos] = key;
+                a.tpays[kb + pos] = S.pays[lo + i];
+            }
+        }
+        wave_lds_sync();
+    }
+}
 
 // Block-wide in-place exclusive scan of arr[0..len) (LDS or global via pointer
 // kind); also writes the result to out[0..len) and out[len] = total.
@@ -122,13 +218,16 @@ __device__ __forceinline__ void block_scan_array(uint32_t len, LoadF ld, StoreF 
     }
 }
 
+// One workgroup per partition of biglist (bucket arrays beyond a wave's LDS
+// slice): LDS counters up to ocap buckets, global atomics beyond.
 template <int HK>
-__global__ __launch_bounds__(kBlock) void k_build(BuildArgs a) {
+__global__ __launch_bounds__(kBlock) void k_build_big(BuildArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint32_t* tmp = reinterpret_cast<uint32_t*>(smem);        // 16 words
     uint32_t* lcnt = tmp + 16;                                // ocap words
-    const uint32_t P = a.L.P;
-    for (uint32_t p = blockIdx.x; p < P; p += gridDim.x) {
+    const uint32_t nbig = *a.bigcount;
+    for (uint32_t bi = blockIdx.x; bi < nbig; bi += gridDim.x) {
+        const uint32_t p = a.biglist[bi];
         const uint32_t kb = a.tkb[p], m = a.tkb[p + 1] - kb;
         const uint32_t ob = a.tob[p], nbk = a.tob[p + 1] - ob - 1;
         uint32_t* offs = a.toffs + ob;
@@ -198,31 +297,42 @@ __global__ __launch_bounds__(kBlock) void k_build(BuildArgs a) {
 
 struct ProbeArgs {
     const int64_t* skeys;
-    const uint32_t* sbounds;
-    const uint32_t* tkb;
-    const uint32_t* tob;
     const int64_t* tkeys;
     const uint32_t* toffs;
-    const uint2* items;
+    const ProbeItem* items;
     const uint32_t* nitems;   // device scalar (itb[P])
     unsigned long long* count;
-    uint32_t kcap;            // LDS staging capacity: keys
-    uint32_t ocap;            // LDS staging capacity: bucket offsets (NB + 1)
     uint64_t seed;
 };
 
+// Probe ITEMS keys per lane in phases so the table reads of all keys are in
+// flight together: bucket bounds, then each bucket's first key, then (rarely)
+// the rest of a bucket. A key counts once (first match, LinearProbing.hpp:160-180).
 template <int HK, int ITEMS, typename KP, typename OP>
 __device__ __forceinline__ uint32_t probe_keys(const int64_t (&k)[ITEMS], uint32_t valid_n,
                                                KP K, OP O, uint32_t nbk, uint64_t seed) {
-    uint32_t hits = 0;
+    uint32_t lo[ITEMS], hi[ITEMS];
 #pragma unroll
     for (int j = 0; j < ITEMS; j++) {
-        if (static_cast<uint32_t>(j * kBlock) + threadIdx.x < valid_n) {
-            const uint64_t h = hash64<HK>(static_cast<uint64_t>(k[j]), seed);
-            const uint32_t b = bucket_of(h, nbk);
-            uint32_t t = O[b];
-            const uint32_t e = O[b + 1];
-            for (; t < e; t++) {
+        const bool v = static_cast<uint32_t>(j * kBlock) + threadIdx.x < valid_n;
+        const uint32_t b = bucket_of(hash64<HK>(static_cast<uint64_t>(k[j]), seed), nbk);
+        lo[j] = v ? O[b] : 0u;
+        hi[j] = v ? O[b + 1] : 0u;
+    }
+    uint32_t hits = 0;
+    bool more = false;
+#pragma unroll
+    for (int j = 0; j < ITEMS; j++) {
+        const bool nonempty = lo[j] < hi[j];
+        const bool hit = nonempty && K[nonempty ? lo[j] : 0] == k[j];
+        hits += hit;
+        lo[j] = hit ? hi[j] : lo[j] + 1;   // consumed
+        more |= lo[j] < hi[j];
+    }
+    if (more) {
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            for (uint32_t t = lo[j]; t < hi[j]; t++) {
                 if (K[t] == k[j]) {
                     hits++;
                     break;
@@ -233,46 +343,99 @@ __device__ __forceinline__ uint32_t probe_keys(const int64_t (&k)[ITEMS], uint32
     return hits;
 }
 
-template <int HK, int ITEMS>
+__device__ __forceinline__ ProbeItem load_item(const ProbeItem* items, uint32_t i, uint32_t n) {
+    ProbeItem it{};
+    if (i < n) {
+        const uint4* q = reinterpret_cast<const uint4*>(items + i);
+        const uint4 x = q[0], y = q[1];
+        it.s_lo = x.x;
+        it.s_cnt = x.y;
+        it.kb = x.z;
+        it.m = x.w;
+        it.ob = y.x;
+        it.nbk = y.y;
+    }
+    return it;
+}
+
+// Persistent probe over work items, software-pipelined one item deep: while
+// item i is probed from LDS, item i+1's S keys and table slice (KPT keys and
+// OPT bucket offsets per lane) are already in flight into registers, and the
+// descriptor of item i+2 is being fetched. Tables larger than the LDS slice
+// (KPT * 256 keys) are probed in place from global memory (L2-resident).
+template <int HK, int ITEMS, int KPT>
 __global__ __launch_bounds__(kBlock) void k_probe(ProbeArgs a) {
-    constexpr uint32_t C = kBlock * ITEMS;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    int64_t* lk = reinterpret_cast<int64_t*>(smem);
-    uint32_t* lo = reinterpret_cast<uint32_t*>(lk + a.kcap);
+    constexpr uint32_t KCAP = kBlock * KPT;        // staged table keys
+    constexpr int OPT = KPT / 2 + 1;               // staged bucket offsets per lane
+    constexpr uint32_t OCAP = kBlock * OPT;
+    __shared__ int64_t lk[KCAP];
+    __shared__ uint32_t lo[OCAP];
     __shared__ uint32_t red[kWaves];
-    const uint32_t nitems = *a.nitems;
+    const uint32_t n = *a.nitems;
+    const uint32_t G = gridDim.x, tid = threadIdx.x;
     uint32_t hits = 0;
-    for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
-        const uint2 it = a.items[item];
-        const uint32_t p = it.x;
-        const uint32_t kb = a.tkb[p], m = a.tkb[p + 1] - kb;
-        const uint32_t ob = a.tob[p], nbk = a.tob[p + 1] - ob - 1;
-        const uint32_t s_lo = a.sbounds[p] + it.y * C;
-        const uint32_t s_hi = min(a.sbounds[p + 1], s_lo + C);
-        const uint32_t valid_n = s_hi - s_lo;
-        int64_t k[ITEMS];
+
+    uint32_t item = blockIdx.x;
+    ProbeItem cur = load_item(a.items, item, n);
+    ProbeItem nxt = load_item(a.items, item + G, n);
+    int64_t k[ITEMS], tk[KPT];
+    uint32_t to[OPT];
+    auto fetch = [&](const ProbeItem& it, int64_t (&kk)[ITEMS], int64_t (&tkk)[KPT], uint32_t (&too)[OPT]) {
 #pragma unroll
         for (int j = 0; j < ITEMS; j++) {
-            const uint32_t off = j * kBlock + threadIdx.x;
-            k[j] = off < valid_n ? a.skeys[s_lo + off] : 0;
+            const uint32_t off = j * kBlock + tid;
+            kk[j] = off < it.s_cnt ? a.skeys[it.s_lo + off] : 0;
         }
-        if (m <= a.kcap && nbk + 1 <= a.ocap) {
-            for (uint32_t i = threadIdx.x; i < m; i += kBlock) lk[i] = a.tkeys[kb + i];
-            for (uint32_t i = threadIdx.x; i <= nbk; i += kBlock) lo[i] = a.toffs[ob + i];
-            __syncthreads();
-            hits += probe_keys<HK, ITEMS>(k, valid_n, lk, lo, nbk, a.seed);
-            __syncthreads();
+        const bool stage = it.m <= KCAP && it.nbk + 1 <= OCAP;
+#pragma unroll
+        for (int j = 0; j < KPT; j++) {
+            const uint32_t i = j * kBlock + tid;
+            tkk[j] = (stage && i < it.m) ? a.tkeys[it.kb + i] : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < OPT; j++) {
+            const uint32_t i = j * kBlock + tid;
+            too[j] = (stage && i <= it.nbk) ? a.toffs[it.ob + i] : 0u;
+        }
+    };
+    if (item < n) fetch(cur, k, tk, to);
+    for (; item < n; item += G) {
+        const bool stage = cur.m <= KCAP && cur.nbk + 1 <= OCAP;
+        if (stage) {
+#pragma unroll
+            for (int j = 0; j < KPT; j++) {
+                const uint32_t i = j * kBlock + tid;
+                if (i < cur.m) lk[i] = tk[j];
+            }
+#pragma unroll
+            for (int j = 0; j < OPT; j++) {
+                const uint32_t i = j * kBlock + tid;
+                if (i <= cur.nbk) lo[i] = to[j];
+            }
+        }
+        __syncthreads();
+        // keep the probe keys of this item; start the next item's loads
+        int64_t kc[ITEMS];
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) kc[j] = k[j];
+        const ProbeItem nn = load_item(a.items, item + 2 * G, n);
+        if (item + G < n) fetch(nxt, k, tk, to);
+        if (stage) {
+            hits += probe_keys<HK, ITEMS>(kc, cur.s_cnt, lk, lo, cur.nbk, a.seed);
         } else {
-            hits += probe_keys<HK, ITEMS>(k, valid_n, a.tkeys + kb, a.toffs + ob, nbk, a.seed);
+            hits += probe_keys<HK, ITEMS>(kc, cur.s_cnt, a.tkeys + cur.kb, a.toffs + cur.ob, cur.nbk, a.seed);
         }
+        __syncthreads();
+        cur = nxt;
+        nxt = nn;
     }
     // block reduce -> one atomic per workgroup
     uint32_t x = hits;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) x += __shfl_down(x, o, 64);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = x;
+    if ((tid & 63) == 0) red[tid >> 6] = x;
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (tid == 0) {
         unsigned long long t = 0;
         for (int w = 0; w < kWaves; w++) t += red[w];
         if (t) atomicAdd(a.count, t);

@@ -66,6 +66,7 @@ struct PassArgs {
     uint32_t* hist;             // [seg][digit][tile]; scanned in place between the kernels
     const uint32_t* seg_bounds; // nseg+1 input offsets; nullptr = one segment [0, n)
     const uint32_t* tile_base;  // nseg+1 cumulative tile counts (segmented passes)
+    const uint32_t* tile_seg;   // tile -> segment (segmented passes)
     uint32_t nseg;
     uint32_t n;
     uint32_t ntiles1;           // tiles of the single-segment case
@@ -102,12 +103,7 @@ __device__ __forceinline__ bool locate_tile_rt(const PassArgs& a, uint32_t tile,
     }
     const uint32_t total = a.tile_base[a.nseg];
     if (tile >= total) return false;
-    uint32_t l = 0, r = a.nseg;  // tile_base[l] <= tile < tile_base[r]
-    while (r - l > 1) {
-        const uint32_t m = (l + r) >> 1;
-        if (a.tile_base[m] <= tile) l = m;
-        else r = m;
-    }
+    const uint32_t l = a.tile_seg[tile];
     L.tb_s = a.tile_base[l];
     L.tseg = tile - L.tb_s;
     L.ntiles_s = a.tile_base[l + 1] - L.tb_s;
@@ -135,6 +131,19 @@ __device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid, uint32_t
         m &= bit ? bb : ~bb;
     }
     return m;
+}
+
+// Count digit d of this lane (if valid) into the wave's LDS row. Lanes that
+// share the first active lane's digit are counted with one add (the common
+// case under key skew, where a plain LDS atomic would serialise 64-way).
+__device__ __forceinline__ void count_digit(uint32_t* row, uint32_t d, bool valid) {
+    const uint64_t act = __ballot(valid);
+    if (act == 0) return;
+    const uint32_t first = __builtin_amdgcn_readlane(d, __builtin_ctzll(act));
+    const uint64_t same = __ballot(valid && d == first);
+    const uint32_t lane = threadIdx.x & 63;
+    if (valid && d != first) atomicAdd(&row[d], 1u);
+    if (lane == static_cast<uint32_t>(__builtin_ctzll(act))) atomicAdd(&row[first], static_cast<uint32_t>(__popcll(same)));
 }
 
 // Exclusive scan of one value per thread across a block of NW waves.
@@ -191,30 +200,47 @@ __global__ __launch_bounds__(BLOCK) void k_hist(PassArgs a) {
     const uint32_t nb = a.nbins;
     const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     for (uint32_t i = tid; i < NW * nb; i += BLOCK) wcnt[i] = 0;
-    const uint32_t cnt = L.hi - L.lo;
-    int64_t key[ITEMS];
-    const uint32_t wbase = wave * 64 * ITEMS;
+    uint32_t* my = wcnt + wave * nb;
+    // Order does not matter for a histogram, so every lane loads 16 B (one AoS
+    // tuple, or two consecutive keys of a SoA key column: aligned pairs) and
+    // counts into its wave's private LDS row (count_digit).
+    if constexpr (AOS) {
+        const uint32_t cnt = L.hi - L.lo;
+        int64_t key[ITEMS];
+        const uint32_t wbase = wave * 64 * ITEMS;
 #pragma unroll
-    for (int i = 0; i < ITEMS; i++) {
-        const uint32_t e = wbase + i * 64 + lane;
-        key[i] = 0;
-        if (e < cnt) {
-            if constexpr (AOS) {
-                key[i] = reinterpret_cast<const longlong2*>(a.in_keys)[L.lo + e].x;
-            } else {
-                key[i] = a.in_keys[L.lo + e];
+        for (int i = 0; i < ITEMS; i++) {
+            const uint32_t e = wbase + i * 64 + lane;
+            key[i] = e < cnt ? reinterpret_cast<const longlong2*>(a.in_keys)[L.lo + e].x : 0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < ITEMS; i++) {
+            const uint32_t e = wbase + i * 64 + lane;
+            const bool valid = e < cnt;
+            count_digit(my, valid ? digit_of<HK>(static_cast<uint64_t>(key[i]), a.f) : 0u, valid);
+        }
+    } else {
+        constexpr int NP = ITEMS / 2 + 1;   // aligned pairs covering [lo, hi)
+        const uint32_t plo = L.lo >> 1, phi = (L.hi + 1) >> 1;
+        longlong2 kp[NP];
+#pragma unroll
+        for (int i = 0; i < NP; i++) {
+            const uint32_t pi = plo + i * BLOCK + tid;
+            kp[i] = pi < phi ? reinterpret_cast<const longlong2*>(a.in_keys)[pi] : make_longlong2(0, 0);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < NP; i++) {
+            const uint32_t e0 = 2 * (plo + i * BLOCK + tid);
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const uint32_t e = e0 + h;
+                const int64_t k = h ? kp[i].y : kp[i].x;
+                const bool valid = e >= L.lo && e < L.hi;
+                count_digit(my, valid ? digit_of<HK>(static_cast<uint64_t>(k), a.f) : 0u, valid);
             }
         }
-    }
-    __syncthreads();
-    uint32_t* my = wcnt + wave * nb;
-#pragma unroll
-    for (int i = 0; i < ITEMS; i++) {
-        const uint32_t e = wbase + i * 64 + lane;
-        const bool valid = e < cnt;
-        const uint32_t d = valid ? digit_of<HK>(static_cast<uint64_t>(key[i]), a.f) : 0u;
-        const uint64_t peers = match_digit(d, valid, a.nbits);
-        if (valid && (peers & lanemask_lt()) == 0) my[d] += __popcll(peers);
     }
     __syncthreads();
     uint32_t* out = a.hist + static_cast<size_t>(L.tb_s) * nb + L.tseg;
@@ -359,68 +385,88 @@ __global__ __launch_bounds__(kBlock) void k_scan_reduce(ScanArgs s) {
     const uint32_t* d = s.data + static_cast<size_t>(blockIdx.y) * s.stride;
     const uint32_t base = blockIdx.x * kScanBlockElems;
     uint32_t acc = 0;
+    if (base + kScanBlockElems <= s.len && (reinterpret_cast<uintptr_t>(d) & 15) == 0) {
+        const uint4* q = reinterpret_cast<const uint4*>(d + base);   // 16 B per lane, coalesced
 #pragma unroll
-    for (int i = 0; i < kScanItems; i++) {
-        const uint32_t idx = base + i * kBlock + threadIdx.x;
-        if (idx < s.len) acc += d[idx];
+        for (int i = 0; i < kScanItems / 4; i++) {
+            const uint4 v = q[i * kBlock + threadIdx.x];
+            acc += v.x + v.y + v.z + v.w;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < kScanItems; i++) {
+            const uint32_t idx = base + i * kBlock + threadIdx.x;
+            if (idx < s.len) acc += d[idx];
+        }
     }
     uint32_t total;
     block_exclusive_scan(acc, tmp, total);
     if (threadIdx.x == 0) s.partials[blockIdx.y * s.nblk + blockIdx.x] = total;
 }
 
-// One block per array: exclusive scan of the block partials.
-__global__ __launch_bounds__(1024) void k_scan_partials(ScanArgs s) {
-    __shared__ uint32_t wsum[16];
-    __shared__ uint32_t carry;
-    uint32_t* p = s.partials + blockIdx.y * s.nblk;
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (tid == 0) carry = 0;
-    __syncthreads();
-    for (uint32_t base = 0; base < s.nblk; base += 1024) {
-        const uint32_t idx = base + tid;
-        const uint32_t v = idx < s.nblk ? p[idx] : 0u;
-        uint32_t x = v;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(x, o, 64);
-            if (lane >= (uint32_t)o) x += y;
-        }
-        if (lane == 63) wsum[wave] = x;
-        __syncthreads();
-        uint32_t before = 0, all = 0;
-        for (int w = 0; w < 16; w++) {
-            const uint32_t t = wsum[w];
-            if (w < (int)wave) before += t;
-            all += t;
-        }
-        const uint32_t c = carry;
-        if (idx < s.nblk) p[idx] = c + before + x - v;
-        __syncthreads();
-        if (tid == 0) carry = c + all;
-        __syncthreads();
-    }
-}
-
+// k_scan_apply: per block, exclusive scan of its elements plus the sum of all
+// preceding blocks' partials (read directly; no separate partials-scan kernel).
 __global__ __launch_bounds__(kBlock) void k_scan_apply(ScanArgs s) {
     __shared__ uint32_t tmp[16];
     uint32_t* d = s.data + static_cast<size_t>(blockIdx.y) * s.stride;
     const uint32_t base = blockIdx.x * kScanBlockElems + threadIdx.x * kScanItems;
+    const bool vec = (reinterpret_cast<uintptr_t>(d) & 15) == 0 && base + kScanItems <= s.len;
     uint32_t v[kScanItems];
     uint32_t acc = 0;
+    if (vec) {
+        const uint4* q = reinterpret_cast<const uint4*>(d + base);
 #pragma unroll
-    for (int i = 0; i < kScanItems; i++) {
-        const uint32_t idx = base + i;
-        v[i] = idx < s.len ? d[idx] : 0u;
-        acc += v[i];
+        for (int i = 0; i < kScanItems / 4; i++) {
+            const uint4 t = q[i];
+            v[4 * i] = t.x;
+            v[4 * i + 1] = t.y;
+            v[4 * i + 2] = t.z;
+            v[4 * i + 3] = t.w;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < kScanItems; i++) {
+            const uint32_t idx = base + i;
+            v[i] = idx < s.len ? d[idx] : 0u;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < kScanItems; i++) acc += v[i];
+    // prefix of the preceding blocks' sums (L2-resident, <= a few thousand words)
+    __shared__ uint32_t pre;
+    {
+        const uint32_t* pp = s.partials + blockIdx.y * s.nblk;
+        uint32_t x = 0;
+        for (uint32_t i = threadIdx.x; i < blockIdx.x; i += kBlock) x += pp[i];
+        uint32_t t;
+        block_exclusive_scan(x, tmp, t);
+        if (threadIdx.x == 0) pre = t;
+        __syncthreads();
     }
     uint32_t total;
-    uint32_t run = block_exclusive_scan(acc, tmp, total) + s.partials[blockIdx.y * s.nblk + blockIdx.x];
+    uint32_t run = block_exclusive_scan(acc, tmp, total) + pre;
+    if (vec) {
+        uint4* q = reinterpret_cast<uint4*>(d + base);
 #pragma unroll
-    for (int i = 0; i < kScanItems; i++) {
-        const uint32_t idx = base + i;
-        if (idx < s.len) d[idx] = run;
-        run += v[i];
+        for (int i = 0; i < kScanItems / 4; i++) {
+            uint4 t;
+            t.x = run;
+            run += v[4 * i];
+            t.y = run;
+            run += v[4 * i + 1];
+            t.z = run;
+            run += v[4 * i + 2];
+            t.w = run;
+            run += v[4 * i + 3];
+            q[i] = t;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < kScanItems; i++) {
+            const uint32_t idx = base + i;
+            if (idx < s.len) d[idx] = run;
+            run += v[i];
+        }
     }
 }
 
@@ -466,6 +512,15 @@ __global__ __launch_bounds__(1024) void k_pass1_finish(const uint32_t* hist, uin
         __syncthreads();
     }
     if (tid == 0) tile_base2[nb] = carry;
+}
+
+// tile_seg[t] = s for every tile t of segment s (one wave per segment).
+__global__ __launch_bounds__(kBlock) void k_tile_seg(const uint32_t* tile_base, uint32_t nseg,
+                                                     uint32_t* tile_seg) {
+    const uint32_t s = blockIdx.x * kWaves + (threadIdx.x >> 6);
+    if (s >= nseg) return;
+    const uint32_t lo = tile_base[s], hi = tile_base[s + 1];
+    for (uint32_t t = lo + (threadIdx.x & 63); t < hi; t += 64) tile_seg[t] = s;
 }
 
 // Final bounds after a segmented pass 2: bounds[s * nb2 + d].

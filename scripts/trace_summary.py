@@ -1,0 +1,49 @@
+#!/usr/bin/env python3
+"""Summarise a rocprofv3 --kernel-trace CSV: per-kernel average duration and,
+for the last bench step, the device timeline (start offsets and gaps).
+
+  python scripts/trace_summary.py <dir with *_kernel_trace.csv> [--step-kernel k_probe]
+"""
+import csv
+import glob
+import os
+import sys
+from collections import defaultdict
+
+
+def main():
+    d = sys.argv[1]
+    files = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
+    if not files:
+        raise SystemExit(f"no kernel_trace.csv under {d}")
+    rows = []
+    for f in files:
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+    rows.sort()
+    stats = defaultdict(list)
+    for s, e, n in rows:
+        stats[n.split("(")[0][:90]].append((e - s) / 1e3)
+    print(f"{'kernel':92s} {'calls':>6s} {'avg_us':>9s} {'total_us':>10s}")
+    for n, v in sorted(stats.items(), key=lambda kv: -sum(kv[1])):
+        print(f"{n:92s} {len(v):6d} {sum(v) / len(v):9.1f} {sum(v):10.1f}")
+    # timeline of the last step: from the last k_hist launch preceding the last k_probe
+    probes = [i for i, r in enumerate(rows) if "k_probe" in r[2]]
+    if probes:
+        last = probes[-1]
+        first = last
+        while first > 0 and rows[first - 1][0] > rows[last][0] - 20_000_000 and "k_probe" not in rows[first - 1][2]:
+            first -= 1
+        t0 = rows[first][0]
+        print("\nlast step timeline (us): start  dur  gap-before  kernel")
+        prev_end = None
+        for s, e, n in rows[first:last + 1]:
+            gap = (s - prev_end) / 1e3 if prev_end is not None else 0.0
+            print(f"{(s - t0) / 1e3:9.1f} {(e - s) / 1e3:8.1f} {gap:8.1f}  {n.split('(')[0][:70]}")
+            prev_end = e if prev_end is None else max(prev_end, e)
+        print(f"step span: {(rows[last][1] - t0) / 1e3:.1f} us")
+
+
+if __name__ == "__main__":
+    main()

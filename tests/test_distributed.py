@@ -1,0 +1,142 @@
+"""Multi-rank orchestration (partitionedhashjoin_amd/distributed.py) over gloo
+on CPU: range sharding, partitioned build-shard all-gather, per-rank join,
+count all-reduce. A test-only engine computes each rank's partitions with the
+oracle, so this exercises exactly the collective layout the HIP engine uses
+(fixed-size padded shards, per-shard partition bounds) without a GPU."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import partitionedhashjoin_amd as phj
+from oracle import oracle as O
+from partitionedhashjoin_amd.distributed import (distributed_join, gathered_segments_numpy,
+                                                 max_shard, shard_range)
+
+
+class _View:
+    def __init__(self, keys, pays, bounds, P):
+        self.keys, self.pays, self.bounds = keys, pays, bounds
+        self.n = keys.shape[0]
+        self.num_partitions = P
+
+
+class _Res:
+    def __init__(self, matches):
+        self.matches = matches
+        self.build_ms = self.probe_ms = 0.0
+
+    def timers(self):
+        return []
+
+
+class OracleShardEngine:
+    """CPU stand-in for HipShardEngine with the same interface (test infrastructure)."""
+
+    def __init__(self, R, S):
+        self.torch = torch
+        self.rel = {0: R, 1: S}
+        self.views = {}
+
+    @staticmethod
+    def _geometry(p):
+        if p.num_partitions:
+            return int(p.num_partitions), False
+        return 1 << (p.radix_bits[0] + p.radix_bits[1]), True
+
+    def tensor(self, n, dtype):
+        return torch.zeros(int(n), dtype=dtype)
+
+    def partition(self, side, params):
+        P, radix = self._geometry(params)
+        out, bounds = O.partition(self.rel[side], P, radix, params.hash, params.hash_seed, workers=2)
+        v = _View(out[:, 0].copy(), out[:, 1].copy(), bounds, P)
+        self.views[side] = v
+        return v
+
+    def export(self, v, maxn):
+        keys, pays = torch.zeros(maxn, dtype=torch.int64), torch.zeros(maxn, dtype=torch.int64)
+        keys[:v.n] = torch.from_numpy(v.keys)
+        pays[:v.n] = torch.from_numpy(v.pays)
+        return keys, pays, torch.from_numpy(v.bounds.astype(np.int64)).to(torch.int32)
+
+    def _count(self, params, segs):
+        P, radix = self._geometry(params)
+        for keys, pays, bounds in segs:
+            # every gathered shard arrives partition-major with consistent bounds
+            q = O.partition_ids(keys, P, radix, params.hash, params.hash_seed).astype(np.int64)
+            expect = np.repeat(np.arange(P), np.diff(bounds.astype(np.int64)))
+            assert np.array_equal(q, expect)
+        rkeys = np.concatenate([k for k, _, _ in segs]) if segs else np.zeros(0, dtype=np.int64)
+        return _Res(O.semijoin_count_keys(rkeys, self.views[1].keys))
+
+    def join_gathered(self, params, keys_all, pays_all, bounds_all, sizes, maxn, P):
+        return self._count(params, gathered_segments_numpy(keys_all.numpy(), pays_all.numpy(),
+                                                           bounds_all.numpy(), sizes, maxn, P))
+
+    def join_local(self, params, v):
+        return self._count(params, [(v.keys, v.pays, v.bounds)])
+
+    def count_tensor(self, value):
+        return torch.tensor([int(value)], dtype=torch.int64)
+
+
+def _tables(nR, nS, alpha, seed):
+    R, S = O.generate_tables(nR, nS, alpha, seed, threads=2)
+    S[::5, 0] += nR  # a fifth of the probe keys miss
+    return R, S
+
+
+def _worker(rank, world, port, nR, nS, alpha, seed, bits, nparts, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        R, S = _tables(nR, nS, alpha, seed)
+        rlo, rhi = shard_range(nR, rank, world)
+        slo, shi = shard_range(nS, rank, world)
+        eng = OracleShardEngine(R[rlo:rhi], S[slo:shi])
+        p = phj.radix_params(bits, num_partitions=nparts, hash=phj.HASH_MURMUR3, seed=1234)
+        res = distributed_join(eng, p, nR, nS, rank, world, dist)
+        out[rank] = (res.matches, res.local_matches)
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_shard_ranges_cover_exactly():
+    for n in (0, 1, 7, 10_000_000):
+        for w in (1, 2, 3, 8):
+            rs = [shard_range(n, r, w) for r in range(w)]
+            assert rs[0][0] == 0 and rs[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
+            assert max_shard(n, w) - min(hi - lo for lo, hi in rs) <= 1
+
+
+@pytest.mark.parametrize("world,bits,nparts", [(2, (4, 4), 0), (3, (6, 0), 0), (2, (1, 0), 37)])
+def test_distributed_join_gloo(world, bits, nparts):
+    nR, nS, alpha, seed = 20_011, 150_007, 1.25, 3
+    R, S = _tables(nR, nS, alpha, seed)
+    expect = O.semijoin_count(R, S)
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), nR, nS, alpha, seed, bits, nparts, out), nprocs=world)
+    totals = {out[r][0] for r in range(world)}
+    assert totals == {expect}
+    assert sum(out[r][1] for r in range(world)) == expect
+
+
+def test_single_rank_path():
+    R, S = _tables(5000, 40_000, 1.05, 8)
+    eng = OracleShardEngine(R, S)
+    res = distributed_join(eng, phj.radix_params((3, 3)), 5000, 40_000, 0, 1, None)
+    assert res.matches == O.semijoin_count(R, S)
