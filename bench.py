@@ -46,6 +46,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, cpus) - 1")
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes")
     return ap.parse_args()
 
 
@@ -60,6 +61,59 @@ def config_params(phj, name):
         "C2: RadixCluster 2-pass 8+8, Murmur3, 10M⋈200M, Zipf s=1.05"
 
 
+# rocprof kernel-name prefix (and input layout) of each timed launch; the
+# S-side launch is the largest grid of that name
+KERNEL_OF_TIMER = {
+    "S.p1.hist": "void phj::k_hist<256, 16, true,", "S.p2.hist": "void phj::k_hist<256, 16, false,",
+    "S.p1.scatter": "void phj::k_scatter<256, 16, true,", "S.p2.scatter": "void phj::k_scatter<256, 16, false,",
+    "probe": "void phj::k_probe<", "build": "void phj::k_build_small<",
+    "np.probe": "void phj::k_np_probe<", "np.build": "void phj::k_np_build<",
+}
+
+
+def pmc_traffic(args, verbose):
+    """HBM bytes per launch from rocprofv3 PMC counters, one counter per pass
+    (MI355X_MICROARCH.md §HBM: FETCH_SIZE reads half the bytes of a wide
+    coalesced stream on gfx950 -> doubled; WRITE_SIZE exact; units of KiB).
+    Runs scripts/pmc_probe.py as child processes BEFORE this process touches
+    the GPU. Returns {timer name: bytes per launch} ({} if unavailable)."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    if not shutil.which("rocprofv3"):
+        return {}
+    per = {}
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        out = tempfile.mkdtemp(prefix="phj_pmc_", dir="/tmp")
+        cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", out, "-o", "run", "--",
+               sys.executable, os.path.join(ROOT, "scripts", "pmc_probe.py"), "--config", args.config,
+               "--primary", str(args.primary), "--secondary", str(args.secondary)]
+        try:
+            subprocess.run(cmd, check=True, capture_output=True, timeout=240, cwd="/tmp",
+                           env=dict(os.environ, TMPDIR="/tmp"))
+        except Exception as e:  # profiler unavailable: traffic stays null
+            if verbose:
+                print(f"pmc pass {counter} failed: {e}", file=sys.stderr)
+            return {}
+        rows = []
+        for f in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
+            with open(f) as fh:
+                rows += list(csv.DictReader(fh))
+        shutil.rmtree(out, ignore_errors=True)
+        for timer, prefix in KERNEL_OF_TIMER.items():
+            cand = [r for r in rows if r["Kernel_Name"].startswith(prefix)]
+            if not cand:
+                continue
+            g = max(int(r["Grid_Size"]) for r in cand)
+            vals = [float(r["Counter_Value"]) for r in cand if int(r["Grid_Size"]) == g]
+            kib = sum(vals) / len(vals)
+            per.setdefault(timer, 0.0)
+            per[timer] += kib * 1024 * (2 if counter == "FETCH_SIZE" else 1)
+    return per
+
+
 def cpu_baseline(ctx, nR, nS, threads, verbose):
     """The oracle's restatement of RadixCluster -p 1024 (XXH3) on this host's cores,
     over the same device-generated relations (copied back), once."""
@@ -67,10 +121,12 @@ def cpu_baseline(ctx, nR, nS, threads, verbose):
     import numpy as np
     R = ctx.download(0)
     S = ctx.download(1)
-    t0 = time.perf_counter()
     res = O.join_radix(R, S, P=1024, radix=False, part_hash=O.HASH_XXH3, part_seed=1,
                        table_hash=O.HASH_XXH3, table_seed=2, ratio=1.25, workers=threads)
-    wall = time.perf_counter() - t0
+    # Run()'s wall from SetPartitioningPhaseBegin to the end of Join(): the
+    # partitioned copies are allocated before the timer, as in the reference
+    # (RadixCluster/HashJoin.hpp:195-198)
+    wall = res.wall_ms * 1e-3
     del R, S
     if verbose:
         print(f"cpu baseline: {res.as_dict()}", file=sys.stderr)
@@ -93,6 +149,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # PMC passes first: child processes, before this process initialises the GPU
+    traffic = {} if (world > 1 or args.no_traffic) else pmc_traffic(args, args.verbose)
     import torch
     import torch.distributed as dist
     import partitionedhashjoin_amd as phj
@@ -181,8 +239,10 @@ def main():
             "correct": int(matches) == inrange,
             "roofline": {"bound": "hbm", "kernel": dom_name, "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": None},
+                         "traffic": traffic.get(dom_name), "algorithmic_bytes": dom_bytes,
+                         "ms": dom_ms},
             "kernels_ms": {k: round(v[0], 4) for k, v in sorted(per_step.items())},
+            "kernels_traffic_bytes": {k: int(v) for k, v in sorted(traffic.items())} or None,
         }
         if world == 1 and not args.no_cpu_baseline:
             threads = args.cpu_threads or max(1, min(16, os.cpu_count() or 1) - 1)

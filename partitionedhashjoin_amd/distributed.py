@@ -103,6 +103,26 @@ class HipShardEngine:
         return self.torch.tensor([value], dtype=self.torch.int64, device=self.device)
 
 
+def _all_gather(dist, out, inp):
+    """all_gather_into_tensor; device tensors are staged through host memory
+    when the process group is gloo (CPU-only collectives: rehearsal runs)."""
+    if inp.is_cuda and dist.get_backend() == "gloo":
+        host_out = out.new_empty(out.shape, device="cpu")
+        dist.all_gather_into_tensor(host_out, inp.cpu())
+        out.copy_(host_out)
+        return None
+    return dist.all_gather_into_tensor(out, inp, async_op=True)
+
+
+def _all_reduce(dist, t):
+    if t.is_cuda and dist.get_backend() == "gloo":
+        h = t.cpu()
+        dist.all_reduce(h)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t)
+
+
 def distributed_join(engine, params, nR: int, nS: int, rank: int, world: int, dist=None):
     """Join the range-sharded relations already resident on every rank.
 
@@ -119,15 +139,15 @@ def distributed_join(engine, params, nR: int, nS: int, rank: int, world: int, di
         keys_all = engine.tensor(world * maxn, torch.int64)
         pays_all = engine.tensor(world * maxn, torch.int64)
         bounds_all = engine.tensor(world * (P + 1), torch.int32)
-        works = [dist.all_gather_into_tensor(keys_all, keys, async_op=True),
-                 dist.all_gather_into_tensor(pays_all, pays, async_op=True),
-                 dist.all_gather_into_tensor(bounds_all, bounds, async_op=True)]
+        works = [_all_gather(dist, keys_all, keys), _all_gather(dist, pays_all, pays),
+                 _all_gather(dist, bounds_all, bounds)]
         engine.partition(1, params)         # overlaps the exchange
         for w in works:
-            w.wait()
+            if w is not None:
+                w.wait()
         res = engine.join_gathered(params, keys_all, pays_all, bounds_all, sizes, maxn, P)
         cnt = engine.count_tensor(res.matches)
-        dist.all_reduce(cnt)
+        _all_reduce(dist, cnt)
         total = int(cnt.item())
     else:
         engine.partition(1, params)

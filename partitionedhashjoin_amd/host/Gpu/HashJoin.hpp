@@ -1,9 +1,9 @@
 // Drop-in GPU joiners with the reference's HashJoiner API:
 //
 //   RadixClustering::HashJoiner<HashTableFactory, HasherType>(Configuration, pool, hasher, factory)
-//     .Run(tableA /*build*/, tableB /*probe*/, timer)       src/RadixCluster/HashJoin.hpp:91-135
+//     .Run(tableA /*build*/, tableB /*probe*/, timer)       src/RadixCluster/HashJoin.hpp:92-135, 190-241
 //   NoPartitioning::HashJoiner<HashTableFactory>(Configuration, pool, factory)
-//     .Run(tableA, tableB, timer)                           src/NoPartitioning/HashJoin.hpp:14-41
+//     .Run(tableA, tableB, timer)                           src/NoPartitioning/HashJoin.hpp:15-41, 54-187
 //
 // The thread-pool slot of the reference constructors takes a Gpu::Device (one
 // phj_ctx: device, stream, workspace). Run() hands &(*table)[0] / GetSize()

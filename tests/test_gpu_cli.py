@@ -1,0 +1,56 @@
+"""The phjoin CLI end to end on the GPU: reference flags in, reference JSON
+out, matched count equal to the oracle's on the same (seeded) relations."""
+import json
+import os
+import subprocess
+
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+CLI = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "partitionedhashjoin_amd", "phjoin")
+
+
+def run_cli(tmp_path, *args):
+    out = tmp_path / "hashjoin.txt"
+    r = subprocess.run([CLI, "--log", "debug", "-f", str(out)] + list(args), capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return json.loads(out.read_text()), r.stderr
+
+
+@pytest.mark.parametrize("args,type_", [
+    (("--join", "radix-partitioning"), "RadixParitioning"),
+    (("--join", "radix-partitioning", "-p", "1024"), "RadixParitioning"),
+    (("--join", "radix-partitioning", "--radix-bits", "8,8", "--hash", "murmur3"), "RadixParitioning"),
+    (("--join", "no-partitioning"), "NoPartitioning"),
+])
+def test_cli_matches_oracle(tmp_path, args, type_):
+    nR, nS, skew, seed = 200_000, 3_000_000, 1.25, 4242
+    res, log = run_cli(tmp_path, "--primary", str(nR), "--secondary", str(nS), "--skew", str(skew),
+                       "--seed", str(seed), "-u", "us", *args)
+    R, S = O.generate_tables(nR, nS, skew, seed)      # the CLI's host generator == the oracle's
+    expect = O.join_radix(R, S, P=256, workers=4).matches
+    assert int(res["results"]["matches"]) == expect == nS
+    assert res["id"] == "hashjointimingresult"
+    assert res["parameters"]["Type"] == type_
+    assert res["parameters"]["PrimaryRelationSize"] == str(nR)
+    assert list(res["results"])[:3] == ["partition", "build", "probe"]
+    assert f"Joined" in log and str(expect) in log
+
+
+def test_cli_device_generation(tmp_path):
+    res, _ = run_cli(tmp_path, "--primary", "1000000", "--secondary", "20000000", "--generate", "device",
+                     "--join", "radix-partitioning", "--radix-bits", "8,8")
+    assert int(res["results"]["matches"]) == 20_000_000
+    assert res["parameters"]["NumberOfPartitions"] == "65536"
+
+
+def test_cli_primary_one_terminates_like_reference(tmp_path):
+    # --primary 1 makes Zipf reject the [1, 1] range outside the join's try block
+    # (src/main.cpp:68-74, Zipf.cpp:61-67): the process terminates abnormally
+    r = subprocess.run([CLI, "--join", "radix-partitioning", "--primary", "1", "--secondary", "10",
+                        "-f", str(tmp_path / "x.txt")], capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0
+    assert "Range for Zipf generation is incorrectly specified" in r.stderr
