@@ -20,6 +20,8 @@ HOST_HDR := $(wildcard $(PKG)/host/*.hpp $(PKG)/host/*/*.hpp) $(PKG)/csrc/phj_ha
 
 ifneq ($(HOST_SRC),)
 all: $(LIB) $(CLI) oracle
+
+lib: $(LIB)
 else
 all: $(LIB) oracle
 endif
@@ -38,4 +40,4 @@ clean:
 	rm -f $(LIB) $(CLI)
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all oracle clean
+.PHONY: all oracle clean lib

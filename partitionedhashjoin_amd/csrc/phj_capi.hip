@@ -39,7 +39,7 @@ struct DevBuf {
 // values; PHJ_TILE_ITEMS / PHJ_P1_AOS / PHJ_XCD_REMAP override them for sweeps.
 struct Tuning {
     int tile = 4096;      // tile kernels: tuples per tile (2048, 4096 or 8192)
-    bool p1_aos = false;  // tile kernels, 2-pass: pass-1 output as 16-B tuples
+    bool p1_aos = true;   // tile kernels, 2-pass: pass-1 output as 16-B tuples (16-B stores)
     bool xcd_remap = true;
     bool wc = false;      // write-combining super-tile kernels (slower on MI355X: DESIGN.md)
     int wc_items = 8;     // WC sub-tile = 256 * wc_items tuples (4 or 8)
@@ -47,6 +47,9 @@ struct Tuning {
     int wc_wgs = 1024;    // target workgroups per WC pass (super-tile size follows)
     bool r_aux = false;   // partition R on the aux stream (no gain measured: DESIGN.md)
     int probe_items = 8;  // S keys per lane per probe work item (8 or 16)
+    int block = 512;      // threads per workgroup of the tile kernels (256, 512 or 1024; tile_shape)
+    bool nt_store = false; // nontemporal scatter stores
+    bool dcol = true;     // 2-pass: pass 1 writes the pass-2 digit column
 };
 
 int env_int(const char* name, int dflt) {
@@ -82,6 +85,7 @@ struct SideState {
     DevBuf owned;
     DevBuf kA, pA, kB, pB;
     DevBuf hist1, hist2, bounds1, tbase2, tseg2, bounds, partials;
+    DevBuf dig;           // pass-2 digit column written by pass 1
     phj_partitioned view{};
     bool partitioned = false;
     Plan plan;
@@ -319,10 +323,22 @@ int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const st
     const size_t hist_lds = static_cast<size_t>(NW) * a.nbins * 4;
     const size_t sc_lds = scatter_lds_bytes(T, a.nbins, NW);
     const std::string hname = prefix + ".hist", cname = prefix + ".scan", sname = prefix + ".scatter";
-    // algorithmic bytes: the histogram reads the key (a whole 16-B tuple when AoS);
-    // the scatter reads and writes every tuple once (16 + 16 B)
-    PHJ_TRY(timer_begin(c, hname.c_str(), n * (IN_AOS ? 16 : 8)));
-    if (hk == kMurmur3)
+    // algorithmic bytes: the histogram reads the key (a whole 16-B tuple when AoS)
+    // or 1-2 B of a digit column; the scatter reads and writes every tuple once
+    // (16 + 16 B) plus the digit column it leaves for pass 2
+    const uint64_t hbytes = a.in_dig ? n * (a.dig_wide ? 2 : 1) : n * (IN_AOS ? 16 : 8);
+    PHJ_TRY(timer_begin(c, hname.c_str(), hbytes));
+    if (a.in_dig) {
+        // wave per tile: 4 tiles per workgroup
+        PassArgs ac = a;
+        uint32_t cgrid = (grid + 3) / 4;
+        if (ac.xcd_remap) cgrid = (cgrid + 7) & ~7u;
+        const size_t clds = 4ull * a.nbins * 4;
+        if (a.dig_wide)
+            hipLaunchKernelGGL((k_hist_col<T, uint16_t>), dim3(cgrid), dim3(256), clds, c->ks, ac);
+        else
+            hipLaunchKernelGGL((k_hist_col<T, uint8_t>), dim3(cgrid), dim3(256), clds, c->ks, ac);
+    } else if (hk == kMurmur3)
         hipLaunchKernelGGL((k_hist<BLOCK, ITEMS, IN_AOS, kMurmur3>), dim3(grid), dim3(BLOCK), hist_lds, c->ks, a);
     else
         hipLaunchKernelGGL((k_hist<BLOCK, ITEMS, IN_AOS, kXXH3>), dim3(grid), dim3(BLOCK), hist_lds, c->ks, a);
@@ -331,14 +347,29 @@ int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const st
     PHJ_TRY(timer_begin(c, cname.c_str(), static_cast<uint64_t>(hist_len) * 12));
     PHJ_TRY(scan_u32(c, a.hist, hist_len, 1, hist_len, c->scan_scratch));
     PHJ_TRY(timer_end(c));
-    PHJ_TRY(timer_begin(c, sname.c_str(), n * 32));
-    if (hk == kMurmur3)
+    PHJ_TRY(timer_begin(c, sname.c_str(), n * 32 + (a.out_dig ? n * (a.dig_wide ? 2 : 1) : 0)));
+    if (hk == kMurmur3) {
         hipLaunchKernelGGL((k_scatter<BLOCK, ITEMS, IN_AOS, OUT_AOS, kMurmur3>), dim3(grid), dim3(BLOCK), sc_lds, c->ks, a);
-    else
+    } else {
         hipLaunchKernelGGL((k_scatter<BLOCK, ITEMS, IN_AOS, OUT_AOS, kXXH3>), dim3(grid), dim3(BLOCK), sc_lds, c->ks, a);
+    }
     PHJ_LAUNCHED(c, sname);
     PHJ_TRY(timer_end(c));
     return PHJ_OK;
+}
+
+// Workgroup size and tile of the tile kernels: the tuned shape when it is one
+// of the compiled ones and its scatter fits the LDS, else 512 x 4096.
+struct TileShape {
+    int block, tile;
+};
+
+TileShape tile_shape(const phj_ctx* c, uint32_t nb) {
+    const int b = c->tune.block, t = c->tune.tile;
+    const bool compiled = (b == 256 && (t == 2048 || t == 4096)) || (b == 512 && (t == 2048 || t == 4096 || t == 8192)) ||
+                          (b == 1024 && t == 8192);
+    if (compiled && scatter_lds_bytes(t, nb, b / 64) <= 160 * 1024) return TileShape{b, t};
+    return TileShape{512, 4096};
 }
 
 // One partition pass over `ntiles` tiles (an upper bound for segmented passes).
@@ -351,8 +382,7 @@ int launch_pass(phj_ctx* c, int hk, bool in_aos, bool out_aos, PassArgs a, uint3
         grid = (ntiles + 7) & ~7u;
         a.xcd_remap = 1;
     }
-    int tile = c->tune.tile;
-    if (tile == 8192 && scatter_lds_bytes(8192, a.nbins, 8) > 160 * 1024) tile = 4096;
+    const TileShape sh = tile_shape(c, a.nbins);
     const int io = (in_aos ? 2 : 0) + (out_aos ? 1 : 0);
 #define PHJ_PASS_CASES(B, I)                                                        \
     switch (io) {                                                                   \
@@ -361,9 +391,13 @@ int launch_pass(phj_ctx* c, int hk, bool in_aos, bool out_aos, PassArgs a, uint3
         case 3: return launch_pass_t<B, I, true, true>(c, hk, a, grid, prefix, n, hist_len);   \
         default: return set_err(c, PHJ_ERR_INVALID, "unsupported pass layout");     \
     }
-    if (tile == 2048) PHJ_PASS_CASES(256, 8)
-    if (tile == 8192) PHJ_PASS_CASES(512, 16)
-    PHJ_PASS_CASES(256, 16)
+    a.nt_store = c->tune.nt_store ? 1u : 0u;
+    if (sh.block == 256 && sh.tile == 2048) PHJ_PASS_CASES(256, 8)
+    if (sh.block == 256 && sh.tile == 4096) PHJ_PASS_CASES(256, 16)
+    if (sh.block == 512 && sh.tile == 2048) PHJ_PASS_CASES(512, 4)
+    if (sh.block == 512 && sh.tile == 8192) PHJ_PASS_CASES(512, 16)
+    if (sh.block == 1024 && sh.tile == 8192) PHJ_PASS_CASES(1024, 8)
+    PHJ_PASS_CASES(512, 8)
 #undef PHJ_PASS_CASES
 }
 
@@ -383,7 +417,7 @@ int launch_pass_wc_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, uint3
     PHJ_TRY(timer_begin(c, cname.c_str(), static_cast<uint64_t>(hist_len) * 12));
     PHJ_TRY(scan_u32(c, a.hist, hist_len, 1, hist_len, c->scan_scratch));
     PHJ_TRY(timer_end(c));
-    PHJ_TRY(timer_begin(c, sname.c_str(), n * 32));
+    PHJ_TRY(timer_begin(c, sname.c_str(), n * 32 + (a.out_dig ? n * (a.dig_wide ? 2 : 1) : 0)));
     if (hk == kMurmur3)
         hipLaunchKernelGGL((k_scatter_wc<ITEMS, IN_AOS, kMurmur3, LW>), dim3(grid), dim3(kBlock), sc_lds, c->ks, a, tsz);
     else
@@ -421,10 +455,7 @@ int launch_pass_wc(phj_ctx* c, int hk, bool in_aos, PassArgs a, uint32_t ntiles,
 // Tuples per (super-)tile of a pass over n tuples with nb digits.
 uint32_t pass_tile(const phj_ctx* c, uint32_t n, uint32_t nb, bool* wc) {
     *wc = c->tune.wc && nb <= static_cast<uint32_t>(kWcMaxBins);
-    if (!*wc) {
-        if (c->tune.tile == 8192 && scatter_lds_bytes(8192, nb, 8) > 160 * 1024) return 4096;
-        return static_cast<uint32_t>(c->tune.tile);
-    }
+    if (!*wc) return tile_shape(c, nb).tile;
     const uint32_t sub = kBlock * static_cast<uint32_t>(c->tune.wc_items);
     const uint64_t subs = (static_cast<uint64_t>(n) + sub - 1) / sub;
     const uint64_t k = std::min<uint64_t>(64, std::max<uint64_t>(1, (subs + c->tune.wc_wgs - 1) / c->tune.wc_wgs));
@@ -444,6 +475,9 @@ int partition_side(phj_ctx* c, int s, const Plan& pl) {
     const uint32_t nt1 = (n + tile - 1) / tile;
     const uint32_t nt2 = pl.npass == 2 ? (n + tile2 - 1) / tile2 + pl.nb1 : 0;  // bound
     const bool p1_aos = pl.npass == 2 && c->tune.p1_aos && !wc1;
+    // pass 1 leaves the pass-2 digit in a column (tile kernels only)
+    const bool dcol = pl.npass == 2 && c->tune.dcol && !wc1 && !wc2;
+    const uint32_t dbytes = pl.bits2 > 8 ? 2 : 1;
     const char* tag = s == PHJ_SIDE_BUILD ? "R" : "S";
     // workspace (grow-only; allocation is outside the timed phases on reuse)
     PHJ_TRY(ensure(c, S.kA, static_cast<size_t>(n) * (p1_aos ? 16 : 8)));
@@ -457,6 +491,7 @@ int partition_side(phj_ctx* c, int s, const Plan& pl) {
         PHJ_TRY(ensure(c, S.hist2, (static_cast<size_t>(nt2) + 8) * pl.nb2 * 4));
         PHJ_TRY(ensure(c, S.tseg2, (static_cast<size_t>(nt2) + 8) * 4));
         PHJ_TRY(ensure(c, S.bounds, (static_cast<size_t>(pl.Ppad) + 1) * 4));
+        if (dcol) PHJ_TRY(ensure(c, S.dig, static_cast<size_t>(n) * dbytes + 64));
     }
     // pass 1: AoS relation -> SoA columns A
     PassArgs a{};
@@ -472,6 +507,11 @@ int partition_side(phj_ctx* c, int s, const Plan& pl) {
     a.nbins = pl.nb1;
     a.nbits = pl.bits1;
     a.f = digit_fn(pl, 1);
+    if (dcol) {
+        a.out_dig = S.dig.p;
+        a.dig_wide = dbytes == 2 ? 1u : 0u;
+        a.dig2_mask = pl.dmask2;
+    }
     if (wc1)
         PHJ_TRY(launch_pass_wc(c, pl.hk, true, a, nt1, tile, std::string(tag) + ".p1", n, nt1 * pl.nb1));
     else
@@ -505,6 +545,10 @@ int partition_side(phj_ctx* c, int s, const Plan& pl) {
         b.nbins = pl.nb2;
         b.nbits = pl.bits2;
         b.f = digit_fn(pl, 2);
+        if (dcol) {
+            b.in_dig = S.dig.p;
+            b.dig_wide = dbytes == 2 ? 1u : 0u;
+        }
         const uint32_t grid2 = n ? nt2 : 0;
         if (wc2)
             PHJ_TRY(launch_pass_wc(c, pl.hk, false, b, grid2, tile2, std::string(tag) + ".p2", n, grid2 * pl.nb2));
@@ -770,11 +814,14 @@ int phj_ctx_create(int device, phj_ctx** out) {
         const int t = env_int("PHJ_TILE", 4096);
         c->tune.tile = (t == 2048 || t == 8192) ? t : 4096;
     }
-    c->tune.p1_aos = env_int("PHJ_P1_AOS", 0) != 0;
+    c->tune.p1_aos = env_int("PHJ_P1_AOS", 1) != 0;
     c->tune.xcd_remap = env_int("PHJ_XCD_REMAP", 1) != 0;
     c->tune.wc = env_int("PHJ_WC", 0) != 0;
     c->tune.r_aux = env_int("PHJ_R_AUX", 0) != 0;
     c->tune.probe_items = env_int("PHJ_PROBE_ITEMS", 8) == 16 ? 16 : 8;
+    c->tune.block = env_int("PHJ_BLOCK", 512);
+    c->tune.nt_store = env_int("PHJ_NT", 0) != 0;
+    c->tune.dcol = env_int("PHJ_DCOL", 1) != 0;
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;

@@ -73,6 +73,12 @@ struct PassArgs {
     uint32_t nbins;
     uint32_t nbits;
     uint32_t xcd_remap;         // 1: give each XCD a contiguous run of tiles (grid % 8 == 0)
+    uint32_t nt_store;          // 1: scatter stores bypass the caches' allocate (nontemporal)
+    uint32_t dig_wide;          // digit column element: 0 = u8, 1 = u16
+    void* out_dig;              // pass-1 scatter: writes the NEXT pass's digit per output slot
+    const void* in_dig;         // pass-2 histogram: counts this column instead of hashing keys
+    uint32_t dig2_mask;         // next pass's digit = q & dig2_mask
+    uint32_t pad1;
     DigitFn f;
 };
 
@@ -188,6 +194,38 @@ __device__ __forceinline__ void load_tuple(const PassArgs& a, uint32_t idx, int6
     }
 }
 
+template <bool OUT_AOS>
+__device__ __forceinline__ void store_tuple(const PassArgs& a, uint32_t o, int64_t k, int64_t p) {
+    if constexpr (OUT_AOS) {
+        longlong2* t = reinterpret_cast<longlong2*>(a.out_keys) + o;
+        if (a.nt_store) {
+            __builtin_nontemporal_store(k, &t->x);
+            __builtin_nontemporal_store(p, &t->y);
+        } else {
+            *t = make_longlong2(k, p);
+        }
+    } else {
+        if (a.nt_store) {
+            __builtin_nontemporal_store(k, a.out_keys + o);
+            __builtin_nontemporal_store(p, a.out_pays + o);
+        } else {
+            a.out_keys[o] = k;
+            a.out_pays[o] = p;
+        }
+    }
+}
+
+// Pass 1 of a 2-pass partition already hashes every tuple: it leaves the
+// pass-2 digit (q & mask, one or two bytes) in a column in output order, so
+// the pass-2 histogram reads 1-2 B per tuple instead of the 8-B key (or the
+// 16-B tuple).
+template <int HK>
+__device__ __forceinline__ void store_next_digit(const PassArgs& a, uint32_t o, int64_t key) {
+    const uint32_t d2 = static_cast<uint32_t>(partition_q<HK>(static_cast<uint64_t>(key), a.f)) & a.dig2_mask;
+    if (a.dig_wide) static_cast<uint16_t*>(a.out_dig)[o] = static_cast<uint16_t>(d2);
+    else static_cast<uint8_t*>(a.out_dig)[o] = static_cast<uint8_t>(d2);
+}
+
 // Per-tile digit histogram -> hist[(tb_s * nbins) + d * ntiles_s + tseg].
 template <int BLOCK, int ITEMS, bool AOS, int HK>
 __global__ __launch_bounds__(BLOCK) void k_hist(PassArgs a) {
@@ -252,10 +290,70 @@ __global__ __launch_bounds__(BLOCK) void k_hist(PassArgs a) {
     }
 }
 
-// LDS bytes of k_scatter for a tile of T tuples, nb digits, NW waves.
-__host__ __device__ constexpr size_t scatter_lds_bytes(int T, uint32_t nb, int NW = kWaves) {
-    return static_cast<size_t>(T) * 18 + static_cast<size_t>(nb) * 4 * (NW + 2) + 64;
+// Per-tile histogram of a digit column (pass 2 after store_next_digit). A
+// tile's digits are only T bytes, so one WAVE counts one tile (16-B loads,
+// count_digit into the wave's own LDS row) and writes that tile's column:
+// no cross-wave reduction, 1/NW of the counter zeroing.
+// tile(wave) = tile_id(block) * 4 + wave; grid covers ceil(tiles / 4) blocks.
+template <int T, typename DT>
+__global__ __launch_bounds__(256) void k_hist_col(PassArgs a) {
+    constexpr int EPC = 16 / static_cast<int>(sizeof(DT));          // digits per 16-B chunk
+    constexpr int ROUNDS = (T / EPC + 1 + 63) / 64;                  // chunks covering a tile, per lane
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t nb = a.nbins;
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint32_t* my = reinterpret_cast<uint32_t*>(smem) + wave * nb;
+    TileLoc L;
+    if (!locate_tile<T>(a, tile_id(a) * 4 + wave, L)) return;   // wave-uniform; no block barrier below
+    for (uint32_t i = lane; i < nb; i += 64) my[i] = 0;
+    const uint32_t c0 = L.lo / EPC, c1 = (L.hi + EPC - 1) / EPC;
+    const uint4* col = static_cast<const uint4*>(a.in_dig);
+    uint4 v[ROUNDS];
+#pragma unroll
+    for (int r = 0; r < ROUNDS; r++) {
+        const uint32_t ci = c0 + r * 64 + lane;
+        v[r] = ci < c1 ? col[ci] : make_uint4(0, 0, 0, 0);
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int r = 0; r < ROUNDS; r++) {
+        const uint32_t e0 = (c0 + r * 64 + lane) * EPC;
+        const uint32_t w[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
+#pragma unroll
+        for (int j = 0; j < EPC; j++) {
+            const uint32_t e = e0 + j;
+            const uint32_t d = sizeof(DT) == 1 ? (w[j >> 2] >> (8 * (j & 3))) & 0xffu
+                                               : (w[j >> 1] >> (16 * (j & 1))) & 0xffffu;
+            const bool valid = e >= L.lo && e < L.hi;
+            count_digit(my, valid ? d : 0u, valid);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    uint32_t* out = a.hist + static_cast<size_t>(L.tb_s) * nb + L.tseg;
+    for (uint32_t d = lane; d < nb; d += 64) out[static_cast<size_t>(d) * L.ntiles_s] = my[d];
 }
+
+// LDS bytes of k_scatter for a tile of T tuples, nb digits, NW waves.
+// The per-tuple digit is kept as one byte when nb <= 256 (two otherwise).
+__host__ __device__ constexpr size_t scatter_lds_bytes(int T, uint32_t nb, int NW = kWaves) {
+    return static_cast<size_t>(T) * (nb <= 256 ? 17 : 18) + static_cast<size_t>(nb) * 4 * (NW + 2) + 64;
+}
+
+// Sorted-digit array of the scatter kernels: u8 for nb <= 256, else u16.
+struct SortedDigits {
+    void* p;
+    bool d8;
+    __device__ __forceinline__ void put(uint32_t i, uint32_t d) const {
+        if (d8) static_cast<uint8_t*>(p)[i] = static_cast<uint8_t>(d);
+        else static_cast<uint16_t*>(p)[i] = static_cast<uint16_t>(d);
+    }
+    __device__ __forceinline__ uint32_t get(uint32_t i) const {
+        return d8 ? static_cast<const uint8_t*>(p)[i] : static_cast<const uint16_t*>(p)[i];
+    }
+    __device__ __forceinline__ void* end(uint32_t T) const {
+        return static_cast<unsigned char*>(p) + (d8 ? T : 2 * T);
+    }
+};
 
 // Stable scatter of one tile using the scanned offsets.
 template <int BLOCK, int ITEMS, bool AOS, bool OUT_AOS, int HK>
@@ -270,7 +368,7 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(PassArgs a) {
     uint32_t* gofs = wcnt + NW * nb;
     uint32_t* dstart = gofs + nb;
     uint32_t* tmp = dstart + nb;                              // 16 words
-    uint16_t* sdig = reinterpret_cast<uint16_t*>(tmp + 16);   // [T]
+    const SortedDigits sdig{tmp + 16, nb <= 256};             // [T]
 
     TileLoc L;
     if (!locate_tile<T>(a, tile_id(a), L)) return;
@@ -345,7 +443,7 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(PassArgs a) {
             const uint32_t pos = my[dig[i]] + rank[i];
             skey[pos] = key[i];
             spay[pos] = pay[i];
-            sdig[pos] = static_cast<uint16_t>(dig[i]);
+            sdig.put(pos, dig[i]);
         }
     }
     __syncthreads();
@@ -353,14 +451,10 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(PassArgs a) {
     for (int i = 0; i < ITEMS; i++) {
         const uint32_t k = i * BLOCK + tid;
         if (k < cnt) {
-            const uint32_t d = sdig[k];
+            const uint32_t d = sdig.get(k);
             const uint32_t o = gofs[d] + (k - dstart[d]);
-            if constexpr (OUT_AOS) {
-                reinterpret_cast<longlong2*>(a.out_keys)[o] = make_longlong2(skey[k], spay[k]);
-            } else {
-                a.out_keys[o] = skey[k];
-                a.out_pays[o] = spay[k];
-            }
+            store_tuple<OUT_AOS>(a, o, skey[k], spay[k]);
+            if (a.out_dig) store_next_digit<HK>(a, o, skey[k]);
         }
     }
 }

@@ -1,0 +1,85 @@
+"""GPU parity of every kernel schedule the context can be tuned to.
+
+The tuning knobs (read from the environment when a context is created) pick
+between kernel schedules that must produce the same bytes: tile size
+(PHJ_TILE) and workgroup size (PHJ_BLOCK) of the histogram/scatter kernels,
+nontemporal stores (PHJ_NT), pass-1 output layout (PHJ_P1_AOS), the pass-2
+digit column (PHJ_DCOL), tile order
+(PHJ_XCD_REMAP), write-combining scatter (PHJ_WC), probe items
+(PHJ_PROBE_ITEMS). Each is
+checked against the oracle's stable partition and semi-join count.
+"""
+import numpy as np
+import pytest
+
+import partitionedhashjoin_amd as phj
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+SEED = 0x0BAD_5EED_0BAD_5EED
+
+SCHEDULES = [
+    {},
+    {"PHJ_BLOCK": "256", "PHJ_TILE": "4096"},
+    {"PHJ_BLOCK": "256", "PHJ_TILE": "2048"},
+    {"PHJ_BLOCK": "512", "PHJ_TILE": "2048"},
+    {"PHJ_BLOCK": "512", "PHJ_TILE": "8192"},
+    {"PHJ_BLOCK": "1024", "PHJ_TILE": "8192"},
+    {"PHJ_BLOCK": "333"},                      # not compiled: falls back to 512 x 4096
+    {"PHJ_P1_AOS": "0"},
+    {"PHJ_P1_AOS": "0", "PHJ_DCOL": "0"},
+    {"PHJ_DCOL": "0"},
+    {"PHJ_XCD_REMAP": "0"},
+    {"PHJ_NT": "1"},
+    {"PHJ_WC": "1"},
+    {"PHJ_PROBE_ITEMS": "16"},
+]
+
+CASES = [((8, 8), 0, phj.HASH_MURMUR3), ((11, 0), 0, phj.HASH_XXH3), ((1, 0), 1000, phj.HASH_XXH3),
+         ((3, 5), 0, phj.HASH_XXH3)]
+
+
+def _sched_id(s):
+    return ",".join(f"{k[4:]}={v}" for k, v in s.items()) or "default"
+
+
+@pytest.fixture(params=SCHEDULES, ids=[_sched_id(s) for s in SCHEDULES])
+def tuned_ctx(request, monkeypatch):
+    for k, v in request.param.items():
+        monkeypatch.setenv(k, v)
+    c = phj.Context(0)
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("n", [1, 4095, 4097, 250_007])
+def test_partition_layout(tuned_ctx, n):
+    rng = np.random.default_rng(n)
+    # a hot key (skew) plus uniform keys
+    keys = rng.integers(-80_000, 80_000, n, dtype=np.int64)
+    keys[rng.random(n) < 0.3] = 42
+    rel = np.stack([keys, np.arange(n, dtype=np.int64)], axis=1)
+    for bits, nparts, hk in CASES:
+        p = phj.radix_params(bits=bits, num_partitions=nparts, hash=hk, seed=SEED)
+        tuned_ctx.upload(phj.SIDE_PROBE, rel)
+        v = tuned_ctx.partition(phj.SIDE_PROBE, p)
+        k, pay, bounds = tuned_ctx.download_partitioned(v)
+        P, radix = (nparts, False) if nparts else (1 << (bits[0] + bits[1]), True)
+        ok = O.HASH_MURMUR3 if hk == phj.HASH_MURMUR3 else O.HASH_XXH3
+        out, ob = O.partition(rel, P, radix, ok, SEED, workers=2)
+        assert np.array_equal(k, out[:, 0]), (bits, nparts)
+        assert np.array_equal(pay, out[:, 1]), (bits, nparts)
+        assert np.array_equal(bounds[:P + 1].astype(np.uint64), ob), (bits, nparts)
+
+
+def test_join_counts(tuned_ctx):
+    R, S = O.generate_tables(30_000, 400_003, 1.05, 21, threads=4)
+    S[::7, 0] += 30_000   # misses
+    expect = O.semijoin_count(R, S)
+    tuned_ctx.upload(phj.SIDE_BUILD, R)
+    tuned_ctx.upload(phj.SIDE_PROBE, S)
+    for p in (phj.radix_params((8, 8), hash=phj.HASH_MURMUR3, seed=SEED),
+              phj.radix_params(num_partitions=1024, hash=phj.HASH_XXH3, seed=SEED),
+              phj.radix_params((6, 0), hash=phj.HASH_XXH3, seed=SEED)):
+        assert tuned_ctx.join(p).matches == expect
