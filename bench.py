@@ -63,55 +63,23 @@ def config_params(phj, name):
 
 # rocprof kernel-name prefix (and input layout) of each timed launch; the
 # S-side launch is the largest grid of that name
-KERNEL_OF_TIMER = {
-    "S.p1.hist": "void phj::k_hist<256, 16, true,", "S.p2.hist": "void phj::k_hist<256, 16, false,",
-    "S.p1.scatter": "void phj::k_scatter<256, 16, true,", "S.p2.scatter": "void phj::k_scatter<256, 16, false,",
-    "probe": "void phj::k_probe<", "build": "void phj::k_build_small<",
-    "np.probe": "void phj::k_np_probe<", "np.build": "void phj::k_np_build<",
-}
-
-
 def pmc_traffic(args, verbose):
-    """HBM bytes per launch from rocprofv3 PMC counters, one counter per pass
-    (MI355X_MICROARCH.md §HBM: FETCH_SIZE reads half the bytes of a wide
-    coalesced stream on gfx950 -> doubled; WRITE_SIZE exact; units of KiB).
-    Runs scripts/pmc_probe.py as child processes BEFORE this process touches
-    the GPU. Returns {timer name: bytes per launch} ({} if unavailable)."""
-    import csv
-    import glob
+    """HBM bytes per launch of each join phase from rocprofv3 PMC counters
+    (scripts/pmc.py: FETCH_SIZE and WRITE_SIZE in separate passes, child
+    processes run BEFORE this process touches the GPU; FETCH_SIZE doubled per
+    MI355X_MICROARCH.md §HBM). Returns {timer name: bytes} ({} if unavailable)."""
     import shutil
-    import subprocess
-    import tempfile
     if not shutil.which("rocprofv3"):
         return {}
-    per = {}
-    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
-        out = tempfile.mkdtemp(prefix="phj_pmc_", dir="/tmp")
-        cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", out, "-o", "run", "--",
-               sys.executable, os.path.join(ROOT, "scripts", "pmc_probe.py"), "--config", args.config,
-               "--primary", str(args.primary), "--secondary", str(args.secondary)]
-        try:
-            subprocess.run(cmd, check=True, capture_output=True, timeout=240, cwd="/tmp",
-                           env=dict(os.environ, TMPDIR="/tmp"))
-        except Exception as e:  # profiler unavailable: traffic stays null
-            if verbose:
-                print(f"pmc pass {counter} failed: {e}", file=sys.stderr)
-            return {}
-        rows = []
-        for f in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
-            with open(f) as fh:
-                rows += list(csv.DictReader(fh))
-        shutil.rmtree(out, ignore_errors=True)
-        for timer, prefix in KERNEL_OF_TIMER.items():
-            cand = [r for r in rows if r["Kernel_Name"].startswith(prefix)]
-            if not cand:
-                continue
-            g = max(int(r["Grid_Size"]) for r in cand)
-            vals = [float(r["Counter_Value"]) for r in cand if int(r["Grid_Size"]) == g]
-            kib = sum(vals) / len(vals)
-            per.setdefault(timer, 0.0)
-            per[timer] += kib * 1024 * (2 if counter == "FETCH_SIZE" else 1)
-    return per
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import pmc
+    try:
+        per = pmc.collect([["FETCH_SIZE"], ["WRITE_SIZE"]], args.config, args.primary, args.secondary)
+    except Exception as e:  # profiler unavailable: traffic stays null
+        if verbose:
+            print(f"pmc passes failed: {e}", file=sys.stderr)
+        return {}
+    return pmc.hbm_bytes(per)
 
 
 def cpu_baseline(ctx, nR, nS, threads, verbose):

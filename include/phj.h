@@ -151,11 +151,20 @@ int phj_partition(phj_ctx *ctx, int side, const phj_join_params *p, phj_partitio
  * params must precede). Synchronous; fills r (build_ms, probe_ms, matches). */
 int phj_join_partitioned(phj_ctx *ctx, const phj_join_params *p, int nbuild,
                          const phj_partitioned *build, phj_join_result *r);
+/* Asynchronous form of phj_join_partitioned for stream-ordered pipelines
+ * (multi-GPU: the count feeds an RCCL all-reduce on the same stream): enqueues
+ * build and probe on the ctx stream and stores the count (uint64) at
+ * `dev_count`, a device address; no host synchronization. The phase timers
+ * are read later with phj_timers_report. */
+int phj_join_partitioned_async(phj_ctx *ctx, const phj_join_params *p, int nbuild,
+                               const phj_partitioned *build, uint64_t *dev_count);
 /* Per-kernel device timers recorded since the last report (e.g. after
  * phj_partition calls); synchronizes the ctx stream, then resets. */
 int phj_timers_report(phj_ctx *ctx, phj_join_result *r);
 /* Copy a partitioned view (keys, payloads: n; bounds: P+1) to host or device
- * buffers (any may be NULL). Synchronous. */
+ * buffers (any may be NULL). Synchronous when any destination is host memory;
+ * with device destinations only, the copies are enqueued on the ctx stream
+ * and the call returns at once. */
 int phj_partitioned_download(phj_ctx *ctx, const phj_partitioned *v, int64_t *keys,
                              int64_t *payloads, uint32_t *bounds);
 

@@ -142,6 +142,12 @@ class Context:
                                                  C.byref(r)))
         return r
 
+    def join_partitioned_async(self, params: JoinParams, segments, dev_count: int) -> None:
+        """Enqueue build + probe; the count lands at device address dev_count (uint64)."""
+        arr = (Partitioned * len(segments))(*segments)
+        self._check(self._L.phj_join_partitioned_async(self._h, C.byref(params), len(segments), arr,
+                                                       C.c_void_p(dev_count)))
+
     def timers_report(self) -> JoinResult:
         r = JoinResult()
         self._check(self._L.phj_timers_report(self._h, C.byref(r)))

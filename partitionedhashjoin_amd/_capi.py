@@ -35,7 +35,7 @@ EXPORTED = [
     "phj_relation_bind_device", "phj_relation_device_ptr", "phj_relation_download",
     "phj_relation_generate_sequential", "phj_relation_generate_zipf",
     "phj_relation_count_in_range", "phj_join", "phj_partition", "phj_join_partitioned",
-    "phj_partitioned_download", "phj_hash_keys", "phj_timers_report",
+    "phj_partitioned_download", "phj_hash_keys", "phj_timers_report", "phj_join_partitioned_async",
 ]
 
 
@@ -115,6 +115,7 @@ def load():
         "phj_partitioned_download": (i, [P, C.POINTER(Partitioned), P, P, P]),
         "phj_hash_keys": (i, [P, i, u64, P, u64, P]),
         "phj_timers_report": (i, [P, C.POINTER(JoinResult)]),
+        "phj_join_partitioned_async": (i, [P, C.POINTER(JoinParams), i, C.POINTER(Partitioned), P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

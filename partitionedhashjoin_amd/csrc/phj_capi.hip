@@ -1025,6 +1025,22 @@ int phj_join_partitioned(phj_ctx* c, const phj_join_params* p, int nbuild, const
     return rc;
 }
 
+int phj_join_partitioned_async(phj_ctx* c, const phj_join_params* p, int nbuild, const phj_partitioned* build,
+                               uint64_t* dev_count) {
+    if (!c) return PHJ_ERR_INVALID;
+    if (!build || !dev_count) return set_err(c, PHJ_ERR_INVALID, "null build segments or count address");
+    if (p && p->algo != PHJ_ALGO_RADIX)
+        return set_err(c, PHJ_ERR_INVALID, "phj_join_partitioned_async needs PHJ_ALGO_RADIX");
+    (void)hipGetLastError();
+    Plan pl;
+    PHJ_TRY(make_plan(c, p, pl));
+    PHJ_HIP(c, hipSetDevice(c->device));
+    hipEvent_t b0, b1, p1;
+    PHJ_TRY(build_and_probe(c, pl, nbuild, build, &b0, &b1, &p1));
+    PHJ_HIP(c, hipMemcpyAsync(dev_count, c->count.p, 8, hipMemcpyDeviceToDevice, c->ks));
+    return PHJ_OK;
+}
+
 int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
     if (!c || !r) return PHJ_ERR_INVALID;
     (void)hipGetLastError();
@@ -1082,7 +1098,17 @@ int phj_partitioned_download(phj_ctx* c, const phj_partitioned* v, int64_t* keys
     if (bounds)
         PHJ_HIP(c, hipMemcpyAsync(bounds, v->bounds, (static_cast<size_t>(v->num_partitions) + 1) * 4,
                                   hipMemcpyDefault, c->ks));
-    PHJ_HIP(c, hipStreamSynchronize(c->ks));
+    // device-only destinations stay stream-ordered; host destinations need the wait
+    auto on_device = [](const void* ptr) {
+        if (!ptr) return true;
+        hipPointerAttribute_t at{};
+        if (hipPointerGetAttributes(&at, ptr) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        return at.type == hipMemoryTypeDevice;
+    };
+    if (!(on_device(keys) && on_device(payloads) && on_device(bounds))) PHJ_HIP(c, hipStreamSynchronize(c->ks));
     return PHJ_OK;
 }
 

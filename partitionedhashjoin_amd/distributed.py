@@ -39,13 +39,21 @@ def max_shard(n: int, world: int) -> int:
 class DistResult:
     matches: int             # global semi-join count (all-reduced)
     local_matches: int
-    build_ms: float          # this rank's device phases (hipEvents)
-    probe_ms: float
-    timers: list
+    timers: list             # this rank's per-kernel device timers (name, ms, bytes)
+
+
+def pack_layout(maxn: int, P: int):
+    """int64 elements of one rank's packed build shard: keys[maxn] | payloads[maxn]
+    | bounds[P+1] (uint32, two per element). maxn is padded to 64 elements so
+    every column stays 16-B aligned inside the gathered buffer."""
+    maxn = (maxn + 63) // 64 * 64
+    return maxn, 2 * maxn + (P + 2) // 2
 
 
 class HipShardEngine:
-    """Per-rank engine over libphj_hip.so; tensors live on the rank's GPU."""
+    """Per-rank engine over libphj_hip.so; tensors live on the rank's GPU and
+    every kernel runs on torch's current stream, so the RCCL collectives and
+    the joins are ordered without host synchronization."""
 
     def __init__(self, device: int):
         import torch
@@ -54,8 +62,12 @@ class HipShardEngine:
         self.device = torch.device("cuda", device)
         torch.cuda.set_device(self.device)
         self.ctx = Context(device)
-        # run every kernel on torch's current stream so RCCL collectives order after them
-        self.ctx.set_stream(torch.cuda.current_stream(self.device).cuda_stream)
+        # one explicit stream shared by torch (allocations, copies, RCCL's stream
+        # dependency) and the ctx kernels; torch's legacy default stream is handle 0,
+        # which the C ABI takes as "create an own stream", so it cannot be shared
+        self.stream = torch.cuda.Stream(self.device)
+        torch.cuda.set_stream(self.stream)
+        self.ctx.set_stream(self.stream.cuda_stream)
 
     def tensor(self, n, dtype):
         return self.torch.empty(int(n), dtype=dtype, device=self.device)
@@ -69,38 +81,48 @@ class HipShardEngine:
     def partition(self, side, params):
         return self.ctx.partition(side, params)
 
-    def export(self, view, maxn):
-        """Copy a partitioned build view into fixed-size tensors for the all-gather."""
+    def pack(self, view, maxn, P):
+        """Stream-ordered device copy of a partitioned build view into the packed layout."""
         import ctypes as C
-        torch = self.torch
-        keys = self.tensor(maxn, torch.int64)
-        pays = self.tensor(maxn, torch.int64)
-        bounds = self.tensor(view.num_partitions + 1, torch.int32)
+        maxn, E = pack_layout(maxn, P)
+        send = self.tensor(E, self.torch.int64)
+        base = send.data_ptr()
         L = self.ctx._L
-        self.ctx._check(L.phj_partitioned_download(self.ctx._h, C.byref(view),
-                                                   C.c_void_p(keys.data_ptr()),
-                                                   C.c_void_p(pays.data_ptr()),
-                                                   C.c_void_p(bounds.data_ptr())))
-        return keys, pays, bounds
+        self.ctx._check(L.phj_partitioned_download(self.ctx._h, C.byref(view), C.c_void_p(base),
+                                                   C.c_void_p(base + maxn * 8),
+                                                   C.c_void_p(base + 2 * maxn * 8)))
+        return send
 
-    def join_gathered(self, params, keys_all, pays_all, bounds_all, sizes, maxn, P):
+    def _count(self):
+        c = self.torch.zeros(1, dtype=self.torch.int64, device=self.device)
+        return c
+
+    def join_packed(self, params, recv, sizes, maxn, P):
+        """Build over every rank's gathered shard, probe the local S shard; returns
+        the local count as a device tensor (nothing waits on the host)."""
         from ._capi import Partitioned
+        maxn, E = pack_layout(maxn, P)
+        base = recv.data_ptr()
         segs = []
         for g, n in enumerate(sizes):
             v = Partitioned()
-            v.keys = keys_all.data_ptr() + g * maxn * 8
-            v.payloads = pays_all.data_ptr() + g * maxn * 8
-            v.bounds = bounds_all.data_ptr() + g * (P + 1) * 4
+            v.keys = base + (g * E) * 8
+            v.payloads = base + (g * E + maxn) * 8
+            v.bounds = base + (g * E + 2 * maxn) * 8
             v.n = n
             v.num_partitions = P
             segs.append(v)
-        return self.ctx.join_partitioned(params, segs)
+        cnt = self._count()
+        self.ctx.join_partitioned_async(params, segs, cnt.data_ptr())
+        return cnt
 
     def join_local(self, params, view):
-        return self.ctx.join_partitioned(params, [view])
+        cnt = self._count()
+        self.ctx.join_partitioned_async(params, [view], cnt.data_ptr())
+        return cnt
 
-    def count_tensor(self, value):
-        return self.torch.tensor([value], dtype=self.torch.int64, device=self.device)
+    def timers(self):
+        return self.ctx.timers_report().timers()
 
 
 def _all_gather(dist, out, inp):
@@ -126,46 +148,42 @@ def _all_reduce(dist, t):
 def distributed_join(engine, params, nR: int, nS: int, rank: int, world: int, dist=None):
     """Join the range-sharded relations already resident on every rank.
 
-    engine.partition(side) partitions this rank's shard (R side 0, S side 1).
-    With world == 1 no collective runs.
+    One step, all on the rank's compute stream: partition R; pack it; start the
+    all-gather (RCCL, asynchronous); partition S meanwhile; wait for the
+    gather; build + probe; all-reduce the count. The host waits once, for the
+    final count. With world == 1 no collective runs.
     """
     torch = engine.torch
     view = engine.partition(0, params)
     P = view.num_partitions
-    maxn = max_shard(nR, world)
     sizes = [hi - lo for lo, hi in (shard_range(nR, r, world) for r in range(world))]
     if world > 1:
-        keys, pays, bounds = engine.export(view, maxn)
-        keys_all = engine.tensor(world * maxn, torch.int64)
-        pays_all = engine.tensor(world * maxn, torch.int64)
-        bounds_all = engine.tensor(world * (P + 1), torch.int32)
-        works = [_all_gather(dist, keys_all, keys), _all_gather(dist, pays_all, pays),
-                 _all_gather(dist, bounds_all, bounds)]
+        maxn = max_shard(nR, world)
+        send = engine.pack(view, maxn, P)
+        recv = engine.tensor(world * send.numel(), torch.int64)
+        work = _all_gather(dist, recv, send)
         engine.partition(1, params)         # overlaps the exchange
-        for w in works:
-            if w is not None:
-                w.wait()
-        res = engine.join_gathered(params, keys_all, pays_all, bounds_all, sizes, maxn, P)
-        cnt = engine.count_tensor(res.matches)
+        if work is not None:
+            work.wait()
+        cnt = engine.join_packed(params, recv, sizes, maxn, P)
+        local = cnt.clone()
         _all_reduce(dist, cnt)
         total = int(cnt.item())
+        local = int(local.item())
     else:
         engine.partition(1, params)
-        res = engine.join_local(params, view)
-        total = int(res.matches)
-    timers = res.timers() if hasattr(res, "timers") else []
-    return DistResult(matches=total, local_matches=int(res.matches),
-                      build_ms=float(getattr(res, "build_ms", 0.0)),
-                      probe_ms=float(getattr(res, "probe_ms", 0.0)), timers=timers)
+        cnt = engine.join_local(params, view)
+        total = local = int(cnt.item())
+    return DistResult(matches=total, local_matches=local, timers=engine.timers())
 
 
-def gathered_segments_numpy(keys_all, pays_all, bounds_all, sizes, maxn, P):
-    """Split gathered buffers back into per-rank (keys, payloads, bounds) numpy views."""
-    keys_all = np.asarray(keys_all)
-    pays_all = np.asarray(pays_all)
-    bounds_all = np.asarray(bounds_all).astype(np.int64) & 0xFFFFFFFF
+def unpack_segments_numpy(recv, sizes, maxn, P):
+    """Split a gathered packed buffer back into per-rank (keys, payloads, bounds)."""
+    maxn, E = pack_layout(maxn, P)
+    recv = np.asarray(recv)
     segs = []
     for g, n in enumerate(sizes):
-        segs.append((keys_all[g * maxn:g * maxn + n], pays_all[g * maxn:g * maxn + n],
-                     bounds_all[g * (P + 1):(g + 1) * (P + 1)]))
+        blk = recv[g * E:(g + 1) * E]
+        bounds = blk[2 * maxn:].view(np.uint32)[:P + 1].astype(np.int64)
+        segs.append((blk[:n], blk[maxn:maxn + n], bounds))
     return segs

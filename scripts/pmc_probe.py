@@ -3,6 +3,7 @@
 (k_count_range reads the 200M-tuple relation: 3.2 GB, 16 B per lane) and
 `--steps` radix joins on the C2 workload."""
 import argparse
+import json
 import os
 import sys
 
@@ -25,3 +26,4 @@ c.count_in_range(1, 1, args.primary)
 for _ in range(args.steps):
     r = c.join(params)
 print("matches", r.matches)
+print("TIMERS " + json.dumps([t[0] for t in r.timers()]))

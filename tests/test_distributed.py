@@ -14,8 +14,8 @@ import torch.multiprocessing as mp
 
 import partitionedhashjoin_amd as phj
 from oracle import oracle as O
-from partitionedhashjoin_amd.distributed import (distributed_join, gathered_segments_numpy,
-                                                 max_shard, shard_range)
+from partitionedhashjoin_amd.distributed import (distributed_join, max_shard, pack_layout, shard_range,
+                                                 unpack_segments_numpy)
 
 
 class _View:
@@ -23,15 +23,6 @@ class _View:
         self.keys, self.pays, self.bounds = keys, pays, bounds
         self.n = keys.shape[0]
         self.num_partitions = P
-
-
-class _Res:
-    def __init__(self, matches):
-        self.matches = matches
-        self.build_ms = self.probe_ms = 0.0
-
-    def timers(self):
-        return []
 
 
 class OracleShardEngine:
@@ -58,11 +49,13 @@ class OracleShardEngine:
         self.views[side] = v
         return v
 
-    def export(self, v, maxn):
-        keys, pays = torch.zeros(maxn, dtype=torch.int64), torch.zeros(maxn, dtype=torch.int64)
-        keys[:v.n] = torch.from_numpy(v.keys)
-        pays[:v.n] = torch.from_numpy(v.pays)
-        return keys, pays, torch.from_numpy(v.bounds.astype(np.int64)).to(torch.int32)
+    def pack(self, v, maxn, P):
+        maxn, E = pack_layout(maxn, P)
+        buf = np.zeros(E, dtype=np.int64)
+        buf[:v.n] = v.keys
+        buf[maxn:maxn + v.n] = v.pays
+        buf[2 * maxn:].view(np.uint32)[:P + 1] = v.bounds.astype(np.uint32)
+        return torch.from_numpy(buf)
 
     def _count(self, params, segs):
         P, radix = self._geometry(params)
@@ -72,17 +65,16 @@ class OracleShardEngine:
             expect = np.repeat(np.arange(P), np.diff(bounds.astype(np.int64)))
             assert np.array_equal(q, expect)
         rkeys = np.concatenate([k for k, _, _ in segs]) if segs else np.zeros(0, dtype=np.int64)
-        return _Res(O.semijoin_count_keys(rkeys, self.views[1].keys))
+        return torch.tensor([O.semijoin_count_keys(rkeys, self.views[1].keys)], dtype=torch.int64)
 
-    def join_gathered(self, params, keys_all, pays_all, bounds_all, sizes, maxn, P):
-        return self._count(params, gathered_segments_numpy(keys_all.numpy(), pays_all.numpy(),
-                                                           bounds_all.numpy(), sizes, maxn, P))
+    def join_packed(self, params, recv, sizes, maxn, P):
+        return self._count(params, unpack_segments_numpy(recv.numpy(), sizes, maxn, P))
 
     def join_local(self, params, v):
         return self._count(params, [(v.keys, v.pays, v.bounds)])
 
-    def count_tensor(self, value):
-        return torch.tensor([int(value)], dtype=torch.int64)
+    def timers(self):
+        return []
 
 
 def _tables(nR, nS, alpha, seed):

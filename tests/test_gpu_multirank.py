@@ -1,5 +1,5 @@
 """Multi-rank HIP path on one GPU: two ranks share cuda:0 over gloo (RCCL
-refuses two ranks on one device), so the real HipShardEngine export /
+refuses two ranks on one device), so the real HipShardEngine pack /
 all-gather / multi-segment join / count all-reduce run end to end."""
 import os
 import socket
@@ -25,11 +25,19 @@ def _worker(rank, world, port, nR, nS, alpha, out):
     try:
         import partitionedhashjoin_amd as phj
         from partitionedhashjoin_amd.distributed import HipShardEngine, distributed_join
+        from partitionedhashjoin_amd.distributed import shard_range
         eng = HipShardEngine(0)
-        eng.generate(nR, nS, alpha, 77, rank, world)
-        inrange = eng.ctx.count_in_range(1, 1, nR)
-        res = distributed_join(eng, phj.radix_params((8, 8)), nR, nS, rank, world, dist)
-        out[rank] = (res.matches, inrange, res.local_matches)
+        # R holds keys [1 + off, |R| + off], S draws from [1, |R|]: S keys below
+        # 1 + off miss, so the expected count is the S keys in [1 + off, |R|]
+        off = nR // 3
+        rlo, rhi = shard_range(nR, rank, world)
+        slo, shi = shard_range(nS, rank, world)
+        eng.ctx.generate_sequential(0, rhi - rlo, 1 + off, rlo)
+        eng.ctx.generate_zipf(1, shi - slo, alpha, 1, nR, 77, slo)
+        expect_local = eng.ctx.count_in_range(1, 1 + off, nR)
+        for _ in range(2):   # a second step reuses every buffer
+            res = distributed_join(eng, phj.radix_params((8, 8)), nR, nS, rank, world, dist)
+        out[rank] = (res.matches, expect_local, res.local_matches)
     finally:
         dist.destroy_process_group()
 
@@ -40,10 +48,11 @@ def test_hip_engine_multirank_on_one_gpu(world):
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_worker, args=(world, _free_port(), nR, nS, 1.25, out), nprocs=world)
-    # every S key is in [1, |R|]: the global count is |S|; local counts sum to it
-    assert {out[r][0] for r in range(world)} == {nS}
-    assert sum(out[r][1] for r in range(world)) == nS
-    assert sum(out[r][2] for r in range(world)) == nS
+    expect = sum(out[r][1] for r in range(world))
+    assert 0 < expect < nS
+    assert {out[r][0] for r in range(world)} == {expect}
+    # each rank's local count is exactly its own S shard's matches
+    assert all(out[r][2] == out[r][1] for r in range(world))
 
 
 def test_single_rank_generation_matches_sharded_generation():

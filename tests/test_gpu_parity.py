@@ -179,9 +179,39 @@ def test_join_partitioned_multi_segment(ctx):
         ctx.partition(phj.SIDE_PROBE, p)
         r = ctx.join_partitioned(p, segs)
         assert r.matches == O.semijoin_count(R, S)
+        # asynchronous form: the count lands in device memory, stream-ordered
+        import torch
+        cnt = torch.full((1,), -1, dtype=torch.int64, device="cuda:0")
+        torch.cuda.synchronize()
+        ctx.join_partitioned_async(p, segs, cnt.data_ptr())
+        ctx.synchronize()
+        assert int(cnt.item()) == r.matches
+        t = ctx.timers_report().timers()
+        assert {"build", "probe"} <= {name for name, _, _ in t}
     finally:
         for c in ctxs:
             c.close()
+
+
+def test_partitioned_download_to_device_is_stream_ordered(ctx):
+    import torch
+    rng = np.random.default_rng(5)
+    rel = np.stack([rng.integers(0, 1 << 40, 70_001, dtype=np.int64), np.arange(70_001, dtype=np.int64)], axis=1)
+    p = phj.radix_params((6, 5), hash=phj.HASH_XXH3, seed=SEED)
+    ctx.upload(phj.SIDE_PROBE, rel)
+    v = ctx.partition(phj.SIDE_PROBE, p)
+    hk, hp, hb = ctx.download_partitioned(v)
+    dk = torch.zeros(v.n, dtype=torch.int64, device="cuda:0")
+    dp = torch.zeros(v.n, dtype=torch.int64, device="cuda:0")
+    db = torch.zeros(v.num_partitions + 1, dtype=torch.int32, device="cuda:0")
+    torch.cuda.synchronize()
+    import ctypes as C
+    ctx._check(ctx._L.phj_partitioned_download(ctx._h, C.byref(v), C.c_void_p(dk.data_ptr()),
+                                               C.c_void_p(dp.data_ptr()), C.c_void_p(db.data_ptr())))
+    ctx.synchronize()
+    assert np.array_equal(dk.cpu().numpy(), hk)
+    assert np.array_equal(dp.cpu().numpy(), hp)
+    assert np.array_equal(db.cpu().numpy().view(np.uint32), hb)
 
 
 def test_gpu_generators(ctx):

@@ -1,0 +1,37 @@
+"""Measurement tooling that runs without a GPU: PMC dispatch attribution
+(scripts/pmc.py) used by bench.py's roofline traffic."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "scripts"))
+import pmc  # noqa: E402
+
+
+def _rows(names, counter="FETCH_SIZE"):
+    return [{"Dispatch_Id": str(i + 1), "Kernel_Name": n, "Counter_Name": counter, "Counter_Value": str(i)}
+            for i, n in enumerate(names)]
+
+
+def test_attribution_takes_the_last_join_in_order():
+    join = ["void phj::k_hist<512, 8, true, 1>(phj::PassArgs)", "phj::k_scan_reduce(phj::ScanArgs)",
+            "void phj::k_scatter<512, 8, true, true, 1>(phj::PassArgs)", "void phj::k_hist_col<4096, unsigned char>",
+            "void phj::k_scatter<512, 8, true, false, 1>(phj::PassArgs)", "phj::k_join_prep(...)",
+            "void phj::k_build_small<1>(phj::BuildArgs)", "void phj::k_build_big<1>(phj::BuildArgs)",
+            "void phj::k_probe<1, 8, 2>(phj::ProbeArgs)"]
+    names = ["phj::k_count_range(...)"] + join + join   # two joins: the second one is reported
+    timers = ["S.p1.hist", "S.p1.scan", "S.p1.scatter", "S.p2.hist", "S.p2.scan", "S.p2.scatter", "build", "probe"]
+    got = pmc.attribute(_rows(names), timers)
+    off = 1 + len(join)
+    assert got["S.p1.hist"]["FETCH_SIZE"] == off + 0
+    assert got["S.p1.scatter"]["FETCH_SIZE"] == off + 2
+    assert got["S.p2.hist"]["FETCH_SIZE"] == off + 3
+    assert got["S.p2.scatter"]["FETCH_SIZE"] == off + 4
+    assert got["build"]["FETCH_SIZE"] == off + 6
+    assert got["probe"]["FETCH_SIZE"] == off + 8
+    assert "S.p1.scan" not in got
+
+
+def test_hbm_bytes_gfx950_correction():
+    per = {"probe": {"FETCH_SIZE": 100.0, "WRITE_SIZE": 10.0}, "build": {"FETCH_SIZE": 1.0}}
+    assert pmc.hbm_bytes(per) == {"probe": (200 + 10) * 1024}
