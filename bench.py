@@ -138,9 +138,13 @@ def main():
     # correctness gate at full size: every generated S key lies in [1, |R|]
     local_inrange = engine.ctx.count_in_range(1, 1, nR)
 
+    radix = params.algo == phj.ALGO_RADIX
+
     def step():
-        if params.algo == phj.ALGO_RADIX:
-            return distributed_join(engine, params, nR, nS, rank, world, dist if world > 1 else None)
+        if radix:
+            # per-kernel timers accumulate on the device; read once after the timed loop
+            return distributed_join(engine, params, nR, nS, rank, world, dist if world > 1 else None,
+                                    timers=False)
         r = engine.ctx.join(params)
 
         class _R:
@@ -157,19 +161,26 @@ def main():
         torch.cuda.synchronize()
 
     barrier()
+    if radix:
+        engine.timers()   # drop the warm-up records
     t0 = time.perf_counter()
     acc = {}
     matches = None
+
+    def accumulate(timers):
+        for name, ms, nbytes in timers:
+            a = acc.setdefault(name, [0.0, 0])
+            a[0] += ms
+            a[1] += nbytes
+
     for _ in range(args.steps):
         res = step()
         matches = res.matches
-        for name, ms, nbytes in res.timers:
-            a = acc.setdefault(name, [0.0, 0, 0])
-            a[0] += ms
-            a[1] += nbytes
-            a[2] += 1
+        accumulate(res.timers)
     barrier()
     elapsed = time.perf_counter() - t0
+    if radix:
+        accumulate(engine.timers())   # sums over the timed steps (hipEvents on the engine stream)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -88,8 +88,9 @@ typedef struct phj_join_result {
     uint64_t algorithmic_bytes;  /* HBM bytes the algorithm must move */
     uint32_t num_partitions;     /* final partition count (radix) */
     uint32_t num_timers;
-    double timer_ms[PHJ_MAX_TIMERS];        /* per-kernel device time (hipEvents on the ctx stream) */
-    uint64_t timer_bytes[PHJ_MAX_TIMERS];   /* algorithmic bytes of that launch */
+    double timer_ms[PHJ_MAX_TIMERS];        /* per-kernel device time (hipEvents on the ctx stream),
+                                               summed over the records of that name */
+    uint64_t timer_bytes[PHJ_MAX_TIMERS];   /* algorithmic bytes of those launches (summed) */
     char timer_name[PHJ_MAX_TIMERS][PHJ_TIMER_NAME];
 } phj_join_result;
 
@@ -159,7 +160,8 @@ int phj_join_partitioned(phj_ctx *ctx, const phj_join_params *p, int nbuild,
 int phj_join_partitioned_async(phj_ctx *ctx, const phj_join_params *p, int nbuild,
                                const phj_partitioned *build, uint64_t *dev_count);
 /* Per-kernel device timers recorded since the last report (e.g. after
- * phj_partition calls); synchronizes the ctx stream, then resets. */
+ * phj_partition / phj_join_partitioned_async calls, possibly several joins),
+ * summed by timer name; synchronizes the ctx stream, then resets. */
 int phj_timers_report(phj_ctx *ctx, phj_join_result *r);
 /* Copy a partitioned view (keys, payloads: n; bounds: P+1) to host or device
  * buffers (any may be NULL). Synchronous when any destination is host memory;

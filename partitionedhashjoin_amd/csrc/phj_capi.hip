@@ -46,10 +46,14 @@ struct Tuning {
     int wc_lw = 8;        // WC line: elements per column (8 = 64 B, 16 = 128 B)
     int wc_wgs = 1024;    // target workgroups per WC pass (super-tile size follows)
     bool r_aux = false;   // partition R on the aux stream (no gain measured: DESIGN.md)
-    int probe_items = 8;  // S keys per lane per probe work item (8 or 16)
+    int probe_items = 8;  // block probe: S keys per lane per work item (8 or 16)
+    int probe_wave = 1;   // wave-per-item probe: 0 never, 1 small partitions (auto), 2 always
     int block = 512;      // threads per workgroup of the tile kernels (256, 512 or 1024; tile_shape)
     bool nt_store = false; // nontemporal scatter stores
     bool dcol = true;     // 2-pass: pass 1 writes the pass-2 digit column
+    unsigned ev_flags = hipEventDisableSystemFence;  // timer / ordering events
+    bool fused = true;    // radix join: fused per-partition LDS build + probe when partitions are small
+    int fused_kpl = 4;    // fused join: S keys per lane per probe round (4 or 8)
 };
 
 int env_int(const char* name, int dflt) {
@@ -77,6 +81,7 @@ struct TimerRec {
     std::string name;
     uint64_t bytes;
     hipEvent_t a, b;
+    int split = 0;   // 1 / 2: the build / probe share of a fused join launch (ctx->split clocks)
 };
 
 struct SideState {
@@ -117,11 +122,13 @@ struct phj_ctx {
     SideState side[2];
     DevBuf scan_partials, prep, tkeys, tpays, toffs, gcursor, items, count, biglist;
     DevBuf np_tab, np_pays;
+    DevBuf fitems, split;   // fused join: item slots; wave clocks {build, probe} since the last timer reset
     std::vector<hipEvent_t> evpool;
     size_t evnext = 0;
     std::vector<TimerRec> timers;
     std::string err;
     Tuning tune;
+    bool last_fused = false;   // the last build_and_probe ran the fused kernel
 };
 
 namespace {
@@ -181,8 +188,17 @@ void free_buf(DevBuf& b) {
 
 hipEvent_t next_event(phj_ctx* c) {
     if (c->evnext == c->evpool.size()) {
-        hipEvent_t e;
-        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        hipEvent_t e = nullptr;
+        // timing / same-device ordering only: no system-scope fence (a default
+        // event's system-scope writeback costs ~10 us per record); the first
+        // flag set the runtime accepts is used
+        const unsigned tries[3] = {c->tune.ev_flags, hipEventReleaseToDevice, hipEventDefault};
+        for (unsigned f : tries) {
+            if (hipEventCreateWithFlags(&e, f) == hipSuccess) break;
+            (void)hipGetLastError();
+            e = nullptr;
+        }
+        if (!e) return nullptr;
         c->evpool.push_back(e);
     }
     return c->evpool[c->evnext++];
@@ -204,21 +220,61 @@ int timer_begin(phj_ctx* c, const char* name, uint64_t bytes) {
 
 int timer_end(phj_ctx* c) { return mark(c, &c->timers.back().b); }
 
+// One launch reported as two timers (build, probe) split by the kernel's own clocks.
+int timer_begin_split(phj_ctx* c, uint64_t build_bytes, uint64_t probe_bytes) {
+    PHJ_TRY(timer_begin(c, "build", build_bytes));
+    c->timers.back().split = 1;
+    c->timers.push_back(TimerRec{"probe", probe_bytes, c->timers.back().a, nullptr, 2});
+    return PHJ_OK;
+}
+
+int timer_end_split(phj_ctx* c) {
+    PHJ_TRY(mark(c, &c->timers.back().b));
+    c->timers[c->timers.size() - 2].b = c->timers.back().b;
+    return PHJ_OK;
+}
+
+constexpr size_t kMaxTimerRecs = 1u << 14;
+
 void reset_timers(phj_ctx* c) {
     c->timers.clear();
     c->evnext = 0;
+    if (c->split.p) (void)hipMemsetAsync(c->split.p, 0, 16, c->ks);
 }
 
+// Build share of the fused join launches since the last reset (wave clocks).
+double fused_build_fraction(phj_ctx* c) {
+    unsigned long long cyc[2] = {0, 0};
+    if (!c->split.p || hipMemcpyAsync(cyc, c->split.p, 16, hipMemcpyDeviceToHost, c->ks) != hipSuccess ||
+        hipStreamSynchronize(c->ks) != hipSuccess)
+        return 0.5;
+    const double t = static_cast<double>(cyc[0]) + static_cast<double>(cyc[1]);
+    return t > 0 ? static_cast<double>(cyc[0]) / t : 0.5;
+}
+
+// Timers aggregated by name (sums over every record since the last reset:
+// one join, or many when a caller reports once after several joins).
 int fill_timers(phj_ctx* c, phj_join_result* r) {
     r->num_timers = 0;
+    double fb = -1.0;
     for (const TimerRec& t : c->timers) {
-        if (r->num_timers >= PHJ_MAX_TIMERS) break;
         float ms = 0;
         PHJ_HIP(c, hipEventElapsedTime(&ms, t.a, t.b));
-        const uint32_t i = r->num_timers++;
-        r->timer_ms[i] = ms;
-        r->timer_bytes[i] = t.bytes;
-        std::snprintf(r->timer_name[i], PHJ_TIMER_NAME, "%s", t.name.c_str());
+        if (t.split) {
+            if (fb < 0) fb = fused_build_fraction(c);
+            ms = static_cast<float>(ms * (t.split == 1 ? fb : 1.0 - fb));
+        }
+        uint32_t i = 0;
+        while (i < r->num_timers && std::strncmp(r->timer_name[i], t.name.c_str(), PHJ_TIMER_NAME - 1) != 0) i++;
+        if (i == r->num_timers) {
+            if (r->num_timers >= PHJ_MAX_TIMERS) continue;
+            r->num_timers++;
+            r->timer_ms[i] = 0;
+            r->timer_bytes[i] = 0;
+            std::snprintf(r->timer_name[i], PHJ_TIMER_NAME, "%s", t.name.c_str());
+        }
+        r->timer_ms[i] += ms;
+        r->timer_bytes[i] += t.bytes;
     }
     return PHJ_OK;
 }
@@ -592,6 +648,55 @@ int build_and_probe(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned*
     }
     if (nR >= (1ull << 32) - 1) return set_err(c, PHJ_ERR_RANGE, "build side above 2^32 tuples");
     const uint64_t nS = PS.view.n;
+    if (c->tune.fused && (nR + P - 1) / P * 2 <= static_cast<uint64_t>(kFusedTcap)) {
+        // fused per-partition join with LDS tables (partitions of <= kFusedTcap build tuples
+        // take one round; larger ones several): HashJoin.hpp:267-303
+        const size_t nslots = nS / kFusedChunk + P + 1;
+        PHJ_TRY(ensure(c, c->fitems, nslots * sizeof(FusedItem)));
+        PHJ_TRY(ensure(c, c->count, 16));
+        if (!c->split.p) {
+            PHJ_TRY(ensure(c, c->split, 16));
+            PHJ_HIP(c, hipMemsetAsync(c->split.p, 0, 16, c->ks));
+        }
+        PHJ_HIP(c, hipMemsetAsync(c->count.p, 0, 8, c->ks));
+        PHJ_TRY(mark(c, e_build0));
+        // algorithmic bytes: R keys once (build), S keys once (probe)
+        PHJ_TRY(timer_begin_split(c, nR * 8, nS * 8));
+        hipLaunchKernelGGL(k_fused_items, dim3((P + kWaves - 1) / kWaves), dim3(kBlock), 0, c->ks,
+                           PS.view.bounds, P, static_cast<FusedItem*>(c->fitems.p));
+        PHJ_LAUNCHED(c, "k_fused_items");
+        FusedArgs fa{};
+        fa.L = L;
+        fa.skeys = PS.view.keys;
+        fa.sbounds = PS.view.bounds;
+        fa.items = static_cast<const FusedItem*>(c->fitems.p);
+        fa.nitems = static_cast<uint32_t>(nslots - 1);
+        fa.count = static_cast<unsigned long long*>(c->count.p);
+        fa.cycles = static_cast<unsigned long long*>(c->split.p);
+        fa.seed = pl.seed;
+        const void* kfn;
+        if (c->tune.fused_kpl == 8)
+            kfn = pl.hk == kMurmur3 ? reinterpret_cast<const void*>(&k_join_fused<kMurmur3, 8, kFusedTcap>)
+                                    : reinterpret_cast<const void*>(&k_join_fused<kXXH3, 8, kFusedTcap>);
+        else
+            kfn = pl.hk == kMurmur3 ? reinterpret_cast<const void*>(&k_join_fused<kMurmur3, kFusedKPL, kFusedTcap>)
+                                    : reinterpret_cast<const void*>(&k_join_fused<kXXH3, kFusedKPL, kFusedTcap>);
+        int per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, kBlock, 0) != hipSuccess || per_cu < 1)
+            per_cu = 2;
+        const size_t wblocks = (nslots + kWaves - 1) / kWaves;
+        const uint32_t grid = static_cast<uint32_t>(
+            std::max<size_t>(1, std::min<size_t>(wblocks, static_cast<size_t>(per_cu) * c->num_cus)));
+        void* kargs[] = {&fa};
+        PHJ_HIP(c, hipLaunchKernel(kfn, dim3(grid), dim3(kBlock), kargs, 0, c->ks));
+        PHJ_LAUNCHED(c, "k_join_fused");
+        PHJ_TRY(timer_end_split(c));
+        *e_build1 = c->timers.back().b;
+        *e_probe1 = c->timers.back().b;
+        c->last_fused = true;
+        return PHJ_OK;
+    }
+    c->last_fused = false;
     const size_t stride = static_cast<size_t>(P) + 1;
     PHJ_TRY(ensure(c, c->prep, stride * 3 * 4));
     PHJ_TRY(ensure(c, c->tkeys, nR * 8));
@@ -599,7 +704,15 @@ int build_and_probe(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned*
     const size_t noffs = nR + 2 * static_cast<size_t>(P) + 1;
     PHJ_TRY(ensure(c, c->toffs, noffs * 4));
     PHJ_TRY(ensure(c, c->gcursor, noffs * 4));
-    const uint32_t kChunk = kBlock * static_cast<uint32_t>(c->tune.probe_items);
+    // probe schedule: small per-partition tables (the radix case) -> one wave
+    // per item of <= 512 S keys; larger tables -> one workgroup per item
+    const uint64_t expect_m = (nR + P - 1) / P;
+    // (measured on C2: the wave schedule wins at <= ~800 S keys per partition,
+    // i.e. the multi-GPU shards; the workgroup schedule at 3000)
+    const uint64_t expect_s = (nS + P - 1) / P;
+    const bool wave_probe = c->tune.probe_wave && expect_m * 2 <= kProbeWaveTcap &&
+                            (c->tune.probe_wave > 1 || expect_s <= 1024);
+    const uint32_t kChunk = wave_probe ? 64u * kProbeWaveKPL : kBlock * static_cast<uint32_t>(c->tune.probe_items);
     const size_t item_bound = P + (nS + kChunk - 1) / kChunk;
     PHJ_TRY(ensure(c, c->items, item_bound * sizeof(ProbeItem)));
     PHJ_TRY(ensure(c, c->count, 16));
@@ -639,12 +752,12 @@ int build_and_probe(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned*
     ba.bigcount = static_cast<uint32_t*>(c->count.p) + 2;
     PHJ_HIP(c, hipMemsetAsync(ba.bigcount, 0, 4, c->ks));
     ba.ocap = ocap_wave;
-    const uint32_t sgrid = std::min<uint32_t>((P + kWaves - 1) / kWaves, 4096);
+    const uint32_t sgrid = (P + kWaves - 1) / kWaves;   // one wave per partition
     const size_t slds = static_cast<size_t>(ocap_wave) * 4 * kWaves;
     if (pl.hk == kMurmur3)
-        hipLaunchKernelGGL((k_build_small<kMurmur3>), dim3(sgrid), dim3(kBlock), slds, c->ks, ba);
+        hipLaunchKernelGGL((k_build_small<kMurmur3, kBuildKPL>), dim3(sgrid), dim3(kBlock), slds, c->ks, ba);
     else
-        hipLaunchKernelGGL((k_build_small<kXXH3>), dim3(sgrid), dim3(kBlock), slds, c->ks, ba);
+        hipLaunchKernelGGL((k_build_small<kXXH3, kBuildKPL>), dim3(sgrid), dim3(kBlock), slds, c->ks, ba);
     PHJ_LAUNCHED(c, "k_build_small");
     ba.ocap = ocap_build;
     const size_t blds = 64 + static_cast<size_t>(ocap_build) * 4;
@@ -679,10 +792,15 @@ int build_and_probe(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned*
         else { if (small) PHJ_PROBE_PICK(kXXH3, 16, 2); else PHJ_PROBE_PICK(kXXH3, 16, 8); }
     }
 #undef PHJ_PROBE_PICK
+    if (wave_probe) {
+        if (pl.hk == kMurmur3) kfn = reinterpret_cast<const void*>(&k_probe_wave<kMurmur3, kProbeWaveKPL, kProbeWaveTcap>);
+        else kfn = reinterpret_cast<const void*>(&k_probe_wave<kXXH3, kProbeWaveKPL, kProbeWaveTcap>);
+    }
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, kBlock, 0) != hipSuccess || per_cu < 1) per_cu = 2;
+    const size_t item_blocks = wave_probe ? (item_bound + kWaves - 1) / kWaves : item_bound;
     const uint32_t pgrid = static_cast<uint32_t>(
-        std::max<size_t>(1, std::min<size_t>(item_bound, static_cast<size_t>(per_cu) * c->num_cus)));
+        std::max<size_t>(1, std::min<size_t>(item_blocks, static_cast<size_t>(per_cu) * c->num_cus)));
     void* kargs[] = {&pa};
     PHJ_HIP(c, hipLaunchKernel(kfn, dim3(pgrid), dim3(kBlock), kargs, 0, c->ks));
     PHJ_LAUNCHED(c, "k_probe");
@@ -819,9 +937,16 @@ int phj_ctx_create(int device, phj_ctx** out) {
     c->tune.wc = env_int("PHJ_WC", 0) != 0;
     c->tune.r_aux = env_int("PHJ_R_AUX", 0) != 0;
     c->tune.probe_items = env_int("PHJ_PROBE_ITEMS", 8) == 16 ? 16 : 8;
+    c->tune.probe_wave = env_int("PHJ_PROBE_WAVE", 1);
     c->tune.block = env_int("PHJ_BLOCK", 512);
     c->tune.nt_store = env_int("PHJ_NT", 0) != 0;
     c->tune.dcol = env_int("PHJ_DCOL", 1) != 0;
+    c->tune.fused = env_int("PHJ_FUSED", 1) != 0;
+    c->tune.fused_kpl = env_int("PHJ_FUSED_KPL", 4) == 8 ? 8 : 4;
+    {
+        const int ev = env_int("PHJ_EVENTS", 1);   // 0 default, 1 no system fence, 2 device release
+        c->tune.ev_flags = ev == 0 ? hipEventDefault : ev == 2 ? hipEventReleaseToDevice : hipEventDisableSystemFence;
+    }
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
@@ -991,8 +1116,9 @@ int phj_partition(phj_ctx* c, int side, const phj_join_params* p, phj_partitione
     Plan pl;
     PHJ_TRY(make_plan(c, p, pl));
     PHJ_HIP(c, hipSetDevice(c->device));
-    // timers accumulate until the next phj_join / phj_join_partitioned reports them
-    if (c->timers.size() > PHJ_MAX_TIMERS) reset_timers(c);
+    // timers accumulate until phj_join / phj_join_partitioned / phj_timers_report
+    // reports them; a caller that never reports loses the oldest records
+    if (c->timers.size() > kMaxTimerRecs) reset_timers(c);
     PHJ_TRY(partition_side(c, side, pl));
     if (out) *out = c->side[side].view;
     return PHJ_OK;
@@ -1015,6 +1141,11 @@ int phj_join_partitioned(phj_ctx* c, const phj_join_params* p, int nbuild, const
     r->matches = m;
     r->build_ms = elapsed(c, b0, b1);
     r->probe_ms = elapsed(c, b1, p1);
+    if (c->last_fused) {   // one fused launch: split by the kernel's own build / probe clocks
+        const double t = elapsed(c, b0, p1), fb = fused_build_fraction(c);
+        r->build_ms = t * fb;
+        r->probe_ms = t * (1.0 - fb);
+    }
     r->total_ms = elapsed(c, b0, p1);
     r->num_partitions = pl.Ppad;
     uint64_t nR = 0;
@@ -1073,6 +1204,11 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
     r->partition_ms = elapsed(c, t0, t1);
     r->build_ms = elapsed(c, b0, b1);
     r->probe_ms = elapsed(c, b1, p1);
+    if (c->last_fused) {   // one fused launch: split by the kernel's own build / probe clocks
+        const double t = elapsed(c, b0, p1), fb = fused_build_fraction(c);
+        r->build_ms = t * fb;
+        r->probe_ms = t * (1.0 - fb);
+    }
     r->total_ms = elapsed(c, t0, p1);
     r->num_partitions = pl.Ppad;
     r->algorithmic_bytes = partition_bytes(pl, R.n) + partition_bytes(pl, S.n) + R.n * 32 + S.n * 8 + R.n * 8;

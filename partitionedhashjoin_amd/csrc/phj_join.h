@@ -35,6 +35,9 @@
 namespace phj {
 
 constexpr int kMaxSegs = 16;
+constexpr int kBuildKPL = 8;   // k_build_small: R tuples per lane (64 * 8 = 512 per partition)
+constexpr int kProbeWaveKPL = 8;     // k_probe_wave: S keys per lane per item (512 per item)
+constexpr int kProbeWaveTcap = 512;  // k_probe_wave: staged table keys per wave
 
 struct Seg {
     const int64_t* keys;
@@ -140,16 +143,33 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 // One wave per partition: bucket counting sort of R_p in the wave's LDS slice
-// (the common case: R_p ~ |R| / P tuples). Partitions whose bucket array does
-// not fit are appended to biglist for k_build_big.
-template <int HK>
+// (the common case: R_p ~ |R| / P tuples). R_p may arrive as up to 16 build
+// segments (the shards of every rank after the multi-GPU all-gather): lane g
+// loads segment g's bounds, a wave prefix over the segment sizes maps every
+// flat index of R_p to (segment, row), and all of R_p is loaded ONCE into
+// registers (KPL tuples per lane) and hashed once; counting, the bucket scan
+// and the placement then run from registers and LDS. Partitions with more than
+// 64 * KPL tuples or a bucket array beyond the wave's LDS slice are appended to
+// biglist for k_build_big. The order inside a bucket is irrelevant to the
+// semi-join count (set membership).
+template <int HK, int KPL>
 __global__ __launch_bounds__(kBlock) void k_build_small(BuildArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     uint32_t* cnt = reinterpret_cast<uint32_t*>(smem) + wave * a.ocap;
-    const uint32_t P = a.L.P;
+    const uint32_t P = a.L.P, nseg = a.L.nseg;
     const uint32_t nw = gridDim.x * kWaves;
+    // lane g < nseg holds segment g's columns
+    const int64_t* skeys = lane < nseg ? a.L.seg[lane].keys : nullptr;
+    const int64_t* spays = lane < nseg ? a.L.seg[lane].pays : nullptr;
+    const uint32_t* sbnd = lane < nseg ? a.L.seg[lane].bounds : nullptr;
     for (uint32_t p = blockIdx.x * kWaves + wave; p < P; p += nw) {
+        // table bases and the segments' bounds in one round of loads
+        uint32_t lo = 0, c = 0;
+        if (lane < nseg) {
+            lo = sbnd[p];
+            c = sbnd[p + 1] - lo;
+        }
         const uint32_t kb = a.tkb[p], m = a.tkb[p + 1] - kb;
         const uint32_t ob = a.tob[p], nbk = a.tob[p + 1] - ob - 1;
         uint32_t* offs = a.toffs + ob;
@@ -157,17 +177,41 @@ __global__ __launch_bounds__(kBlock) void k_build_small(BuildArgs a) {
             for (uint32_t i = lane; i <= nbk; i += 64) offs[i] = 0;
             continue;
         }
-        if (nbk > a.ocap) {
+        if (nbk > a.ocap || m > 64u * KPL) {
             if (lane == 0) a.biglist[atomicAdd(a.bigcount, 1u)] = p;
             continue;
         }
+        uint32_t inc = c;   // inclusive prefix of the segment sizes (lanes < 16)
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+            const uint32_t y = __shfl_up(inc, o, 64);
+            if (lane >= static_cast<uint32_t>(o)) inc += y;
+        }
+        const int64_t rowoff = static_cast<int64_t>(lo) - static_cast<int64_t>(inc - c);   // row = flat + rowoff
+        int64_t key[KPL], pay[KPL];
+        uint32_t bkt[KPL];
+#pragma unroll
+        for (int j = 0; j < KPL; j++) {
+            const uint32_t f = j * 64 + lane;
+            uint32_t g = 0;
+            for (uint32_t l = 0; l + 1 < nseg; l++) g += f >= static_cast<uint32_t>(__shfl(inc, l, 64)) ? 1u : 0u;
+            const int64_t ro = __shfl(rowoff, static_cast<int>(g), 64);
+            const int64_t* kp = reinterpret_cast<const int64_t*>(__shfl(reinterpret_cast<intptr_t>(skeys), static_cast<int>(g), 64));
+            const int64_t* pp = reinterpret_cast<const int64_t*>(__shfl(reinterpret_cast<intptr_t>(spays), static_cast<int>(g), 64));
+            key[j] = 0;
+            pay[j] = 0;
+            if (f < m) {
+                const int64_t row = static_cast<int64_t>(f) + ro;
+                key[j] = kp[row];
+                pay[j] = pp[row];
+            }
+        }
         for (uint32_t i = lane; i < nbk; i += 64) cnt[i] = 0;
         wave_lds_sync();
-        for (uint32_t g = 0; g < a.L.nseg; g++) {
-            const Seg& S = a.L.seg[g];
-            const uint32_t lo = S.bounds[p], c = S.bounds[p + 1] - lo;
-            for (uint32_t i = lane; i < c; i += 64)
-                atomicAdd(&cnt[bucket_of(hash64<HK>(static_cast<uint64_t>(S.keys[lo + i]), a.seed), nbk)], 1u);
+#pragma unroll
+        for (int j = 0; j < KPL; j++) {
+            bkt[j] = bucket_of(hash64<HK>(static_cast<uint64_t>(key[j]), a.seed), nbk);
+            if (j * 64 + lane < m) atomicAdd(&cnt[bkt[j]], 1u);
         }
         wave_lds_sync();
         uint32_t carry = 0;
@@ -188,15 +232,12 @@ __global__ __launch_bounds__(kBlock) void k_build_small(BuildArgs a) {
         }
         if (lane == 0) offs[nbk] = m;
         wave_lds_sync();
-        for (uint32_t g = 0; g < a.L.nseg; g++) {
-            const Seg& S = a.L.seg[g];
-            const uint32_t lo = S.bounds[p], c = S.bounds[p + 1] - lo;
-            for (uint32_t i = lane; i < c; i += 64) {
-                const int64_t key = S.keys[lo + i];
-                const uint32_t b = bucket_of(hash64<HK>(static_cast<uint64_t>(key), a.seed), nbk);
-                const uint32_t pos = atomicAdd(&cnt[b], 1u);
-                a.tkeys[kb + pos] = key;
-                a.tpays[kb + pos] = S.pays[lo + i];
+#pragma unroll
+        for (int j = 0; j < KPL; j++) {
+            if (j * 64 + lane < m) {
+                const uint32_t pos = atomicAdd(&cnt[bkt[j]], 1u);
+                a.tkeys[kb + pos] = key[j];
+                a.tpays[kb + pos] = pay[j];
             }
         }
         wave_lds_sync();
@@ -308,13 +349,15 @@ struct ProbeArgs {
 // Probe ITEMS keys per lane in phases so the table reads of all keys are in
 // flight together: bucket bounds, then each bucket's first key, then (rarely)
 // the rest of a bucket. A key counts once (first match, LinearProbing.hpp:160-180).
-template <int HK, int ITEMS, typename KP, typename OP>
+// Key j of this lane is item key j * STRIDE + idx (idx: thread or lane index).
+template <int HK, int ITEMS, int STRIDE = kBlock, typename KP, typename OP>
 __device__ __forceinline__ uint32_t probe_keys(const int64_t (&k)[ITEMS], uint32_t valid_n,
-                                               KP K, OP O, uint32_t nbk, uint64_t seed) {
+                                               KP K, OP O, uint32_t nbk, uint64_t seed,
+                                               uint32_t idx = threadIdx.x) {
     uint32_t lo[ITEMS], hi[ITEMS];
 #pragma unroll
     for (int j = 0; j < ITEMS; j++) {
-        const bool v = static_cast<uint32_t>(j * kBlock) + threadIdx.x < valid_n;
+        const bool v = static_cast<uint32_t>(j * STRIDE) + idx < valid_n;
         const uint32_t b = bucket_of(hash64<HK>(static_cast<uint64_t>(k[j]), seed), nbk);
         lo[j] = v ? O[b] : 0u;
         hi[j] = v ? O[b + 1] : 0u;
@@ -341,6 +384,42 @@ __device__ __forceinline__ uint32_t probe_keys(const int64_t (&k)[ITEMS], uint32
         }
     }
     return hits;
+}
+
+// probe_keys returning one bit per key (bit j: key j of this lane matched).
+template <int HK, int ITEMS, typename KP, typename OP>
+__device__ __forceinline__ uint32_t probe_bits(const int64_t (&k)[ITEMS], uint32_t valid_n, KP K, OP O,
+                                               uint32_t nbk, uint64_t seed, uint32_t lane) {
+    uint32_t lo[ITEMS], hi[ITEMS];
+#pragma unroll
+    for (int j = 0; j < ITEMS; j++) {
+        const bool v = static_cast<uint32_t>(j * 64) + lane < valid_n;
+        const uint32_t b = bucket_of(hash64<HK>(static_cast<uint64_t>(k[j]), seed), nbk);
+        lo[j] = v ? O[b] : 0u;
+        hi[j] = v ? O[b + 1] : 0u;
+    }
+    uint32_t bits = 0;
+    bool more = false;
+#pragma unroll
+    for (int j = 0; j < ITEMS; j++) {
+        const bool nonempty = lo[j] < hi[j];
+        const bool hit = nonempty && K[nonempty ? lo[j] : 0] == k[j];
+        bits |= static_cast<uint32_t>(hit) << j;
+        lo[j] = hit ? hi[j] : lo[j] + 1;
+        more |= lo[j] < hi[j];
+    }
+    if (more) {
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            for (uint32_t t = lo[j]; t < hi[j]; t++) {
+                if (K[t] == k[j]) {
+                    bits |= 1u << j;
+                    break;
+                }
+            }
+        }
+    }
+    return bits;
 }
 
 __device__ __forceinline__ ProbeItem load_item(const ProbeItem* items, uint32_t i, uint32_t n) {
@@ -439,6 +518,317 @@ __global__ __launch_bounds__(kBlock) void k_probe(ProbeArgs a) {
         unsigned long long t = 0;
         for (int w = 0; w < kWaves; w++) t += red[w];
         if (t) atomicAdd(a.count, t);
+    }
+}
+
+// Persistent probe with one WAVE per work item (S chunks of <= 64 * KPL keys):
+// each wave stages its item's table (<= TCAP keys, <= TCAP / 2 + 1 bucket
+// offsets) into its own LDS slice and probes from there, ordered by the wave's
+// own in-order LDS queue: no workgroup barriers, so small items (the
+// multi-GPU case: |S| / (W * P) keys per partition) cost no block-wide
+// synchronisation. The next item's S keys, table keys and offsets are loaded
+// into registers while the current one is probed. Tables beyond the slice
+// are probed in place from global memory.
+template <int HK, int KPL, int TCAP>
+__global__ __launch_bounds__(kBlock) void k_probe_wave(ProbeArgs a) {
+    constexpr int TPL = TCAP / 64;              // staged table keys per lane
+    constexpr int OCAP = TCAP / 2 + 1;          // table_buckets(TCAP) + 1
+    constexpr int OPL = (OCAP + 63) / 64;       // staged offsets per lane
+    __shared__ int64_t lk_all[kWaves][TCAP];
+    __shared__ uint32_t lo_all[kWaves][OPL * 64];
+    __shared__ uint32_t red[kWaves];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int64_t* lk = lk_all[wave];
+    uint32_t* lo = lo_all[wave];
+    const uint32_t n = *a.nitems;
+    const uint32_t W = gridDim.x * kWaves;
+    uint32_t hits = 0;
+
+    uint32_t item = blockIdx.x * kWaves + wave;
+    ProbeItem cur = load_item(a.items, item, n);
+    int64_t k[KPL], tk[TPL];
+    uint32_t to[OPL];
+    auto fetch = [&](const ProbeItem& it, int64_t (&kk)[KPL], int64_t (&tkk)[TPL], uint32_t (&too)[OPL]) {
+#pragma unroll
+        for (int j = 0; j < KPL; j++) {
+            const uint32_t off = j * 64 + lane;
+            kk[j] = off < it.s_cnt ? a.skeys[it.s_lo + off] : 0;
+        }
+        const bool stage = it.m <= static_cast<uint32_t>(TCAP) && it.nbk + 1 <= static_cast<uint32_t>(OCAP);
+#pragma unroll
+        for (int j = 0; j < TPL; j++) {
+            const uint32_t i = j * 64 + lane;
+            tkk[j] = (stage && i < it.m) ? a.tkeys[it.kb + i] : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < OPL; j++) {
+            const uint32_t i = j * 64 + lane;
+            too[j] = (stage && i <= it.nbk) ? a.toffs[it.ob + i] : 0u;
+        }
+    };
+    if (item < n) fetch(cur, k, tk, to);
+    for (; item < n; item += W) {
+        const bool stage = cur.m <= static_cast<uint32_t>(TCAP) && cur.nbk + 1 <= static_cast<uint32_t>(OCAP);
+        if (stage) {
+#pragma unroll
+            for (int j = 0; j < TPL; j++) {
+                const uint32_t i = j * 64 + lane;
+                if (i < cur.m) lk[i] = tk[j];
+            }
+#pragma unroll
+            for (int j = 0; j < OPL; j++) {
+                const uint32_t i = j * 64 + lane;
+                if (i <= cur.nbk) lo[i] = to[j];
+            }
+        }
+        wave_lds_sync();
+        int64_t kc[KPL];
+#pragma unroll
+        for (int j = 0; j < KPL; j++) kc[j] = k[j];
+        const ProbeItem nxt = load_item(a.items, item + W, n);
+        if (item + W < n) fetch(nxt, k, tk, to);
+        if (stage)
+            hits += probe_keys<HK, KPL, 64>(kc, cur.s_cnt, lk, lo, cur.nbk, a.seed, lane);
+        else
+            hits += probe_keys<HK, KPL, 64>(kc, cur.s_cnt, a.tkeys + cur.kb, a.toffs + cur.ob, cur.nbk, a.seed, lane);
+        wave_lds_sync();   // this item's LDS reads before the next item's stores
+        cur = nxt;
+    }
+    uint32_t x = hits;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_down(x, o, 64);
+    if (lane == 0) red[wave] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (int w = 0; w < kWaves; w++) t += red[w];
+        if (t) atomicAdd(a.count, t);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Fused per-partition join (the reference's Join() loop, RadixCluster/
+// HashJoin.hpp:267-303: for each partition, build its hash table, then probe
+// it) with the table in LDS: it never goes to HBM.
+//
+// Work items: partition p's S keys in chunks of <= kFusedChunk; item slots
+// have the closed form itb[p] = floor(sb[p] / kFusedChunk) + p (enough slots
+// for ceil(s_p / chunk) items; the rest are empty), so no scan is needed.
+// One WAVE per item: R_p is gathered from the build segments (lane g loads
+// segment g's bounds, a wave prefix maps flat indices to rows), hashed and
+// counting-sorted into a bucketed table in the wave's LDS slice (<= TCAP keys
+// per round), then the item's S keys are probed 64 * KPL at a time. A
+// partition with more than TCAP build tuples is joined in rounds of TCAP,
+// keeping one hit bit per S key of the item (semi-join: a key counts once).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kFusedChunk = 4096;   // S keys per item (16 probe rounds of 64 x 4)
+constexpr int kFusedKPL = 4;             // S keys per lane per probe round
+constexpr int kFusedTcap = 512;          // build keys per LDS table round
+
+struct FusedItem {
+    uint32_t s_lo, s_cnt, p, pad;
+};
+
+// One wave per partition writes its item slots [itb[p], itb[p+1]).
+__global__ __launch_bounds__(kBlock) void k_fused_items(const uint32_t* sbounds, uint32_t P, FusedItem* items) {
+    const uint32_t p = blockIdx.x * kWaves + (threadIdx.x >> 6);
+    if (p >= P) return;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t sb = sbounds[p], se = sbounds[p + 1];
+    const uint32_t lo = sb / kFusedChunk + p, hi = se / kFusedChunk + p + 1;
+    for (uint32_t i = lo + lane; i < hi; i += 64) {
+        FusedItem it;
+        const uint32_t s0 = sb + (i - lo) * kFusedChunk;
+        it.s_lo = s0;
+        it.s_cnt = s0 < se ? min(kFusedChunk, se - s0) : 0u;
+        it.p = p;
+        it.pad = 0;
+        items[i] = it;
+    }
+}
+
+struct FusedArgs {
+    SegList L;
+    const int64_t* skeys;
+    const uint32_t* sbounds;
+    const FusedItem* items;
+    uint32_t nitems;
+    uint32_t pad;
+    unsigned long long* count;
+    unsigned long long* cycles;   // [0] build, [1] probe: wave clock sums (time split)
+    uint64_t seed;
+};
+
+template <int KPL>
+__device__ __forceinline__ void fused_load_s(const int64_t* skeys, uint32_t lo, uint32_t n, uint32_t lane,
+                                             int64_t (&k)[KPL]) {
+#pragma unroll
+    for (int j = 0; j < KPL; j++) {
+        const uint32_t off = j * 64 + lane;
+        k[j] = off < n ? skeys[lo + off] : 0;
+    }
+}
+
+// Latency schedule per wave: the next item's descriptor is fetched one item
+// ahead; an item's first S sub-chunk is loaded together with its R bounds and
+// R keys; sub-chunk k + 1 is loaded while k is probed.
+template <int HK, int KPL, int TCAP>
+__global__ __launch_bounds__(kBlock) void k_join_fused(FusedArgs a) {
+    constexpr int RPL = TCAP / 64;                 // build keys per lane per round
+    constexpr int OCAP = TCAP / 2 + 1;             // bucket offsets (table_buckets(TCAP) + 1)
+    constexpr uint32_t SUB = 64 * KPL;             // S keys per probe sub-chunk
+    constexpr int NSUB = kFusedChunk / SUB;        // sub-chunks per item (hit bits: NSUB * KPL <= 64)
+    static_assert(NSUB * KPL <= 64, "hit bits per lane");
+    __shared__ int64_t lk_all[kWaves][TCAP];
+    __shared__ uint32_t lo_all[kWaves][OCAP];
+    __shared__ uint32_t cur_all[kWaves][OCAP];
+    __shared__ unsigned long long red[kWaves][3];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int64_t* lk = lk_all[wave];
+    uint32_t* loffs = lo_all[wave];   // bucket starts, [nbk] = keys of the round
+    uint32_t* lcur = cur_all[wave];   // counts, then placement cursors
+    const uint32_t nseg = a.L.nseg;
+    const int64_t* segk = lane < nseg ? a.L.seg[lane].keys : nullptr;
+    const uint32_t* segb = lane < nseg ? a.L.seg[lane].bounds : nullptr;
+    const uint32_t W = gridDim.x * kWaves;
+    unsigned long long hits = 0, cyc_b = 0, cyc_p = 0;
+
+    uint32_t item = blockIdx.x * kWaves + wave;
+    FusedItem it = item < a.nitems ? a.items[item] : FusedItem{0, 0, 0, 0};
+    for (; item < a.nitems; item += W) {
+        const FusedItem nxt = item + W < a.nitems ? a.items[item + W] : FusedItem{0, 0, 0, 0};
+        if (it.s_cnt == 0) {
+            it = nxt;
+            continue;
+        }
+        const uint64_t tb0 = wall_clock64();
+        const uint32_t p = it.p;
+        uint32_t rlo = 0, rc = 0;
+        if (lane < nseg) {
+            rlo = segb[p];
+            rc = segb[p + 1] - rlo;
+        }
+        int64_t sk[KPL];
+        fused_load_s<KPL>(a.skeys, it.s_lo, min(SUB, it.s_cnt), lane, sk);
+        uint32_t inc = rc;
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+            const uint32_t y = __shfl_up(inc, o, 64);
+            if (lane >= static_cast<uint32_t>(o)) inc += y;
+        }
+        const uint32_t m = __shfl(inc, static_cast<int>(nseg - 1), 64);
+        if (m == 0) {   // empty build partition: no S key of p matches
+            it = nxt;
+            continue;
+        }
+        const int64_t rowoff = static_cast<int64_t>(rlo) - static_cast<int64_t>(inc - rc);
+        const uint32_t nsub = (it.s_cnt + SUB - 1) / SUB;
+        uint64_t hitbits = 0;   // bit (sub * KPL + j): S key j of sub-chunk sub matched
+        for (uint32_t rb = 0; rb < m; rb += TCAP) {
+            const uint64_t tb = rb == 0 ? tb0 : wall_clock64();
+            const uint32_t mr = min(static_cast<uint32_t>(TCAP), m - rb);
+            const uint32_t nbk = table_buckets(mr);
+            const uint32_t rj = (mr + 63) / 64;   // rounds of 64 build keys in use
+            int64_t rk[RPL];
+            uint32_t bk[RPL];
+            if (nseg == 1) {   // one build segment (single GPU): plain strided loads
+                const int64_t* kp = a.L.seg[0].keys + __builtin_amdgcn_readfirstlane(rlo);
+#pragma unroll
+                for (int j = 0; j < RPL; j++) {
+                    const uint32_t f = rb + j * 64 + lane;
+                    rk[j] = (static_cast<uint32_t>(j) < rj && j * 64 + lane < mr) ? kp[f] : 0;
+                }
+            } else
+#pragma unroll
+            for (int j = 0; j < RPL; j++) {
+                rk[j] = 0;
+                if (static_cast<uint32_t>(j) < rj) {
+                    const uint32_t f = rb + j * 64 + lane;
+                    uint32_t g = 0;
+                    for (uint32_t l = 0; l + 1 < nseg; l++)
+                        g += f >= static_cast<uint32_t>(__shfl(inc, l, 64)) ? 1u : 0u;
+                    const int64_t ro = __shfl(rowoff, static_cast<int>(g), 64);
+                    const int64_t* kp = reinterpret_cast<const int64_t*>(
+                        __shfl(reinterpret_cast<intptr_t>(segk), static_cast<int>(g), 64));
+                    if (j * 64 + lane < mr) rk[j] = kp[static_cast<int64_t>(f) + ro];
+                }
+            }
+            for (uint32_t i = lane; i < nbk; i += 64) lcur[i] = 0;
+            wave_lds_sync();
+#pragma unroll
+            for (int j = 0; j < RPL; j++) {
+                if (static_cast<uint32_t>(j) < rj) {
+                    bk[j] = bucket_of(hash64<HK>(static_cast<uint64_t>(rk[j]), a.seed), nbk);
+                    if (j * 64 + lane < mr) atomicAdd(&lcur[bk[j]], 1u);
+                }
+            }
+            wave_lds_sync();
+            // exclusive scan: bucket starts (loffs[0..nbk]) and placement cursors
+            uint32_t carry = 0;
+            for (uint32_t base = 0; base < nbk; base += 64) {
+                const uint32_t i = base + lane;
+                const uint32_t v = i < nbk ? lcur[i] : 0u;
+                uint32_t x = v;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const uint32_t y = __shfl_up(x, o, 64);
+                    if (lane >= static_cast<uint32_t>(o)) x += y;
+                }
+                if (i < nbk) {
+                    loffs[i] = carry + x - v;
+                    lcur[i] = carry + x - v;
+                }
+                carry += __shfl(x, 63, 64);
+            }
+            if (lane == 0) loffs[nbk] = mr;
+            wave_lds_sync();
+#pragma unroll
+            for (int j = 0; j < RPL; j++) {
+                if (static_cast<uint32_t>(j) < rj && j * 64 + lane < mr) lk[atomicAdd(&lcur[bk[j]], 1u)] = rk[j];
+            }
+            wave_lds_sync();
+            const uint64_t tp = wall_clock64();
+            cyc_b += tp - tb;
+            // probe the item's S sub-chunks; sub-chunk 0 is already in registers
+            // (reloaded for later rounds of an oversized build partition)
+            if (rb > 0) fused_load_s<KPL>(a.skeys, it.s_lo, min(SUB, it.s_cnt), lane, sk);
+            for (uint32_t sub = 0; sub < nsub; sub++) {
+                int64_t nk[KPL];
+                if (sub + 1 < nsub)
+                    fused_load_s<KPL>(a.skeys, it.s_lo + (sub + 1) * SUB, min(SUB, it.s_cnt - (sub + 1) * SUB), lane, nk);
+                const uint32_t n_sub = min(SUB, it.s_cnt - sub * SUB);
+                hitbits |= static_cast<uint64_t>(probe_bits<HK, KPL>(sk, n_sub, lk, loffs, nbk, a.seed, lane))
+                           << (sub * KPL);
+                if (sub + 1 < nsub) {
+#pragma unroll
+                    for (int j = 0; j < KPL; j++) sk[j] = nk[j];
+                }
+            }
+            wave_lds_sync();   // this round's LDS reads before the next round's stores
+            cyc_p += wall_clock64() - tp;
+        }
+        hits += __popcll(hitbits);
+        it = nxt;
+    }
+    unsigned long long x = hits;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_down(x, o, 64);
+    if (lane == 0) {
+        red[wave][0] = x;
+        red[wave][1] = cyc_b;
+        red[wave][2] = cyc_p;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0, b = 0, q = 0;
+        for (int w = 0; w < kWaves; w++) {
+            t += red[w][0];
+            b += red[w][1];
+            q += red[w][2];
+        }
+        if (t) atomicAdd(a.count, t);
+        atomicAdd(&a.cycles[0], b);
+        atomicAdd(&a.cycles[1], q);
     }
 }
 

@@ -61,13 +61,18 @@ class HipShardEngine:
         self.torch = torch
         self.device = torch.device("cuda", device)
         torch.cuda.set_device(self.device)
+        # S (probe side, the join) on the main stream, shared with torch
+        # (allocations, RCCL's stream dependency); R (build side) partitions on
+        # its own context and stream, concurrently with S. torch's legacy default
+        # stream is handle 0, which the C ABI takes as "create an own stream",
+        # so explicit streams are used.
         self.ctx = Context(device)
-        # one explicit stream shared by torch (allocations, copies, RCCL's stream
-        # dependency) and the ctx kernels; torch's legacy default stream is handle 0,
-        # which the C ABI takes as "create an own stream", so it cannot be shared
         self.stream = torch.cuda.Stream(self.device)
         torch.cuda.set_stream(self.stream)
         self.ctx.set_stream(self.stream.cuda_stream)
+        self.ctx_r = Context(device)
+        self.stream_r = torch.cuda.Stream(self.device)
+        self.ctx_r.set_stream(self.stream_r.cuda_stream)
 
     def tensor(self, n, dtype):
         return self.torch.empty(int(n), dtype=dtype, device=self.device)
@@ -75,22 +80,42 @@ class HipShardEngine:
     def generate(self, nR, nS, alpha, seed, rank, world):
         rlo, rhi = shard_range(nR, rank, world)
         slo, shi = shard_range(nS, rank, world)
-        self.ctx.generate_sequential(0, rhi - rlo, 1, rlo)
+        self.ctx_r.generate_sequential(0, rhi - rlo, 1, rlo)
         self.ctx.generate_zipf(1, shi - slo, alpha, 1, nR, seed, slo)
+        self.share_build()
+
+    def share_build(self):
+        """Make the main context see the R shard owned by the R context (for
+        single-call joins such as NoPartitioning on the main context)."""
+        ptr, n = self.ctx_r.relation_ptr(0)
+        if n:
+            self.ctx.bind_device(0, ptr, n, keepalive=self.ctx_r)
 
     def partition(self, side, params):
+        """Partition this rank's R (side 0, on the R stream) or S (side 1) shard."""
+        if side == 0:
+            return self.ctx_r.partition(0, params)
         return self.ctx.partition(side, params)
 
+    def build_ready(self):
+        """Order the main stream after everything enqueued on the R stream."""
+        ev = self.torch.cuda.Event()
+        ev.record(self.stream_r)
+        self.stream.wait_event(ev)
+
     def pack(self, view, maxn, P):
-        """Stream-ordered device copy of a partitioned build view into the packed layout."""
+        """Device copy of a partitioned R view into the packed send layout, on
+        the R stream; returns the send tensor once the main stream is ordered
+        after it (the all-gather is issued from the main stream)."""
         import ctypes as C
         maxn, E = pack_layout(maxn, P)
-        send = self.tensor(E, self.torch.int64)
+        with self.torch.cuda.stream(self.stream_r):
+            send = self.tensor(E, self.torch.int64)
         base = send.data_ptr()
-        L = self.ctx._L
-        self.ctx._check(L.phj_partitioned_download(self.ctx._h, C.byref(view), C.c_void_p(base),
-                                                   C.c_void_p(base + maxn * 8),
-                                                   C.c_void_p(base + 2 * maxn * 8)))
+        L = self.ctx_r._L
+        self.ctx_r._check(L.phj_partitioned_download(self.ctx_r._h, C.byref(view), C.c_void_p(base),
+                                                     C.c_void_p(base + maxn * 8),
+                                                     C.c_void_p(base + 2 * maxn * 8)))
         return send
 
     def _count(self):
@@ -122,7 +147,24 @@ class HipShardEngine:
         return cnt
 
     def timers(self):
-        return self.ctx.timers_report().timers()
+        t = {}
+        for ctx in (self.ctx_r, self.ctx):
+            for name, ms, nbytes in ctx.timers_report().timers():
+                a = t.setdefault(name, [0.0, 0])
+                a[0] += ms
+                a[1] += nbytes
+        return [(k, v[0], v[1]) for k, v in t.items()]
+
+    def count_in_range(self, side, lo, hi):
+        return (self.ctx_r if side == 0 else self.ctx).count_in_range(side, lo, hi)
+
+
+class _null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
 
 
 def _all_gather(dist, out, inp):
@@ -145,24 +187,34 @@ def _all_reduce(dist, t):
         dist.all_reduce(t)
 
 
-def distributed_join(engine, params, nR: int, nS: int, rank: int, world: int, dist=None):
+def distributed_join(engine, params, nR: int, nS: int, rank: int, world: int, dist=None,
+                     timers: bool = True):
     """Join the range-sharded relations already resident on every rank.
 
     One step, all on the rank's compute stream: partition R; pack it; start the
     all-gather (RCCL, asynchronous); partition S meanwhile; wait for the
     gather; build + probe; all-reduce the count. The host waits once, for the
-    final count. With world == 1 no collective runs.
+    final count. With world == 1 no collective runs. timers=False leaves the
+    per-kernel timers accumulating in the engine (read them once, after many
+    steps, with engine.timers()).
     """
     torch = engine.torch
-    view = engine.partition(0, params)
+    view = engine.partition(0, params)      # R stream
     P = view.num_partitions
     sizes = [hi - lo for lo, hi in (shard_range(nR, r, world) for r in range(world))]
     if world > 1:
         maxn = max_shard(nR, world)
         send = engine.pack(view, maxn, P)
-        recv = engine.tensor(world * send.numel(), torch.int64)
-        work = _all_gather(dist, recv, send)
-        engine.partition(1, params)         # overlaps the exchange
+        engine.partition(1, params)         # main stream, beside R and the exchange
+        # the all-gather waits on R (not on S): it runs on RCCL's stream, issued
+        # from the R stream, while S is still being partitioned
+        side = getattr(engine, "stream_r", None)
+        with torch.cuda.stream(side) if side is not None else _null():
+            recv = engine.tensor(world * send.numel(), torch.int64)
+            work = _all_gather(dist, recv, send)
+        if side is not None:
+            recv.record_stream(engine.stream)
+        engine.build_ready()
         if work is not None:
             work.wait()
         cnt = engine.join_packed(params, recv, sizes, maxn, P)
@@ -172,9 +224,10 @@ def distributed_join(engine, params, nR: int, nS: int, rank: int, world: int, di
         local = int(local.item())
     else:
         engine.partition(1, params)
+        engine.build_ready()
         cnt = engine.join_local(params, view)
         total = local = int(cnt.item())
-    return DistResult(matches=total, local_matches=local, timers=engine.timers())
+    return DistResult(matches=total, local_matches=local, timers=engine.timers() if timers else [])
 
 
 def unpack_segments_numpy(recv, sizes, maxn, P):

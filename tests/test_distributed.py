@@ -76,6 +76,9 @@ class OracleShardEngine:
     def timers(self):
         return []
 
+    def build_ready(self):
+        pass
+
 
 def _tables(nR, nS, alpha, seed):
     R, S = O.generate_tables(nR, nS, alpha, seed, threads=2)

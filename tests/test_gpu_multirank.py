@@ -32,8 +32,9 @@ def _worker(rank, world, port, nR, nS, alpha, out):
         off = nR // 3
         rlo, rhi = shard_range(nR, rank, world)
         slo, shi = shard_range(nS, rank, world)
-        eng.ctx.generate_sequential(0, rhi - rlo, 1 + off, rlo)
+        eng.ctx_r.generate_sequential(0, rhi - rlo, 1 + off, rlo)
         eng.ctx.generate_zipf(1, shi - slo, alpha, 1, nR, 77, slo)
+        eng.share_build()
         expect_local = eng.ctx.count_in_range(1, 1 + off, nR)
         for _ in range(2):   # a second step reuses every buffer
             res = distributed_join(eng, phj.radix_params((8, 8)), nR, nS, rank, world, dist)

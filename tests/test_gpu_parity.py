@@ -193,6 +193,42 @@ def test_join_partitioned_multi_segment(ctx):
             c.close()
 
 
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_hot_build_partition_over_segments(fused, monkeypatch):
+    # one build key repeated 5000 times (its partition exceeds one 512-key LDS
+    # table round of the fused join) next to ordinary keys, split over 4 build
+    # segments; S holds the hot key, ordinary hits and misses
+    monkeypatch.setenv("PHJ_FUSED", fused)
+    rng = np.random.default_rng(17)
+    hot = 123_456_789
+    rk = np.concatenate([np.full(5000, hot, dtype=np.int64), rng.integers(0, 300_000, 40_000, dtype=np.int64)])
+    rng.shuffle(rk)
+    R = np.stack([rk, np.arange(rk.size, dtype=np.int64)], axis=1)
+    sk = np.concatenate([np.full(7000, hot, dtype=np.int64), rng.integers(0, 600_000, 300_000, dtype=np.int64)])
+    rng.shuffle(sk)
+    S = np.stack([sk, np.arange(sk.size, dtype=np.int64)], axis=1)
+    p = phj.radix_params((8, 8), hash=phj.HASH_XXH3, seed=SEED)
+    ctxs = [phj.Context(0) for _ in range(5)]
+    try:
+        segs = []
+        for c, sh in zip(ctxs[1:], np.array_split(R, 4)):
+            c.upload(phj.SIDE_BUILD, sh)
+            segs.append(c.partition(phj.SIDE_BUILD, p))
+            c.synchronize()
+        main = ctxs[0]
+        main.upload(phj.SIDE_PROBE, S)
+        main.partition(phj.SIDE_PROBE, p)
+        r = main.join_partitioned(p, segs)
+        assert r.matches == O.semijoin_count(R, S)
+        assert r.build_ms >= 0 and r.probe_ms >= 0
+        # and the single-call join over the whole relation
+        main.upload(phj.SIDE_BUILD, R)
+        assert main.join(p).matches == r.matches
+    finally:
+        for c in ctxs:
+            c.close()
+
+
 def test_partitioned_download_to_device_is_stream_ordered(ctx):
     import torch
     rng = np.random.default_rng(5)

@@ -5,8 +5,9 @@ between kernel schedules that must produce the same bytes: tile size
 (PHJ_TILE) and workgroup size (PHJ_BLOCK) of the histogram/scatter kernels,
 nontemporal stores (PHJ_NT), pass-1 output layout (PHJ_P1_AOS), the pass-2
 digit column (PHJ_DCOL), tile order
-(PHJ_XCD_REMAP), write-combining scatter (PHJ_WC), probe items
-(PHJ_PROBE_ITEMS). Each is
+(PHJ_XCD_REMAP), write-combining scatter (PHJ_WC), fused LDS join vs HBM
+tables (PHJ_FUSED) and the probe schedule of the latter (PHJ_PROBE_WAVE,
+PHJ_PROBE_ITEMS). Each is
 checked against the oracle's stable partition and semi-join count.
 """
 import numpy as np
@@ -33,7 +34,11 @@ SCHEDULES = [
     {"PHJ_XCD_REMAP": "0"},
     {"PHJ_NT": "1"},
     {"PHJ_WC": "1"},
-    {"PHJ_PROBE_ITEMS": "16"},
+    {"PHJ_PROBE_ITEMS": "16", "PHJ_PROBE_WAVE": "0"},
+    {"PHJ_FUSED": "0", "PHJ_PROBE_WAVE": "0"},
+    {"PHJ_FUSED": "0", "PHJ_PROBE_WAVE": "2"},
+    {"PHJ_FUSED": "0"},
+    {"PHJ_FUSED_KPL": "8"},
 ]
 
 CASES = [((8, 8), 0, phj.HASH_MURMUR3), ((11, 0), 0, phj.HASH_XXH3), ((1, 0), 1000, phj.HASH_XXH3),
