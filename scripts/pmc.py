@@ -30,8 +30,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 FAMILIES = [
     (re.compile(r"\.hist$"), re.compile(r"phj::k_hist")),
     (re.compile(r"\.scatter$"), re.compile(r"phj::k_scatter")),
-    (re.compile(r"^build$"), re.compile(r"phj::k_build_small")),
-    (re.compile(r"^probe$"), re.compile(r"phj::k_probe")),
+    (re.compile(r"^build$"), re.compile(r"phj::k_(build_small|join_fused)")),
+    (re.compile(r"^probe$"), re.compile(r"phj::k_(probe|join_fused)")),
     (re.compile(r"^np\.build$"), re.compile(r"phj::k_np_build")),
     (re.compile(r"^np\.probe$"), re.compile(r"phj::k_np_probe")),
 ]
@@ -76,15 +76,21 @@ def attribute(rows, timers):
     seq = [disp[k] for k in sorted(disp)]
     res = {}
     i = len(seq) - 1
+    shared = None   # the fused join: "build" and "probe" are one dispatch
     for t in reversed(timers):
         fam = family(t)
         if fam is None:
+            continue
+        if shared is not None and fam.search(shared["name"]):
+            res[t] = dict(shared["vals"])
+            shared = None
             continue
         while i >= 0 and not fam.search(seq[i]["name"]):
             i -= 1
         if i < 0:
             break
         res[t] = dict(seq[i]["vals"])
+        shared = seq[i] if "k_join_fused" in seq[i]["name"] else None
         i -= 1
     return res
 

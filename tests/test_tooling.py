@@ -35,3 +35,14 @@ def test_attribution_takes_the_last_join_in_order():
 def test_hbm_bytes_gfx950_correction():
     per = {"probe": {"FETCH_SIZE": 100.0, "WRITE_SIZE": 10.0}, "build": {"FETCH_SIZE": 1.0}}
     assert pmc.hbm_bytes(per) == {"probe": (200 + 10) * 1024}
+
+
+def test_fused_join_is_one_dispatch_for_build_and_probe():
+    join = ["void phj::k_hist<512, 8, true, 1>(phj::PassArgs)", "void phj::k_scatter<512, 8, true, true, 1>",
+            "phj::k_fused_items(...)", "void phj::k_join_fused<1, 4, 512>(phj::FusedArgs)"]
+    names = join + join
+    timers = ["S.p1.hist", "S.p1.scatter", "build", "probe"]
+    got = pmc.attribute(_rows(names), timers)
+    assert got["build"] == got["probe"] == {"FETCH_SIZE": 7.0}
+    assert got["S.p1.scatter"]["FETCH_SIZE"] == 5
+    assert got["S.p1.hist"]["FETCH_SIZE"] == 4
