@@ -191,42 +191,45 @@ def distributed_join(engine, params, nR: int, nS: int, rank: int, world: int, di
                      timers: bool = True):
     """Join the range-sharded relations already resident on every rank.
 
-    One step, all on the rank's compute stream: partition R; pack it; start the
-    all-gather (RCCL, asynchronous); partition S meanwhile; wait for the
-    gather; build + probe; all-reduce the count. The host waits once, for the
+    One step: partition R (R stream); pack it; start the all-gather (RCCL,
+    asynchronous); partition S meanwhile (main stream); wait for the gather;
+    build + probe; all-reduce the count. The host waits once, for the
     final count. With world == 1 no collective runs. timers=False leaves the
     per-kernel timers accumulating in the engine (read them once, after many
     steps, with engine.timers()).
     """
     torch = engine.torch
-    view = engine.partition(0, params)      # R stream
-    P = view.num_partitions
-    sizes = [hi - lo for lo, hi in (shard_range(nR, r, world) for r in range(world))]
-    if world > 1:
-        maxn = max_shard(nR, world)
-        send = engine.pack(view, maxn, P)
-        engine.partition(1, params)         # main stream, beside R and the exchange
-        # the all-gather waits on R (not on S): it runs on RCCL's stream, issued
-        # from the R stream, while S is still being partitioned
-        side = getattr(engine, "stream_r", None)
-        with torch.cuda.stream(side) if side is not None else _null():
-            recv = engine.tensor(world * send.numel(), torch.int64)
-            work = _all_gather(dist, recv, send)
-        if side is not None:
-            recv.record_stream(engine.stream)
-        engine.build_ready()
-        if work is not None:
-            work.wait()
-        cnt = engine.join_packed(params, recv, sizes, maxn, P)
-        local = cnt.clone()
-        _all_reduce(dist, cnt)
-        total = int(cnt.item())
-        local = int(local.item())
-    else:
+    if world == 1:
+        # no exchange waits on R: issue the long S partition first so the GPU
+        # is busy while the host issues R's (small) kernels on the R stream
         engine.partition(1, params)
+        view = engine.partition(0, params)
         engine.build_ready()
         cnt = engine.join_local(params, view)
         total = local = int(cnt.item())
+        return DistResult(matches=total, local_matches=local, timers=engine.timers() if timers else [])
+    view = engine.partition(0, params)      # R stream
+    P = view.num_partitions
+    sizes = [hi - lo for lo, hi in (shard_range(nR, r, world) for r in range(world))]
+    maxn = max_shard(nR, world)
+    send = engine.pack(view, maxn, P)
+    # the all-gather waits on R only: issued from the R stream (RCCL runs it on
+    # its own stream) before the host spends time issuing the S partition
+    side = getattr(engine, "stream_r", None)
+    with torch.cuda.stream(side) if side is not None else _null():
+        recv = engine.tensor(world * send.numel(), torch.int64)
+        work = _all_gather(dist, recv, send)
+    if side is not None:
+        recv.record_stream(engine.stream)
+    engine.partition(1, params)             # main stream, beside the exchange
+    engine.build_ready()
+    if work is not None:
+        work.wait()
+    cnt = engine.join_packed(params, recv, sizes, maxn, P)
+    local = cnt.clone()
+    _all_reduce(dist, cnt)
+    total = int(cnt.item())
+    local = int(local.item())
     return DistResult(matches=total, local_matches=local, timers=engine.timers() if timers else [])
 
 

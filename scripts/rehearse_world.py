@@ -45,11 +45,14 @@ def main():
         torch.cuda.synchronize()
         maxn = max_shard(nR, W)
 
-        def step():
-            v = eng.partition(0, p)
-            if W > 1:
+        def step():   # the issue order of distributed_join
+            if W == 1:
+                eng.partition(1, p)
+                v = eng.partition(0, p)
+            else:
+                v = eng.partition(0, p)
                 eng.pack(v, maxn, v.num_partitions)
-            eng.partition(1, p)
+                eng.partition(1, p)
             eng.build_ready()
             cnt = eng._count()
             eng.ctx.join_partitioned_async(p, [v] + segs, cnt.data_ptr())
