@@ -648,9 +648,10 @@ int build_and_probe(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned*
     }
     if (nR >= (1ull << 32) - 1) return set_err(c, PHJ_ERR_RANGE, "build side above 2^32 tuples");
     const uint64_t nS = PS.view.n;
-    if (c->tune.fused && (nR + P - 1) / P * 2 <= static_cast<uint64_t>(kFusedTcap)) {
-        // fused per-partition join with LDS tables (partitions of <= kFusedTcap build tuples
-        // take one round; larger ones several): HashJoin.hpp:267-303
+    // fused when the average partition fits one LDS round with margin (larger
+    // ones take extra rounds, each re-probing the item's S keys)
+    if (c->tune.fused && (nR + P - 1) / P * 3 <= static_cast<uint64_t>(kFusedTcap) * 2) {
+        // fused per-partition join with LDS tables: HashJoin.hpp:267-303
         const size_t nslots = nS / kFusedChunk + P + 1;
         PHJ_TRY(ensure(c, c->fitems, nslots * sizeof(FusedItem)));
         PHJ_TRY(ensure(c, c->count, 16));

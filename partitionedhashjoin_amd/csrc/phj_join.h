@@ -623,7 +623,7 @@ __global__ __launch_bounds__(kBlock) void k_probe_wave(ProbeArgs a) {
 // ---------------------------------------------------------------------------
 constexpr uint32_t kFusedChunk = 4096;   // S keys per item (16 probe rounds of 64 x 4)
 constexpr int kFusedKPL = 4;             // S keys per lane per probe round
-constexpr int kFusedTcap = 512;          // build keys per LDS table round
+constexpr int kFusedTcap = 256;          // build keys per LDS table round
 
 struct FusedItem {
     uint32_t s_lo, s_cnt, p, pad;
@@ -672,8 +672,11 @@ __device__ __forceinline__ void fused_load_s(const int64_t* skeys, uint32_t lo, 
 // Latency schedule per wave: the next item's descriptor is fetched one item
 // ahead; an item's first S sub-chunk is loaded together with its R bounds and
 // R keys; sub-chunk k + 1 is loaded while k is probed.
+// 5 waves per SIMD at KPL = 4 (92 VGPRs, no spill): the S loads in flight
+// per CU, not the arithmetic, bound this kernel
 template <int HK, int KPL, int TCAP>
-__global__ __launch_bounds__(kBlock) void k_join_fused(FusedArgs a) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KPL <= 4 ? 5 : 3, 8))) void k_join_fused(
+    FusedArgs a) {
     constexpr int RPL = TCAP / 64;                 // build keys per lane per round
     constexpr int OCAP = TCAP / 2 + 1;             // bucket offsets (table_buckets(TCAP) + 1)
     constexpr uint32_t SUB = 64 * KPL;             // S keys per probe sub-chunk
