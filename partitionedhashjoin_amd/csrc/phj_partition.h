@@ -315,18 +315,30 @@ __global__ __launch_bounds__(256) void k_hist_col(PassArgs a) {
         v[r] = ci < c1 ? col[ci] : make_uint4(0, 0, 0, 0);
     }
     __builtin_amdgcn_wave_barrier();
+    // each lane walks its 16 consecutive digits and merges runs of equal digits
+    // before adding (one LDS add per run: a skewed tile of one hot key costs one
+    // add per lane per chunk, a uniform one about one per digit)
 #pragma unroll
     for (int r = 0; r < ROUNDS; r++) {
         const uint32_t e0 = (c0 + r * 64 + lane) * EPC;
         const uint32_t w[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
+        uint32_t prev = 0, cnt = 0;
 #pragma unroll
         for (int j = 0; j < EPC; j++) {
             const uint32_t e = e0 + j;
             const uint32_t d = sizeof(DT) == 1 ? (w[j >> 2] >> (8 * (j & 3))) & 0xffu
                                                : (w[j >> 1] >> (16 * (j & 1))) & 0xffffu;
-            const bool valid = e >= L.lo && e < L.hi;
-            count_digit(my, valid ? d : 0u, valid);
+            if (e >= L.lo && e < L.hi) {
+                if (cnt && d == prev) {
+                    cnt++;
+                } else {
+                    if (cnt) atomicAdd(&my[prev], cnt);
+                    prev = d;
+                    cnt = 1;
+                }
+            }
         }
+        if (cnt) atomicAdd(&my[prev], cnt);
     }
     __builtin_amdgcn_wave_barrier();
     uint32_t* out = a.hist + static_cast<size_t>(L.tb_s) * nb + L.tseg;
