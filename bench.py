@@ -61,8 +61,6 @@ def config_params(phj, name):
         "C2: RadixCluster 2-pass 8+8, Murmur3, 10M⋈200M, Zipf s=1.05"
 
 
-# rocprof kernel-name prefix (and input layout) of each timed launch; the
-# S-side launch is the largest grid of that name
 def pmc_traffic(args, verbose):
     """HBM bytes per launch of each join phase from rocprofv3 PMC counters
     (scripts/pmc.py: FETCH_SIZE and WRITE_SIZE in separate passes, child

@@ -53,6 +53,8 @@ struct Tuning {
     bool dcol = true;     // 2-pass: pass 1 writes the pass-2 digit column
     unsigned ev_flags = hipEventDisableSystemFence;  // timer / ordering events
     bool fused = true;    // radix join: fused per-partition LDS build + probe when partitions are small
+    int onepass_max = 256; // hash % P: largest P partitioned in one pass
+    int ptab = 1;         // partitioned bucket tables: 0 never, 1 very large partitions, 2 always
     int fused_kpl = 4;    // fused join: S keys per lane per probe round (4 or 8)
 };
 
@@ -296,7 +298,10 @@ int make_plan(phj_ctx* c, const phj_join_params* p, Plan& pl) {
     if (p->num_partitions > 0) {
         pl.mode = 1;
         pl.P = p->num_partitions;
-        if (pl.P <= static_cast<uint64_t>(kMaxBins)) {
+        // one pass while the scatter's runs stay long (a 4096-tuple tile over
+        // <= 256 digits); beyond, two passes with balanced digits: pass 1 on
+        // q >> b2, pass 2 on q & (2^b2 - 1), 2^b2 ~ sqrt(P)
+        if (pl.P <= static_cast<uint64_t>(std::min<int>(c->tune.onepass_max, kMaxBins))) {
             pl.npass = 1;
             pl.nb1 = static_cast<uint32_t>(pl.P);
             pl.bits1 = ceil_log2(pl.P);
@@ -305,14 +310,15 @@ int make_plan(phj_ctx* c, const phj_join_params* p, Plan& pl) {
         } else {
             if (pl.P > (1ull << (2 * kMaxDigitBits)))
                 return set_err(c, PHJ_ERR_RANGE, "num_partitions above 2^22");
+            const uint32_t b2 = std::min<uint32_t>(kMaxDigitBits, (ceil_log2(pl.P) + 1) / 2);
             pl.npass = 2;
-            pl.nb2 = kMaxBins;
-            pl.bits2 = kMaxDigitBits;
-            pl.nb1 = static_cast<uint32_t>((pl.P + kMaxBins - 1) / kMaxBins);
+            pl.nb2 = 1u << b2;
+            pl.bits2 = b2;
+            pl.nb1 = static_cast<uint32_t>((pl.P + pl.nb2 - 1) / pl.nb2);
             pl.bits1 = ceil_log2(pl.nb1);
-            pl.shift1 = kMaxDigitBits;
+            pl.shift1 = b2;
             pl.dmask1 = 0xffffffffu;
-            pl.dmask2 = kMaxBins - 1;
+            pl.dmask2 = pl.nb2 - 1;
         }
     } else {
         const uint32_t b0 = p->radix_bits[0], b1 = p->radix_bits[1];
@@ -698,6 +704,66 @@ int build_and_probe(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned*
         return PHJ_OK;
     }
     c->last_fused = false;
+    // very large partitions (the reference's -p 32 .. 128 at 10M build tuples):
+    // partitioned bucket tables, whose build is one pass of atomics over all
+    // tuples; the CSR build below gives each partition one workgroup (3.9 ms at
+    // -p 32 against 0.76), while its probe is faster from -p 1024 up
+    if (c->tune.ptab > 1 || (c->tune.ptab == 1 && (nR + P - 1) / P >= 65536)) {
+        // partitioned bucket tables in HBM (large partitions)
+        const uint32_t ratio_x256 = static_cast<uint32_t>(kNPDefaultRatio * 256);
+        const size_t nbk_bound = static_cast<size_t>(nR) * ratio_x256 / 256 / kNPSlots + 2 * static_cast<size_t>(P) + 1;
+        PHJ_TRY(ensure(c, c->np_tab, nbk_bound * sizeof(NPBucket)));
+        PHJ_TRY(ensure(c, c->np_pays, nbk_bound * kNPSlots * 8));
+        PHJ_TRY(ensure(c, c->prep, (static_cast<size_t>(P) + 1) * 4));
+        PHJ_TRY(ensure(c, c->count, 16));
+        PtabArgs ta{};
+        ta.L = L;
+        uint64_t off = 0;
+        for (int g = 0; g < nseg; g++) {
+            ta.segoff[g] = static_cast<uint32_t>(off);
+            off += segs[g].n;
+        }
+        ta.segoff[nseg] = static_cast<uint32_t>(off);
+        ta.tab = static_cast<NPBucket*>(c->np_tab.p);
+        ta.pays = static_cast<int64_t*>(c->np_pays.p);
+        ta.tob = static_cast<const uint32_t*>(c->prep.p);
+        ta.f = DigitFn{pl.seed, pl.P, pl.mode == 1 ? (~0ull) / pl.P : 0, pl.mode, 0, 0xffffffffu, 0};
+        ta.seed = pl.seed;
+        PHJ_TRY(mark(c, e_build0));
+        PHJ_TRY(timer_begin(c, "build", nR * 32 + nbk_bound * 64));
+        PHJ_HIP(c, hipMemsetAsync(c->np_tab.p, 0, nbk_bound * sizeof(NPBucket), c->ks));
+        hipLaunchKernelGGL(k_pt_prep, dim3((P + 1 + kBlock - 1) / kBlock), dim3(kBlock), 0, c->ks, L, ratio_x256,
+                           static_cast<uint32_t*>(c->prep.p));
+        PHJ_LAUNCHED(c, "k_pt_prep");
+        PHJ_TRY(scan_u32(c, static_cast<uint32_t*>(c->prep.p), P + 1, 1, P + 1));
+        if (nR) {
+            const dim3 bg(static_cast<uint32_t>((nR + kBlock - 1) / kBlock));
+            if (pl.hk == kMurmur3) hipLaunchKernelGGL((k_pt_build<kMurmur3>), bg, dim3(kBlock), 0, c->ks, ta);
+            else hipLaunchKernelGGL((k_pt_build<kXXH3>), bg, dim3(kBlock), 0, c->ks, ta);
+            PHJ_LAUNCHED(c, "k_pt_build");
+        }
+        PHJ_TRY(timer_end(c));
+        PHJ_TRY(mark(c, e_build1));
+        PHJ_HIP(c, hipMemsetAsync(c->count.p, 0, 8, c->ks));
+        PHJ_TRY(timer_begin(c, "probe", nS * 8 + nS * 64));
+        if (nS) {
+            constexpr int IT = 4;
+            const dim3 pg(static_cast<uint32_t>((nS + kBlock * IT - 1) / (kBlock * IT)));
+            auto* cnt = static_cast<unsigned long long*>(c->count.p);
+            const auto* tab = static_cast<const NPBucket*>(c->np_tab.p);
+            const auto* tob = static_cast<const uint32_t*>(c->prep.p);
+            if (pl.hk == kMurmur3)
+                hipLaunchKernelGGL((k_pt_probe<kMurmur3, IT>), pg, dim3(kBlock), 0, c->ks, PS.view.keys,
+                                   static_cast<uint32_t>(nS), tab, tob, ta.f, pl.seed, cnt);
+            else
+                hipLaunchKernelGGL((k_pt_probe<kXXH3, IT>), pg, dim3(kBlock), 0, c->ks, PS.view.keys,
+                                   static_cast<uint32_t>(nS), tab, tob, ta.f, pl.seed, cnt);
+            PHJ_LAUNCHED(c, "k_pt_probe");
+        }
+        PHJ_TRY(timer_end(c));
+        PHJ_TRY(mark(c, e_probe1));
+        return PHJ_OK;
+    }
     const size_t stride = static_cast<size_t>(P) + 1;
     PHJ_TRY(ensure(c, c->prep, stride * 3 * 4));
     PHJ_TRY(ensure(c, c->tkeys, nR * 8));
@@ -943,6 +1009,8 @@ int phj_ctx_create(int device, phj_ctx** out) {
     c->tune.nt_store = env_int("PHJ_NT", 0) != 0;
     c->tune.dcol = env_int("PHJ_DCOL", 1) != 0;
     c->tune.fused = env_int("PHJ_FUSED", 1) != 0;
+    c->tune.onepass_max = std::max(1, env_int("PHJ_ONEPASS_MAX", 256));
+    c->tune.ptab = env_int("PHJ_PTAB", 1);
     c->tune.fused_kpl = env_int("PHJ_FUSED_KPL", 4) == 8 ? 8 : 4;
     {
         const int ev = env_int("PHJ_EVENTS", 1);   // 0 default, 1 no system fence, 2 device release

@@ -920,6 +920,125 @@ __global__ __launch_bounds__(kBlock) void k_np_probe(const longlong2* S, uint64_
     }
 }
 
+// One bucketized-linear-probing lookup from home bucket b (NoPartitioning
+// semantics, LinearProbing.hpp:160-180: stop at the first non-full bucket).
+__device__ __forceinline__ bool np_lookup(const NPBucket* tab, uint32_t nb, uint32_t b, int64_t key) {
+    for (uint32_t step = 0; step < nb; step++) {
+        const longlong2* bp = reinterpret_cast<const longlong2*>(tab + b);
+        const longlong2 q0 = bp[0], q1 = bp[1], q2 = bp[2], q3 = bp[3];
+        const uint32_t fill = static_cast<uint32_t>(q3.y);
+        const uint32_t c = fill < kNPSlots ? fill : kNPSlots;
+        if ((c > 0 && q0.x == key) || (c > 1 && q0.y == key) || (c > 2 && q1.x == key) || (c > 3 && q1.y == key) ||
+            (c > 4 && q2.x == key) || (c > 5 && q2.y == key) || (c > 6 && q3.x == key))
+            return true;
+        if (fill < kNPSlots) return false;
+        b = (b + 1 == nb) ? 0 : b + 1;
+    }
+    return false;
+}
+
+// ---------------------------------------------------------------------------
+// Partitioned bucket tables in HBM, for partitions too large for the fused
+// LDS join (the reference's small-P configurations, e.g. -p 32: 312K build
+// tuples per partition). Partition p owns buckets [tob[p], tob[p+1]) of
+// 64-B NoPartitioning buckets (nb_p = ceil(m_p * ratio / 7)); a tuple's
+// partition is recomputed from its hash (q = the pass digits concatenated),
+// so neither build nor probe needs a work list. S is probed in its
+// partitioned order: consecutive lanes hit the same partition's region,
+// which stays in L2 while that partition is being probed.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t q_of_hash(uint64_t h, const DigitFn& f) {
+    if (f.mode == 0) return static_cast<uint32_t>(h & (f.P - 1));
+    const uint64_t qt = __umul64hi(h, f.magic);
+    uint64_t r = h - qt * f.P;
+    if (r >= f.P) r -= f.P;
+    return static_cast<uint32_t>(r);
+}
+
+// arr[p] = buckets of partition p (>= 1), arr[P] = 0; exclusive scan -> tob.
+__global__ __launch_bounds__(kBlock) void k_pt_prep(SegList L, uint32_t ratio_x256, uint32_t* arr) {
+    const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+    if (p > L.P) return;
+    if (p == L.P) {
+        arr[p] = 0;
+        return;
+    }
+    uint32_t m = 0;
+    for (uint32_t g = 0; g < L.nseg; g++) m += L.seg[g].bounds[p + 1] - L.seg[g].bounds[p];
+    const uint64_t slots = (static_cast<uint64_t>(m) * ratio_x256 + 255) / 256;
+    arr[p] = static_cast<uint32_t>(max<uint64_t>(1, (slots + kNPSlots - 1) / kNPSlots));
+}
+
+struct PtabArgs {
+    SegList L;
+    uint32_t segoff[kMaxSegs + 1];   // prefix of the segments' tuple counts
+    NPBucket* tab;
+    int64_t* pays;
+    const uint32_t* tob;
+    DigitFn f;                       // q of a hash: shift 0, all digit bits
+    uint64_t seed;
+};
+
+template <int HK>
+__global__ __launch_bounds__(kBlock) void k_pt_build(PtabArgs a) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= a.segoff[a.L.nseg]) return;
+    uint32_t g = 0;
+    while (i >= a.segoff[g + 1]) g++;
+    const uint32_t row = i - a.segoff[g];
+    const int64_t key = a.L.seg[g].keys[row];
+    const int64_t pay = a.L.seg[g].pays[row];
+    const uint64_t h = hash64<HK>(static_cast<uint64_t>(key), a.seed);
+    const uint32_t q = q_of_hash(h, a.f);
+    const uint32_t base = a.tob[q], nb = a.tob[q + 1] - base;
+    NPBucket* tab = a.tab + base;
+    uint32_t b = np_home(h, nb);
+    for (uint32_t step = 0; step < nb; step++) {
+        const uint32_t slot = atomicAdd(&tab[b].fill, 1u);
+        if (slot < kNPSlots) {
+            tab[b].key[slot] = key;
+            a.pays[(static_cast<size_t>(base) + b) * kNPSlots + slot] = pay;
+            return;
+        }
+        b = (b + 1 == nb) ? 0 : b + 1;
+    }
+}
+
+template <int HK, int ITEMS>
+__global__ __launch_bounds__(kBlock) void k_pt_probe(const int64_t* skeys, uint32_t nS, const NPBucket* tab,
+                                                     const uint32_t* tob, DigitFn f, uint64_t seed,
+                                                     unsigned long long* count) {
+    __shared__ uint32_t red[kWaves];
+    uint32_t hits = 0;
+    const uint32_t base0 = blockIdx.x * kBlock * ITEMS;
+    int64_t k[ITEMS];
+#pragma unroll
+    for (int j = 0; j < ITEMS; j++) {
+        const uint32_t idx = base0 + j * kBlock + threadIdx.x;
+        k[j] = idx < nS ? skeys[idx] : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < ITEMS; j++) {
+        const uint32_t idx = base0 + j * kBlock + threadIdx.x;
+        if (idx < nS) {
+            const uint64_t h = hash64<HK>(static_cast<uint64_t>(k[j]), seed);
+            const uint32_t q = q_of_hash(h, f);
+            const uint32_t b0 = tob[q], nb = tob[q + 1] - b0;
+            hits += np_lookup(tab + b0, nb, np_home(h, nb), k[j]) ? 1u : 0u;
+        }
+    }
+    uint32_t x = hits;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_down(x, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (int w = 0; w < kWaves; w++) t += red[w];
+        if (t) atomicAdd(count, t);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Generators and utilities.
 // ---------------------------------------------------------------------------

@@ -5,9 +5,10 @@ between kernel schedules that must produce the same bytes: tile size
 (PHJ_TILE) and workgroup size (PHJ_BLOCK) of the histogram/scatter kernels,
 nontemporal stores (PHJ_NT), pass-1 output layout (PHJ_P1_AOS), the pass-2
 digit column (PHJ_DCOL), tile order
-(PHJ_XCD_REMAP), write-combining scatter (PHJ_WC), fused LDS join vs HBM
-tables (PHJ_FUSED) and the probe schedule of the latter (PHJ_PROBE_WAVE,
-PHJ_PROBE_ITEMS). Each is
+(PHJ_XCD_REMAP), write-combining scatter (PHJ_WC), the one-pass limit of
+hash % P (PHJ_ONEPASS_MAX), fused LDS join vs HBM tables (PHJ_FUSED), the
+partitioned bucket tables vs CSR tables (PHJ_PTAB) and the CSR probe
+schedule (PHJ_PROBE_WAVE, PHJ_PROBE_ITEMS). Each is
 checked against the oracle's stable partition and semi-join count.
 """
 import numpy as np
@@ -34,10 +35,13 @@ SCHEDULES = [
     {"PHJ_XCD_REMAP": "0"},
     {"PHJ_NT": "1"},
     {"PHJ_WC": "1"},
-    {"PHJ_PROBE_ITEMS": "16", "PHJ_PROBE_WAVE": "0"},
-    {"PHJ_FUSED": "0", "PHJ_PROBE_WAVE": "0"},
-    {"PHJ_FUSED": "0", "PHJ_PROBE_WAVE": "2"},
+    {"PHJ_PROBE_ITEMS": "16", "PHJ_PROBE_WAVE": "0", "PHJ_FUSED": "0", "PHJ_PTAB": "0"},
+    {"PHJ_FUSED": "0", "PHJ_PTAB": "0", "PHJ_PROBE_WAVE": "0"},
+    {"PHJ_FUSED": "0", "PHJ_PTAB": "0", "PHJ_PROBE_WAVE": "2"},
+    {"PHJ_FUSED": "0", "PHJ_PTAB": "0"},
     {"PHJ_FUSED": "0"},
+    {"PHJ_FUSED": "0", "PHJ_PTAB": "2"},
+    {"PHJ_ONEPASS_MAX": "2048"},
     {"PHJ_FUSED_KPL": "8"},
 ]
 
