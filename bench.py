@@ -61,6 +61,28 @@ def config_params(phj, name):
         "C2: RadixCluster 2-pass 8+8, Murmur3, 10M⋈200M, Zipf s=1.05"
 
 
+def probe_phase(per_step, nR, nS):
+    """The north star's probe-phase roofline (target >= 60 % at 1 GPU).
+    SURVEY.md §8(d) defines its bytes as 16 B per R and S tuple (the tuples a
+    build+probe reads) over the fused build+probe kernel; this join reads only
+    the 8-B key columns (SoA partitions), so both figures are reported:
+    `frac_survey_def` (16 B/tuple, the definition) and `frac_bytes_read`
+    (8 B/key actually read). The time is the fused kernel's (build + probe
+    timers are one launch)."""
+    if "probe" not in per_step:
+        return None
+    ms = per_step["probe"][0] + per_step.get("build", (0.0, 0))[0]
+    if ms <= 0:
+        return None
+    sec = ms * 1e-3
+    b_def, b_read = 16 * (nR + nS), 8 * (nR + nS)
+    return {"kernel": "build+probe", "ms": ms, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "bytes_survey_def": b_def, "achieved_survey_def": b_def / sec / 1e9,
+            "frac_survey_def": b_def / sec / 1e9 / HBM_PEAK_GBS,
+            "bytes_read": b_read, "achieved_bytes_read": b_read / sec / 1e9,
+            "frac_bytes_read": b_read / sec / 1e9 / HBM_PEAK_GBS}
+
+
 def pmc_traffic(args, verbose):
     """HBM bytes per launch of each join phase from rocprofv3 PMC counters
     (scripts/pmc.py: FETCH_SIZE and WRITE_SIZE in separate passes, child
@@ -218,6 +240,7 @@ def main():
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic.get(dom_name), "algorithmic_bytes": dom_bytes,
                          "ms": dom_ms},
+            "probe_phase": probe_phase(per_step, nR, nS) if radix else None,
             "kernels_ms": {k: round(v[0], 4) for k, v in sorted(per_step.items())},
             "kernels_traffic_bytes": {k: int(v) for k, v in sorted(traffic.items())} or None,
         }

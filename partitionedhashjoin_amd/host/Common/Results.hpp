@@ -4,8 +4,9 @@
 // SetProbePhaseEnd measures from the build start, Results.hpp:202), and a JSON
 // formatter whose output has the layout Boost.PropertyTree's write_json gives
 // the reference (results/*/partitions_*.txt): 4-space indent, string values,
-// keys `id`, `parameters.*`, `results.{partition,build,probe}`. New keys are
-// only ever appended (results.matches, results.probe_only, results.device_*).
+// keys `id`, `parameters.*`, `results.{partition,build,probe}`. New values go
+// into an appended top-level `device` object (matches, device_total_us, ...),
+// never into `results`, whose values scripts/generate.sh pastes as rows.
 #pragma once
 
 #include <chrono>
@@ -144,14 +145,17 @@ class JSONResultsFormatter final : public IResultsFormatter {
 
     void Format(std::basic_ostream<char>& stream, const HashJoinTimingResult& r) override {
         std::vector<std::pair<std::string, std::string>> params(r.GetParameters().begin(), r.GetParameters().end());
-        std::vector<std::pair<std::string, std::string>> results = {
+        const std::vector<std::pair<std::string, std::string>> results = {
             {"partition", Cast(r.GetPartitioningPhaseDuration())},
             {"build", Cast(r.GetBuildPhaseDuration())},
             {"probe", Cast(r.GetProbePhaseDuration())}};
-        for (const auto& kv : r.GetExtraResults()) results.push_back(kv);
+        const auto& extra = r.GetExtraResults();
         stream << "{\n    \"id\": \"hashjointimingresult\",\n";
         WriteObject(stream, "parameters", params, true);
-        WriteObject(stream, "results", results, false);
+        // `results` holds exactly the reference's three phases: scripts/generate.sh
+        // pastes every `.results` value into figure.dat (generate.sh:25)
+        WriteObject(stream, "results", results, !extra.empty());
+        if (!extra.empty()) WriteObject(stream, "device", extra, false);
         stream << "}\n";
     }
 
