@@ -45,7 +45,7 @@ struct Tuning {
     int wc_items = 8;     // WC sub-tile = 256 * wc_items tuples (4 or 8)
     int wc_lw = 8;        // WC line: elements per column (8 = 64 B, 16 = 128 B)
     int wc_wgs = 1024;    // target workgroups per WC pass (super-tile size follows)
-    bool r_aux = false;   // partition R on the aux stream (no gain measured: DESIGN.md)
+    bool r_aux = true;    // phj_join: partition R on the aux stream beside S
     int probe_items = 8;  // block probe: S keys per lane per work item (8 or 16)
     int probe_wave = 1;   // wave-per-item probe: 0 never, 1 small partitions (auto), 2 always
     int block = 512;      // threads per workgroup of the tile kernels (256, 512 or 1024; tile_shape)
@@ -55,6 +55,7 @@ struct Tuning {
     bool fused = true;    // radix join: fused per-partition LDS build + probe when partitions are small
     int onepass_max = 256; // hash % P: largest P partitioned in one pass
     int ptab = 1;         // partitioned bucket tables: 0 never, 1 very large partitions, 2 always
+    bool subpart = true;  // phj_join: sub-partition large partitions for the fused join
     int fused_kpl = 4;    // fused join: S keys per lane per probe round (4 or 8)
 };
 
@@ -73,9 +74,10 @@ struct Plan {
     uint32_t bits1 = 0, bits2 = 0;
     uint32_t shift1 = 0, dmask1 = 0, dmask2 = 0;
     uint32_t Ppad = 1;    // nb1 * nb2 = final bounds length - 1
+    uint32_t sub_bits = 0, sub_shift = 0;   // phj_join: sub-partitions per partition (refine_plan)
     bool operator==(const Plan& o) const {
         return hk == o.hk && seed == o.seed && mode == o.mode && P == o.P && npass == o.npass &&
-               nb1 == o.nb1 && nb2 == o.nb2;
+               nb1 == o.nb1 && nb2 == o.nb2 && sub_bits == o.sub_bits && sub_shift == o.sub_shift;
     }
 };
 
@@ -343,12 +345,45 @@ int make_plan(phj_ctx* c, const phj_join_params* p, Plan& pl) {
     return PHJ_OK;
 }
 
+// phj_join only: when the requested partitions are too large for the fused LDS
+// join (the reference's -p 32 .. 8192 at 10M build tuples), split every
+// partition into 2^s sub-partitions of ~<= 170 build tuples (DigitFn sub_bits)
+// and partition on the refined q in two balanced passes. The count is the
+// same (a partition's hash table is simply organised by further hash bits);
+// phj_partition keeps the exact layout of the requested partitions.
+void refine_plan(const phj_ctx* c, Plan& pl, uint64_t nR) {
+    if (!c->tune.subpart || !c->tune.fused || pl.P == 0) return;
+    const double expect = static_cast<double>(nR) / static_cast<double>(pl.P);
+    if (expect * 3 <= static_cast<double>(kFusedTcap) * 2) return;
+    const uint32_t logP = ceil_log2(pl.P);
+    uint32_t s = 0;
+    while (expect / static_cast<double>(1ull << s) > 170.0 && logP + s < 2u * kMaxDigitBits) s++;
+    if (s == 0) return;
+    pl.sub_bits = s;
+    // radix: the hash bits just above the partition bits; hash % P: bits 40+
+    // (the LDS table buckets use bits 32..39)
+    pl.sub_shift = pl.mode == 0 ? logP : 40;
+    const uint64_t range = (pl.mode == 0 ? (1ull << logP) : pl.P) << s;
+    const uint32_t b2 = std::min<uint32_t>(kMaxDigitBits, (ceil_log2(range) + 1) / 2);
+    pl.npass = 2;
+    pl.nb2 = 1u << b2;
+    pl.bits2 = b2;
+    pl.dmask2 = pl.nb2 - 1;
+    pl.nb1 = static_cast<uint32_t>((range + pl.nb2 - 1) / pl.nb2);
+    pl.bits1 = ceil_log2(pl.nb1);
+    pl.shift1 = b2;
+    pl.dmask1 = 0xffffffffu;
+    pl.Ppad = pl.nb1 * pl.nb2;
+}
+
 DigitFn digit_fn(const Plan& pl, int pass) {
     DigitFn f{};
     f.seed = pl.seed;
     f.P = pl.P;
     f.mode = pl.mode;
     f.magic = pl.mode == 1 ? (~0ull) / pl.P : 0;
+    f.sub_bits = pl.sub_bits;
+    f.sub_shift = pl.sub_shift;
     if (pass == 1) {
         f.shift = pl.shift1;
         f.dmask = pl.dmask1;
@@ -727,7 +762,8 @@ int build_and_probe(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned*
         ta.tab = static_cast<NPBucket*>(c->np_tab.p);
         ta.pays = static_cast<int64_t*>(c->np_pays.p);
         ta.tob = static_cast<const uint32_t*>(c->prep.p);
-        ta.f = DigitFn{pl.seed, pl.P, pl.mode == 1 ? (~0ull) / pl.P : 0, pl.mode, 0, 0xffffffffu, 0};
+        ta.f = DigitFn{pl.seed, pl.P, pl.mode == 1 ? (~0ull) / pl.P : 0, pl.mode, 0, 0xffffffffu,
+                       pl.sub_bits, pl.sub_shift, 0};
         ta.seed = pl.seed;
         PHJ_TRY(mark(c, e_build0));
         PHJ_TRY(timer_begin(c, "build", nR * 32 + nbk_bound * 64));
@@ -1002,7 +1038,7 @@ int phj_ctx_create(int device, phj_ctx** out) {
     c->tune.p1_aos = env_int("PHJ_P1_AOS", 1) != 0;
     c->tune.xcd_remap = env_int("PHJ_XCD_REMAP", 1) != 0;
     c->tune.wc = env_int("PHJ_WC", 0) != 0;
-    c->tune.r_aux = env_int("PHJ_R_AUX", 0) != 0;
+    c->tune.r_aux = env_int("PHJ_R_AUX", 1) != 0;
     c->tune.probe_items = env_int("PHJ_PROBE_ITEMS", 8) == 16 ? 16 : 8;
     c->tune.probe_wave = env_int("PHJ_PROBE_WAVE", 1);
     c->tune.block = env_int("PHJ_BLOCK", 512);
@@ -1011,6 +1047,7 @@ int phj_ctx_create(int device, phj_ctx** out) {
     c->tune.fused = env_int("PHJ_FUSED", 1) != 0;
     c->tune.onepass_max = std::max(1, env_int("PHJ_ONEPASS_MAX", 256));
     c->tune.ptab = env_int("PHJ_PTAB", 1);
+    c->tune.subpart = env_int("PHJ_SUBPART", 1) != 0;
     c->tune.fused_kpl = env_int("PHJ_FUSED_KPL", 4) == 8 ? 8 : 4;
     {
         const int ev = env_int("PHJ_EVENTS", 1);   // 0 default, 1 no system fence, 2 device release
@@ -1254,16 +1291,19 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
     PHJ_TRY(make_plan(c, p, pl));
     SideState& R = c->side[PHJ_SIDE_BUILD];
     SideState& S = c->side[PHJ_SIDE_PROBE];
+    const uint32_t requested = pl.Ppad;   // reported; the join may sub-partition
+    refine_plan(c, pl, R.n);
     hipEvent_t t0, t1, tr, b0, b1, p1;
-    // Partition(R) || Partition(S) (HashJoin.hpp:210-216): R on the aux stream
+    // Partition(R) || Partition(S) (HashJoin.hpp:210-216): S (the long one) is
+    // issued first on the ctx stream, R beside it on the aux stream
     PHJ_TRY(mark(c, &t0));
     PHJ_HIP(c, hipStreamWaitEvent(c->aux, t0, 0));
+    PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, pl));
     c->ks = c->tune.r_aux ? c->aux : c->stream;
     int rc = partition_side(c, PHJ_SIDE_BUILD, pl);
     if (rc == PHJ_OK) rc = mark(c, &tr);
     c->ks = c->stream;
     PHJ_TRY(rc);
-    PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, pl));
     PHJ_HIP(c, hipStreamWaitEvent(c->stream, tr, 0));
     PHJ_TRY(mark(c, &t1));
     PHJ_TRY(build_and_probe(c, pl, 1, &R.view, &b0, &b1, &p1));
@@ -1279,7 +1319,7 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
         r->probe_ms = t * (1.0 - fb);
     }
     r->total_ms = elapsed(c, t0, p1);
-    r->num_partitions = pl.Ppad;
+    r->num_partitions = requested;
     r->algorithmic_bytes = partition_bytes(pl, R.n) + partition_bytes(pl, S.n) + R.n * 32 + S.n * 8 + R.n * 8;
     return fill_timers(c, r);
 }

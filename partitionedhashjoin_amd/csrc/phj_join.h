@@ -948,11 +948,7 @@ __device__ __forceinline__ bool np_lookup(const NPBucket* tab, uint32_t nb, uint
 // which stays in L2 while that partition is being probed.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t q_of_hash(uint64_t h, const DigitFn& f) {
-    if (f.mode == 0) return static_cast<uint32_t>(h & (f.P - 1));
-    const uint64_t qt = __umul64hi(h, f.magic);
-    uint64_t r = h - qt * f.P;
-    if (r >= f.P) r -= f.P;
-    return static_cast<uint32_t>(r);
+    return static_cast<uint32_t>(q_from_hash(h, f));
 }
 
 // arr[p] = buckets of partition p (>= 1), arr[P] = 0; exclusive scan -> tob.

@@ -33,6 +33,10 @@ constexpr int kMaxBins = 1 << kMaxDigitBits;
 
 // q(key) -> this pass's digit. mode 0: q = h & (P - 1); mode 1: q = h % P
 // (Barrett: magic = floor((2^64 - 1) / P), one correction step).
+// With sub_bits > 0 (phj_join on large partitions, phj_capi.hip refine_plan)
+// q is refined to (q << sub_bits) | sub_bits hash bits taken at sub_shift:
+// every partition q stays contiguous and is split into 2^sub_bits
+// sub-partitions; equal keys have equal hashes, so they still meet.
 struct DigitFn {
     uint64_t seed;
     uint64_t P;
@@ -40,17 +44,31 @@ struct DigitFn {
     uint32_t mode;
     uint32_t shift;
     uint32_t dmask;
+    uint32_t sub_bits;
+    uint32_t sub_shift;
     uint32_t pad;
 };
 
+__host__ __device__ __forceinline__ uint64_t q_from_hash(uint64_t h, const DigitFn& f) {
+    uint64_t q;
+    if (f.mode == 0) {
+        q = h & (f.P - 1);
+    } else {
+#if defined(__HIP_DEVICE_COMPILE__)
+        const uint64_t qt = __umul64hi(h, f.magic);
+#else
+        const uint64_t qt = static_cast<uint64_t>((static_cast<unsigned __int128>(h) * f.magic) >> 64);
+#endif
+        q = h - qt * f.P;
+        if (q >= f.P) q -= f.P;
+    }
+    if (f.sub_bits) q = (q << f.sub_bits) | ((h >> f.sub_shift) & ((1ull << f.sub_bits) - 1));
+    return q;
+}
+
 template <int HK>
 __device__ __forceinline__ uint64_t partition_q(uint64_t key, const DigitFn& f) {
-    const uint64_t h = hash64<HK>(key, f.seed);
-    if (f.mode == 0) return h & (f.P - 1);
-    const uint64_t qt = __umul64hi(h, f.magic);
-    uint64_t r = h - qt * f.P;
-    if (r >= f.P) r -= f.P;
-    return r;
+    return q_from_hash(hash64<HK>(key, f.seed), f);
 }
 
 template <int HK>

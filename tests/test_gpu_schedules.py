@@ -6,7 +6,8 @@ between kernel schedules that must produce the same bytes: tile size
 nontemporal stores (PHJ_NT), pass-1 output layout (PHJ_P1_AOS), the pass-2
 digit column (PHJ_DCOL), tile order
 (PHJ_XCD_REMAP), write-combining scatter (PHJ_WC), the one-pass limit of
-hash % P (PHJ_ONEPASS_MAX), fused LDS join vs HBM tables (PHJ_FUSED), the
+hash % P (PHJ_ONEPASS_MAX), the join's sub-partitioning of large partitions
+(PHJ_SUBPART), fused LDS join vs HBM tables (PHJ_FUSED), the
 partitioned bucket tables vs CSR tables (PHJ_PTAB) and the CSR probe
 schedule (PHJ_PROBE_WAVE, PHJ_PROBE_ITEMS). Each is
 checked against the oracle's stable partition and semi-join count.
@@ -42,6 +43,8 @@ SCHEDULES = [
     {"PHJ_FUSED": "0"},
     {"PHJ_FUSED": "0", "PHJ_PTAB": "2"},
     {"PHJ_ONEPASS_MAX": "2048"},
+    {"PHJ_SUBPART": "0"},
+    {"PHJ_R_AUX": "0"},
     {"PHJ_FUSED_KPL": "8"},
 ]
 
@@ -90,5 +93,8 @@ def test_join_counts(tuned_ctx):
     tuned_ctx.upload(phj.SIDE_PROBE, S)
     for p in (phj.radix_params((8, 8), hash=phj.HASH_MURMUR3, seed=SEED),
               phj.radix_params(num_partitions=1024, hash=phj.HASH_XXH3, seed=SEED),
+              phj.radix_params(num_partitions=32, hash=phj.HASH_XXH3, seed=SEED),
+              phj.radix_params(num_partitions=1, hash=phj.HASH_MURMUR3, seed=SEED),
+              phj.radix_params(num_partitions=777, hash=phj.HASH_XXH3, seed=SEED),
               phj.radix_params((6, 0), hash=phj.HASH_XXH3, seed=SEED)):
         assert tuned_ctx.join(p).matches == expect
