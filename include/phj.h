@@ -142,6 +142,12 @@ int phj_relation_count_in_range(phj_ctx *ctx, int side, int64_t lo, int64_t hi, 
 /* Synchronous: partition (radix) / build / probe on the device, count back on the host. */
 int phj_join(phj_ctx *ctx, const phj_join_params *p, phj_join_result *r);
 
+/* Allocate (grow-only) every workspace buffer phj_join with these params needs
+ * for the relations currently bound, launching nothing: the reference keeps
+ * its allocations outside the timed phases (RadixCluster/HashJoin.hpp:195-198),
+ * and a first phj_join after phj_prepare allocates nothing. Optional. */
+int phj_prepare(phj_ctx *ctx, const phj_join_params *p);
+
 /* ---- building blocks (multi-GPU: range-sharded relations, RCCL exchange) ---- */
 /* Radix-partition the bound relation of `side`; fills `out` with ctx-owned views.
  * Asynchronous on the ctx stream (order later work on the same stream). */

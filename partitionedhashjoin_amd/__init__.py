@@ -125,6 +125,10 @@ class Context:
         return c.value
 
     # -- join --
+    def prepare(self, params: JoinParams) -> None:
+        """Allocate join's workspace for the bound relations (nothing runs)."""
+        self._check(self._L.phj_prepare(self._h, C.byref(params)))
+
     def join(self, params: JoinParams) -> JoinResult:
         r = JoinResult()
         self._check(self._L.phj_join(self._h, C.byref(params), C.byref(r)))

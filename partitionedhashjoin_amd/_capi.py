@@ -36,6 +36,7 @@ EXPORTED = [
     "phj_relation_generate_sequential", "phj_relation_generate_zipf",
     "phj_relation_count_in_range", "phj_join", "phj_partition", "phj_join_partitioned",
     "phj_partitioned_download", "phj_hash_keys", "phj_timers_report", "phj_join_partitioned_async",
+    "phj_prepare",
 ]
 
 
@@ -116,6 +117,7 @@ def load():
         "phj_hash_keys": (i, [P, i, u64, P, u64, P]),
         "phj_timers_report": (i, [P, C.POINTER(JoinResult)]),
         "phj_join_partitioned_async": (i, [P, C.POINTER(JoinParams), i, C.POINTER(Partitioned), P]),
+        "phj_prepare": (i, [P, C.POINTER(JoinParams)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

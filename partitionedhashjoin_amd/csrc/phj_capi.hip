@@ -133,6 +133,7 @@ struct phj_ctx {
     std::string err;
     Tuning tune;
     bool last_fused = false;   // the last build_and_probe ran the fused kernel
+    bool dry = false;          // phj_prepare: size and allocate the workspace, launch nothing
 };
 
 namespace {
@@ -404,6 +405,7 @@ int scan_u32(phj_ctx* c, uint32_t* data, uint32_t len, uint32_t narrays, uint32_
     s.nblk = (len + kScanBlockElems - 1) / kScanBlockElems;
     DevBuf& part = scratch ? *scratch : c->scan_partials;
     PHJ_TRY(ensure(c, part, static_cast<size_t>(s.nblk) * narrays * 4));
+    if (c->dry) return PHJ_OK;
     s.partials = static_cast<uint32_t*>(part.p);
     hipLaunchKernelGGL(k_scan_reduce, dim3(s.nblk, narrays), dim3(kBlock), 0, c->ks, s);
     PHJ_LAUNCHED(c, "k_scan_reduce");
@@ -590,6 +592,11 @@ int partition_side(phj_ctx* c, int s, const Plan& pl) {
         PHJ_TRY(ensure(c, S.bounds, (static_cast<size_t>(pl.Ppad) + 1) * 4));
         if (dcol) PHJ_TRY(ensure(c, S.dig, static_cast<size_t>(n) * dbytes + 64));
     }
+    if (c->dry) {   // scan scratch of both passes, then nothing is launched
+        PHJ_TRY(scan_u32(c, nullptr, nt1 * pl.nb1, 1, nt1 * pl.nb1, c->scan_scratch));
+        if (pl.npass == 2 && n) PHJ_TRY(scan_u32(c, nullptr, nt2 * pl.nb2, 1, nt2 * pl.nb2, c->scan_scratch));
+        return PHJ_OK;
+    }
     // pass 1: AoS relation -> SoA columns A
     PassArgs a{};
     a.in_keys = reinterpret_cast<const int64_t*>(S.rel);
@@ -671,7 +678,7 @@ int partition_side(phj_ctx* c, int s, const Plan& pl) {
 int build_and_probe(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned* segs,
                     hipEvent_t* e_build0, hipEvent_t* e_build1, hipEvent_t* e_probe1) {
     SideState& PS = c->side[PHJ_SIDE_PROBE];
-    if (!PS.partitioned || !(PS.plan == pl))
+    if (!c->dry && (!PS.partitioned || !(PS.plan == pl)))
         return set_err(c, PHJ_ERR_STATE, "probe relation not partitioned with these params");
     if (nseg < 1 || nseg > kMaxSegs) return set_err(c, PHJ_ERR_INVALID, "nbuild must be in [1,16]");
     const uint32_t P = pl.Ppad;
@@ -688,7 +695,7 @@ int build_and_probe(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned*
         nR += segs[g].n;
     }
     if (nR >= (1ull << 32) - 1) return set_err(c, PHJ_ERR_RANGE, "build side above 2^32 tuples");
-    const uint64_t nS = PS.view.n;
+    const uint64_t nS = c->dry ? PS.n : PS.view.n;
     // fused when the average partition fits one LDS round with margin (larger
     // ones take extra rounds, each re-probing the item's S keys)
     if (c->tune.fused && (nR + P - 1) / P * 3 <= static_cast<uint64_t>(kFusedTcap) * 2) {
@@ -700,6 +707,7 @@ int build_and_probe(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned*
             PHJ_TRY(ensure(c, c->split, 16));
             PHJ_HIP(c, hipMemsetAsync(c->split.p, 0, 16, c->ks));
         }
+        if (c->dry) return PHJ_OK;
         PHJ_HIP(c, hipMemsetAsync(c->count.p, 0, 8, c->ks));
         PHJ_TRY(mark(c, e_build0));
         // algorithmic bytes: R keys once (build), S keys once (probe)
@@ -765,6 +773,7 @@ int build_and_probe(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned*
         ta.f = DigitFn{pl.seed, pl.P, pl.mode == 1 ? (~0ull) / pl.P : 0, pl.mode, 0, 0xffffffffu,
                        pl.sub_bits, pl.sub_shift, 0};
         ta.seed = pl.seed;
+        if (c->dry) return scan_u32(c, nullptr, P + 1, 1, P + 1);
         PHJ_TRY(mark(c, e_build0));
         PHJ_TRY(timer_begin(c, "build", nR * 32 + nbk_bound * 64));
         PHJ_HIP(c, hipMemsetAsync(c->np_tab.p, 0, nbk_bound * sizeof(NPBucket), c->ks));
@@ -827,6 +836,7 @@ int build_and_probe(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned*
     const uint32_t kcap = expect * 2 > 8192 ? 256u : std::max<uint32_t>(256, next_pow2_u32(static_cast<uint32_t>(expect * 2)));
     const uint32_t ocap_build = 16384;
     const uint32_t ocap_wave = std::min<uint32_t>(2048, std::max<uint32_t>(64, kcap));
+    if (c->dry) return scan_u32(c, nullptr, P + 1, 3, static_cast<uint32_t>(stride));
 
     PHJ_TRY(mark(c, e_build0));
     PHJ_TRY(timer_begin(c, "build", nR * 32));
@@ -937,6 +947,7 @@ int join_nopart(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
     PHJ_TRY(ensure(c, c->np_tab, static_cast<size_t>(nb) * sizeof(NPBucket)));
     PHJ_TRY(ensure(c, c->np_pays, static_cast<size_t>(nb) * kNPSlots * 8));
     PHJ_TRY(ensure(c, c->count, 8));
+    if (c->dry) return PHJ_OK;
     hipEvent_t e0, e1, e2;
     const uint32_t nR = static_cast<uint32_t>(R.n);
     PHJ_TRY(mark(c, &e0));
@@ -1322,6 +1333,35 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
     r->num_partitions = requested;
     r->algorithmic_bytes = partition_bytes(pl, R.n) + partition_bytes(pl, S.n) + R.n * 32 + S.n * 8 + R.n * 8;
     return fill_timers(c, r);
+}
+
+int phj_prepare(phj_ctx* c, const phj_join_params* p) {
+    if (!c) return PHJ_ERR_INVALID;
+    if (!p) return set_err(c, PHJ_ERR_INVALID, "null params");
+    (void)hipGetLastError();
+    PHJ_HIP(c, hipSetDevice(c->device));
+    struct DryScope {
+        phj_ctx* c;
+        ~DryScope() { c->dry = false; }
+    } scope{c};
+    c->dry = true;
+    if (p->algo == PHJ_ALGO_NO_PARTITIONING) {
+        phj_join_result r{};
+        return join_nopart(c, p, &r);
+    }
+    if (p->algo != PHJ_ALGO_RADIX) return set_err(c, PHJ_ERR_INVALID, "Unrecognized join algorithm");
+    Plan pl;
+    PHJ_TRY(make_plan(c, p, pl));
+    refine_plan(c, pl, c->side[PHJ_SIDE_BUILD].n);
+    PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, pl));
+    PHJ_TRY(partition_side(c, PHJ_SIDE_BUILD, pl));
+    phj_partitioned seg{};
+    seg.n = c->side[PHJ_SIDE_BUILD].n;
+    seg.num_partitions = pl.Ppad;
+    hipEvent_t b0, b1, p1;
+    PHJ_TRY(build_and_probe(c, pl, 1, &seg, &b0, &b1, &p1));
+    PHJ_HIP(c, hipStreamSynchronize(c->stream));
+    return PHJ_OK;
 }
 
 int phj_timers_report(phj_ctx* c, phj_join_result* r) {

@@ -276,3 +276,17 @@ def test_large_generated_workload_property(ctx):
     for p in (phj.radix_params((8, 8)), phj.radix_params((11, 0), hash=phj.HASH_XXH3),
               phj.nopart_params()):
         assert ctx.join(p).matches == inrange
+
+
+@pytest.mark.parametrize("params", [phj.radix_params((8, 8), hash=phj.HASH_MURMUR3, seed=SEED),
+                                    phj.radix_params(num_partitions=32, hash=phj.HASH_XXH3, seed=SEED),
+                                    phj.nopart_params(hash=phj.HASH_XXH3, seed=SEED)])
+def test_prepare_then_join(params):
+    # phj_prepare allocates the workspace for the bound relations; the join that
+    # follows is unchanged (fresh context: nothing was allocated before)
+    R, S = O.generate_tables(50_000, 600_001, 1.05, 31, threads=4)
+    with phj.Context(0) as c:
+        c.upload(phj.SIDE_BUILD, R)
+        c.upload(phj.SIDE_PROBE, S)
+        c.prepare(params)
+        assert c.join(params).matches == O.semijoin_count(R, S)
