@@ -56,6 +56,7 @@ struct Tuning {
     int onepass_max = 256; // hash % P: largest P partitioned in one pass
     int ptab = 1;         // partitioned bucket tables: 0 never, 1 very large partitions, 2 always
     bool subpart = true;  // phj_join: sub-partition large partitions for the fused join
+    bool timers = true;   // per-kernel timer events (phase events are always recorded)
     int fused_kpl = 4;    // fused join: S keys per lane per probe round (4 or 8)
 };
 
@@ -134,6 +135,9 @@ struct phj_ctx {
     Tuning tune;
     bool last_fused = false;   // the last build_and_probe ran the fused kernel
     bool dry = false;          // phj_prepare: size and allocate the workspace, launch nothing
+    hipEvent_t last_ev = nullptr;      // the last event recorded (mark) ...
+    hipStream_t last_ev_stream = nullptr;  // ... on this stream ...
+    uint32_t since_ev = 0;             // ... and the kernels launched since
 };
 
 namespace {
@@ -153,6 +157,7 @@ int set_err(phj_ctx* c, int code, const std::string& msg) {
 
 #define PHJ_LAUNCHED(ctx, what)                                                              \
     do {                                                                                     \
+        (ctx)->since_ev++;                                                                   \
         hipError_t e_ = hipGetLastError();                                                   \
         if (e_ != hipSuccess)                                                                \
             return set_err(ctx, PHJ_ERR_HIP, std::string("launch ") + what + ": " +         \
@@ -213,20 +218,28 @@ int mark(phj_ctx* c, hipEvent_t* out) {
     *out = next_event(c);
     if (!*out) return set_err(c, PHJ_ERR_HIP, "hipEventCreate failed");
     PHJ_HIP(c, hipEventRecord(*out, c->ks));
+    c->last_ev = *out;
+    c->last_ev_stream = c->ks;
+    c->since_ev = 0;
     return PHJ_OK;
 }
 
 int timer_begin(phj_ctx* c, const char* name, uint64_t bytes) {
+    if (!c->tune.timers) return PHJ_OK;
     TimerRec t{name, bytes, nullptr, nullptr};
-    PHJ_TRY(mark(c, &t.a));
+    // back-to-back timers on one stream share the boundary event (the previous
+    // timer's end is this one's start when nothing was launched in between)
+    if (c->last_ev && c->last_ev_stream == c->ks && c->since_ev == 0) t.a = c->last_ev;
+    else PHJ_TRY(mark(c, &t.a));
     c->timers.push_back(t);
     return PHJ_OK;
 }
 
-int timer_end(phj_ctx* c) { return mark(c, &c->timers.back().b); }
+int timer_end(phj_ctx* c) { return c->tune.timers ? mark(c, &c->timers.back().b) : PHJ_OK; }
 
 // One launch reported as two timers (build, probe) split by the kernel's own clocks.
 int timer_begin_split(phj_ctx* c, uint64_t build_bytes, uint64_t probe_bytes) {
+    if (!c->tune.timers) return PHJ_OK;
     PHJ_TRY(timer_begin(c, "build", build_bytes));
     c->timers.back().split = 1;
     c->timers.push_back(TimerRec{"probe", probe_bytes, c->timers.back().a, nullptr, 2});
@@ -234,6 +247,7 @@ int timer_begin_split(phj_ctx* c, uint64_t build_bytes, uint64_t probe_bytes) {
 }
 
 int timer_end_split(phj_ctx* c) {
+    if (!c->tune.timers) return PHJ_OK;
     PHJ_TRY(mark(c, &c->timers.back().b));
     c->timers[c->timers.size() - 2].b = c->timers.back().b;
     return PHJ_OK;
@@ -244,6 +258,7 @@ constexpr size_t kMaxTimerRecs = 1u << 14;
 void reset_timers(phj_ctx* c) {
     c->timers.clear();
     c->evnext = 0;
+    c->last_ev = nullptr;
     if (c->split.p) (void)hipMemsetAsync(c->split.p, 0, 16, c->ks);
 }
 
@@ -741,8 +756,8 @@ int build_and_probe(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned*
         PHJ_HIP(c, hipLaunchKernel(kfn, dim3(grid), dim3(kBlock), kargs, 0, c->ks));
         PHJ_LAUNCHED(c, "k_join_fused");
         PHJ_TRY(timer_end_split(c));
-        *e_build1 = c->timers.back().b;
-        *e_probe1 = c->timers.back().b;
+        PHJ_TRY(mark(c, e_probe1));
+        *e_build1 = *e_probe1;
         c->last_fused = true;
         return PHJ_OK;
     }
@@ -1059,6 +1074,7 @@ int phj_ctx_create(int device, phj_ctx** out) {
     c->tune.onepass_max = std::max(1, env_int("PHJ_ONEPASS_MAX", 256));
     c->tune.ptab = env_int("PHJ_PTAB", 1);
     c->tune.subpart = env_int("PHJ_SUBPART", 1) != 0;
+    c->tune.timers = env_int("PHJ_TIMERS", 1) != 0;
     c->tune.fused_kpl = env_int("PHJ_FUSED_KPL", 4) == 8 ? 8 : 4;
     {
         const int ev = env_int("PHJ_EVENTS", 1);   // 0 default, 1 no system fence, 2 device release

@@ -73,6 +73,15 @@ class HipShardEngine:
         self.ctx_r = Context(device)
         self.stream_r = torch.cuda.Stream(self.device)
         self.ctx_r.set_stream(self.stream_r.cuda_stream)
+        # a second host thread issues the S partition while the main thread issues
+        # R, the pack and the all-gather (ctypes releases the GIL; the two contexts
+        # and streams are independent)
+        from concurrent.futures import ThreadPoolExecutor
+        self.issuer = ThreadPoolExecutor(max_workers=1, thread_name_prefix="phj-s-issue")
+
+    def partition_async(self, side, params):
+        """Issue a partition from the issuer thread; returns a future of the view."""
+        return self.issuer.submit(self.partition, side, params)
 
     def tensor(self, n, dtype):
         return self.torch.empty(int(n), dtype=dtype, device=self.device)
@@ -208,6 +217,7 @@ def distributed_join(engine, params, nR: int, nS: int, rank: int, world: int, di
         cnt = engine.join_local(params, view)
         total = local = int(cnt.item())
         return DistResult(matches=total, local_matches=local, timers=engine.timers() if timers else [])
+    s_done = engine.partition_async(1, params) if hasattr(engine, "partition_async") else None
     view = engine.partition(0, params)      # R stream
     P = view.num_partitions
     sizes = [hi - lo for lo, hi in (shard_range(nR, r, world) for r in range(world))]
@@ -221,7 +231,10 @@ def distributed_join(engine, params, nR: int, nS: int, rank: int, world: int, di
         work = _all_gather(dist, recv, send)
     if side is not None:
         recv.record_stream(engine.stream)
-    engine.partition(1, params)             # main stream, beside the exchange
+    if s_done is not None:
+        s_done.result()                     # S was issued by the issuer thread meanwhile
+    else:
+        engine.partition(1, params)         # main stream, beside the exchange
     engine.build_ready()
     if work is not None:
         work.wait()

@@ -50,9 +50,10 @@ def main():
                 eng.partition(1, p)
                 v = eng.partition(0, p)
             else:
+                fut = eng.partition_async(1, p)
                 v = eng.partition(0, p)
                 eng.pack(v, maxn, v.num_partitions)
-                eng.partition(1, p)
+                fut.result()
             eng.build_ready()
             cnt = eng._count()
             eng.ctx.join_partitioned_async(p, [v] + segs, cnt.data_ptr())

@@ -45,6 +45,7 @@ SCHEDULES = [
     {"PHJ_ONEPASS_MAX": "2048"},
     {"PHJ_SUBPART": "0"},
     {"PHJ_R_AUX": "0"},
+    {"PHJ_TIMERS": "0"},
     {"PHJ_FUSED_KPL": "8"},
 ]
 
