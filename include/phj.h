@@ -154,6 +154,9 @@ int phj_prepare(phj_ctx *ctx, const phj_join_params *p);
 int phj_partition(phj_ctx *ctx, int side, const phj_join_params *p, phj_partitioned *out);
 /* Build bucket-chained tables over the union of `nbuild` partitioned build
  * segments (e.g. every rank's shard after an all-gather) and probe the ctx's
+ * partitioned probe relation. Build segments may omit payloads (NULL in every
+ * segment): the join only tests key equality, as the reference's Join() only
+ * tests Get() for null (RadixCluster/HashJoin.hpp:295-301). Probe the ctx's
  * partitioned probe relation (phj_partition(PHJ_SIDE_PROBE) with the same
  * params must precede). Synchronous; fills r (build_ms, probe_ms, matches). */
 int phj_join_partitioned(phj_ctx *ctx, const phj_join_params *p, int nbuild,

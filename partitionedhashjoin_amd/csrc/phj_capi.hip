@@ -706,6 +706,8 @@ int build_and_probe(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned*
             return set_err(c, PHJ_ERR_INVALID, "build segment partition count mismatch");
         L.seg[g].keys = segs[g].keys;
         L.seg[g].pays = segs[g].payloads;
+        if ((segs[g].payloads == nullptr) != (segs[0].payloads == nullptr))
+            return set_err(c, PHJ_ERR_INVALID, "build segments must all carry payloads or none");
         L.seg[g].bounds = segs[g].bounds;
         nR += segs[g].n;
     }

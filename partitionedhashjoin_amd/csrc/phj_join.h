@@ -162,6 +162,9 @@ __global__ __launch_bounds__(kBlock) void k_build_small(BuildArgs a) {
     // lane g < nseg holds segment g's columns
     const int64_t* skeys = lane < nseg ? a.L.seg[lane].keys : nullptr;
     const int64_t* spays = lane < nseg ? a.L.seg[lane].pays : nullptr;
+    // key-only build segments (the multi-GPU exchange ships keys): no payloads
+    // to copy; every probe only tests key equality
+    const bool spays_all = a.L.seg[0].pays != nullptr;
     const uint32_t* sbnd = lane < nseg ? a.L.seg[lane].bounds : nullptr;
     for (uint32_t p = blockIdx.x * kWaves + wave; p < P; p += nw) {
         // table bases and the segments' bounds in one round of loads
@@ -203,7 +206,7 @@ __global__ __launch_bounds__(kBlock) void k_build_small(BuildArgs a) {
             if (f < m) {
                 const int64_t row = static_cast<int64_t>(f) + ro;
                 key[j] = kp[row];
-                pay[j] = pp[row];
+                if (pp) pay[j] = pp[row];
             }
         }
         for (uint32_t i = lane; i < nbk; i += 64) cnt[i] = 0;
@@ -237,7 +240,7 @@ __global__ __launch_bounds__(kBlock) void k_build_small(BuildArgs a) {
             if (j * 64 + lane < m) {
                 const uint32_t pos = atomicAdd(&cnt[bkt[j]], 1u);
                 a.tkeys[kb + pos] = key[j];
-                a.tpays[kb + pos] = pay[j];
+                if (spays_all) a.tpays[kb + pos] = pay[j];
             }
         }
         wave_lds_sync();
@@ -323,13 +326,13 @@ __global__ __launch_bounds__(kBlock) void k_build_big(BuildArgs a) {
             const uint32_t lo = S.bounds[p], c = S.bounds[p + 1] - lo;
             for (uint32_t i = threadIdx.x; i < c; i += kBlock) {
                 const int64_t key = S.keys[lo + i];
-                const int64_t pay = S.pays[lo + i];
+                const int64_t pay = S.pays ? S.pays[lo + i] : 0;
                 const uint32_t b = bucket_of(hash64<HK>(static_cast<uint64_t>(key), a.seed), nbk);
                 uint32_t pos;
                 if (in_lds) pos = atomicAdd(&cnt[b], 1u);
                 else pos = __hip_atomic_fetch_add(&cnt[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 a.tkeys[kb + pos] = key;
-                a.tpays[kb + pos] = pay;
+                if (S.pays) a.tpays[kb + pos] = pay;
             }
         }
         __syncthreads();
@@ -983,7 +986,8 @@ __global__ __launch_bounds__(kBlock) void k_pt_build(PtabArgs a) {
     while (i >= a.segoff[g + 1]) g++;
     const uint32_t row = i - a.segoff[g];
     const int64_t key = a.L.seg[g].keys[row];
-    const int64_t pay = a.L.seg[g].pays[row];
+    const int64_t* sp = a.L.seg[g].pays;
+    const int64_t pay = sp ? sp[row] : 0;
     const uint64_t h = hash64<HK>(static_cast<uint64_t>(key), a.seed);
     const uint32_t q = q_of_hash(h, a.f);
     const uint32_t base = a.tob[q], nb = a.tob[q + 1] - base;
@@ -993,7 +997,7 @@ __global__ __launch_bounds__(kBlock) void k_pt_build(PtabArgs a) {
         const uint32_t slot = atomicAdd(&tab[b].fill, 1u);
         if (slot < kNPSlots) {
             tab[b].key[slot] = key;
-            a.pays[(static_cast<size_t>(base) + b) * kNPSlots + slot] = pay;
+            if (sp) a.pays[(static_cast<size_t>(base) + b) * kNPSlots + slot] = pay;
             return;
         }
         b = (b + 1 == nb) ? 0 : b + 1;

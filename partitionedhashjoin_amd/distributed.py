@@ -43,11 +43,14 @@ class DistResult:
 
 
 def pack_layout(maxn: int, P: int):
-    """int64 elements of one rank's packed build shard: keys[maxn] | payloads[maxn]
-    | bounds[P+1] (uint32, two per element). maxn is padded to 64 elements so
-    every column stays 16-B aligned inside the gathered buffer."""
+    """int64 elements of one rank's packed build shard: keys[maxn] | bounds[P+1]
+    (uint32, two per element). Only the keys travel: the join tests key
+    equality and never reads a build payload (the reference's Join() only
+    checks Get() for null, RadixCluster/HashJoin.hpp:295-301), which halves the
+    all-gather. maxn is padded to 64 elements so every column stays 16-B
+    aligned inside the gathered buffer."""
     maxn = (maxn + 63) // 64 * 64
-    return maxn, 2 * maxn + (P + 2) // 2
+    return maxn, maxn + (P + 2) // 2
 
 
 class HipShardEngine:
@@ -123,8 +126,7 @@ class HipShardEngine:
         base = send.data_ptr()
         L = self.ctx_r._L
         self.ctx_r._check(L.phj_partitioned_download(self.ctx_r._h, C.byref(view), C.c_void_p(base),
-                                                     C.c_void_p(base + maxn * 8),
-                                                     C.c_void_p(base + 2 * maxn * 8)))
+                                                     C.c_void_p(0), C.c_void_p(base + maxn * 8)))
         return send
 
     def _count(self):
@@ -141,8 +143,8 @@ class HipShardEngine:
         for g, n in enumerate(sizes):
             v = Partitioned()
             v.keys = base + (g * E) * 8
-            v.payloads = base + (g * E + maxn) * 8
-            v.bounds = base + (g * E + 2 * maxn) * 8
+            v.payloads = None          # key-only build segments
+            v.bounds = base + (g * E + maxn) * 8
             v.n = n
             v.num_partitions = P
             segs.append(v)
@@ -247,12 +249,12 @@ def distributed_join(engine, params, nR: int, nS: int, rank: int, world: int, di
 
 
 def unpack_segments_numpy(recv, sizes, maxn, P):
-    """Split a gathered packed buffer back into per-rank (keys, payloads, bounds)."""
+    """Split a gathered packed buffer back into per-rank (keys, bounds)."""
     maxn, E = pack_layout(maxn, P)
     recv = np.asarray(recv)
     segs = []
     for g, n in enumerate(sizes):
         blk = recv[g * E:(g + 1) * E]
-        bounds = blk[2 * maxn:].view(np.uint32)[:P + 1].astype(np.int64)
-        segs.append((blk[:n], blk[maxn:maxn + n], bounds))
+        bounds = blk[maxn:].view(np.uint32)[:P + 1].astype(np.int64)
+        segs.append((blk[:n], bounds))
     return segs

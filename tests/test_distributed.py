@@ -53,25 +53,24 @@ class OracleShardEngine:
         maxn, E = pack_layout(maxn, P)
         buf = np.zeros(E, dtype=np.int64)
         buf[:v.n] = v.keys
-        buf[maxn:maxn + v.n] = v.pays
-        buf[2 * maxn:].view(np.uint32)[:P + 1] = v.bounds.astype(np.uint32)
+        buf[maxn:].view(np.uint32)[:P + 1] = v.bounds.astype(np.uint32)
         return torch.from_numpy(buf)
 
     def _count(self, params, segs):
         P, radix = self._geometry(params)
-        for keys, pays, bounds in segs:
+        for keys, bounds in segs:
             # every gathered shard arrives partition-major with consistent bounds
             q = O.partition_ids(keys, P, radix, params.hash, params.hash_seed).astype(np.int64)
             expect = np.repeat(np.arange(P), np.diff(bounds.astype(np.int64)))
             assert np.array_equal(q, expect)
-        rkeys = np.concatenate([k for k, _, _ in segs]) if segs else np.zeros(0, dtype=np.int64)
+        rkeys = np.concatenate([k for k, _ in segs]) if segs else np.zeros(0, dtype=np.int64)
         return torch.tensor([O.semijoin_count_keys(rkeys, self.views[1].keys)], dtype=torch.int64)
 
     def join_packed(self, params, recv, sizes, maxn, P):
         return self._count(params, unpack_segments_numpy(recv.numpy(), sizes, maxn, P))
 
     def join_local(self, params, v):
-        return self._count(params, [(v.keys, v.pays, v.bounds)])
+        return self._count(params, [(v.keys, v.bounds)])
 
     def timers(self):
         return []

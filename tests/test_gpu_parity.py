@@ -290,3 +290,38 @@ def test_prepare_then_join(params):
         c.upload(phj.SIDE_PROBE, S)
         c.prepare(params)
         assert c.join(params).matches == O.semijoin_count(R, S)
+
+
+@pytest.mark.parametrize("params,env", [
+    (phj.radix_params((8, 8), hash=phj.HASH_MURMUR3, seed=SEED), {}),                       # fused LDS join
+    (phj.radix_params(num_partitions=2, hash=phj.HASH_XXH3, seed=SEED), {}),                # bucket tables
+    (phj.radix_params(num_partitions=64, hash=phj.HASH_XXH3, seed=SEED), {"PHJ_PTAB": "0"}),  # CSR tables
+])
+def test_key_only_build_segments(params, env, monkeypatch):
+    # the multi-GPU exchange ships build keys only (payloads NULL in every segment)
+    import ctypes
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    rng = np.random.default_rng(23)
+    R = np.stack([rng.integers(0, 400_000, 150_000, dtype=np.int64), np.arange(150_000, dtype=np.int64)], axis=1)
+    S = np.stack([rng.integers(0, 800_000, 700_000, dtype=np.int64), np.arange(700_000, dtype=np.int64)], axis=1)
+    ctxs = [phj.Context(0) for _ in range(4)]
+    try:
+        segs = []
+        for c, sh in zip(ctxs[1:], np.array_split(R, 3)):
+            c.upload(phj.SIDE_BUILD, sh)
+            v = c.partition(phj.SIDE_BUILD, params)
+            c.synchronize()
+            v.payloads = None
+            segs.append(v)
+        main = ctxs[0]
+        main.upload(phj.SIDE_PROBE, S)
+        main.partition(phj.SIDE_PROBE, params)
+        assert main.join_partitioned(params, segs).matches == O.semijoin_count(R, S)
+        # mixing key-only and full segments is rejected
+        segs[0].payloads = ctypes.c_void_p(segs[1].keys).value
+        with pytest.raises(phj.PhjError):
+            main.join_partitioned(params, segs)
+    finally:
+        for c in ctxs:
+            c.close()
