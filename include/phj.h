@@ -69,11 +69,19 @@ typedef struct phj_join_params {
      * (pass digits: high bits first). Maximum 22 bits (4,194,304 partitions). */
     uint32_t num_partitions;
     uint8_t radix_bits[2];
-    uint8_t reserved[2];
+    uint8_t flags;           /* PHJ_PART_* */
+    uint8_t reserved;
     /* NoPartitioning: hash-table slots per build tuple (>= 1). 0 selects the default. */
     double table_ratio;
 } phj_join_params;
 
+/* flags: PHJ_PART_STABLE asks phj_partition for the reference's exact layout
+ * (a STABLE partition: partition-major, then input order, as partitionTable
+ * writes it, RadixCluster/HashJoin.hpp:394-412). Without it a 2-pass
+ * partition may order the tuples inside each partition arbitrarily (the
+ * first pass then needs no histogram pass over the relation); partition
+ * contents, bounds and every join count are identical either way. */
+#define PHJ_PART_STABLE 0x1
 #define PHJ_MAX_TIMERS 32
 #define PHJ_TIMER_NAME 24
 

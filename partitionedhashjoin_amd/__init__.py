@@ -22,12 +22,18 @@ __all__ = ["Context", "radix_params", "nopart_params", "JoinParams", "JoinResult
            "HASH_MURMUR3", "SIDE_BUILD", "SIDE_PROBE", "DEFAULT_SEED"]
 
 DEFAULT_SEED = 0x9E3779B97F4A7C15
+PART_STABLE = 0x1   # include/phj.h PHJ_PART_STABLE
 
 
-def radix_params(bits=(8, 8), num_partitions=0, hash=HASH_MURMUR3, seed=DEFAULT_SEED) -> JoinParams:
+def radix_params(bits=(8, 8), num_partitions=0, hash=HASH_MURMUR3, seed=DEFAULT_SEED,
+                 stable=False) -> JoinParams:
     """RadixCluster parameters. num_partitions > 0 reproduces the reference's
-    `hash % P` partitioning (`phjoin -p P`); otherwise q = hash & (2^(b0+b1)-1)."""
+    `hash % P` partitioning (`phjoin -p P`); otherwise q = hash & (2^(b0+b1)-1).
+    stable=True asks `partition` for the reference's exact layout (input order
+    inside each partition, RadixCluster/HashJoin.hpp:394-412); otherwise the
+    order inside a partition is unspecified (PHJ_PART_STABLE, include/phj.h)."""
     p = JoinParams()
+    p.flags = PART_STABLE if stable else 0
     p.algo = ALGO_RADIX
     p.hash = hash
     p.hash_seed = seed

@@ -10,7 +10,7 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libphj_hip.so")
+LIB_PATH = os.environ.get("PHJ_LIB") or os.path.join(HERE, "libphj_hip.so")   # PHJ_LIB: an A/B build of the same sources
 
 PHJ_OK = 0
 PHJ_ERR_INVALID = -1
@@ -48,7 +48,8 @@ class Tuple(C.Structure):
 class JoinParams(C.Structure):
     _fields_ = [("algo", C.c_int32), ("hash", C.c_int32), ("hash_seed", C.c_uint64),
                 ("num_partitions", C.c_uint32), ("radix_bits", C.c_uint8 * 2),
-                ("reserved", C.c_uint8 * 2), ("table_ratio", C.c_double)]
+                ("flags", C.c_uint8), ("reserved", C.c_uint8),
+                ("table_ratio", C.c_double)]
 
 
 class JoinResult(C.Structure):

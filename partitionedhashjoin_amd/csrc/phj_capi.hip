@@ -58,6 +58,8 @@ struct Tuning {
     bool subpart = true;  // phj_join: sub-partition large partitions for the fused join
     bool timers = true;   // per-kernel timer events (phase events are always recorded)
     int fused_kpl = 4;    // fused join: S keys per lane per probe round (4 or 8)
+    bool p1_chunk = true; // 2-pass, unordered partitions: chunked pass 1 without a histogram pass
+    int p1_slots = 0;     // chunked pass 1: workgroups per shard (0 = fill the chip once, -1 = one per tile)
 };
 
 int env_int(const char* name, int dflt) {
@@ -76,6 +78,7 @@ struct Plan {
     uint32_t shift1 = 0, dmask1 = 0, dmask2 = 0;
     uint32_t Ppad = 1;    // nb1 * nb2 = final bounds length - 1
     uint32_t sub_bits = 0, sub_shift = 0;   // phj_join: sub-partitions per partition (refine_plan)
+    bool stable = false;  // PHJ_PART_STABLE: the reference's order inside each partition (not compared by ==)
     bool operator==(const Plan& o) const {
         return hk == o.hk && seed == o.seed && mode == o.mode && P == o.P && npass == o.npass &&
                nb1 == o.nb1 && nb2 == o.nb2 && sub_bits == o.sub_bits && sub_shift == o.sub_shift;
@@ -96,6 +99,8 @@ struct SideState {
     DevBuf kA, pA, kB, pB;
     DevBuf hist1, hist2, bounds1, tbase2, tseg2, bounds, partials;
     DevBuf dig;           // pass-2 digit column written by pass 1
+    DevBuf ccur, ctab, tstart;   // chunked pass 1: digit cursors + pool counter, chunk table, pass-2 tile starts
+    uint32_t gen = 0;            // chunked pass 1: tag of the current chunk-table entries
     phj_partitioned view{};
     bool partitioned = false;
     Plan plan;
@@ -311,6 +316,7 @@ int make_plan(phj_ctx* c, const phj_join_params* p, Plan& pl) {
     if (p->hash != PHJ_HASH_XXH3 && p->hash != PHJ_HASH_MURMUR3)
         return set_err(c, PHJ_ERR_INVALID, "unknown hash function");
     pl = Plan{};
+    pl.stable = (p->flags & PHJ_PART_STABLE) != 0;
     pl.hk = p->hash;
     pl.seed = p->hash_seed;
     if (p->num_partitions > 0) {
@@ -429,14 +435,43 @@ int scan_u32(phj_ctx* c, uint32_t* data, uint32_t len, uint32_t narrays, uint32_
     return PHJ_OK;
 }
 
+
 template <int BLOCK, int ITEMS, bool IN_AOS, bool OUT_AOS>
 int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const std::string& prefix,
                   uint64_t n, uint32_t hist_len) {
     constexpr int T = BLOCK * ITEMS;
     constexpr int NW = BLOCK / 64;
     const size_t hist_lds = static_cast<size_t>(NW) * a.nbins * 4;
-    const size_t sc_lds = scatter_lds_bytes(T, a.nbins, NW);
+    const size_t sc_lds = scatter_lds_bytes(T, a.nbins, NW, a.chunk_cursor != nullptr);
     const std::string hname = prefix + ".hist", cname = prefix + ".scan", sname = prefix + ".scatter";
+    if (a.chunk_cursor) {
+        // chunked pass 1: no histogram / scan; the digit cursors and the pool
+        // counter start at zero
+        PHJ_HIP(c, hipMemsetAsync(a.chunk_cursor, 0, chunk_state_bytes(a.nbins), c->ks));
+        c->since_ev++;
+        PHJ_TRY(timer_begin(c, sname.c_str(), n * 32 + (a.out_dig ? n * (a.dig_wide ? 2 : 1) : 0)));
+        if constexpr (IN_AOS && OUT_AOS && ITEMS <= 8) {
+            // persistent: as many workgroups per shard as fit the chip at once
+            // (two per CU at 81 KB of LDS), never more than the shard's tiles
+            const uint32_t ntiles = static_cast<uint32_t>((n + T - 1) / T);
+            const uint32_t per = (ntiles + kShards - 1) / kShards;
+            const uint32_t fit = std::max<uint32_t>(1, static_cast<uint32_t>(160 * 1024 / sc_lds));
+            uint32_t slots = std::max<uint32_t>(1, std::min<uint32_t>(per, fit * c->num_cus / kShards));
+            if (c->tune.p1_slots > 0) slots = std::min<uint32_t>(per, c->tune.p1_slots);
+            if (c->tune.p1_slots < 0) slots = per;   // one tile per workgroup
+            if (hk == kMurmur3)
+                hipLaunchKernelGGL((k_scatter_chunked<BLOCK, ITEMS, kMurmur3>), dim3(slots * kShards), dim3(BLOCK), sc_lds,
+                                   c->ks, a, ntiles, per);
+            else
+                hipLaunchKernelGGL((k_scatter_chunked<BLOCK, ITEMS, kXXH3>), dim3(slots * kShards), dim3(BLOCK), sc_lds,
+                                   c->ks, a, ntiles, per);
+            PHJ_LAUNCHED(c, sname);
+        } else {
+            (void)grid;
+            return set_err(c, PHJ_ERR_INVALID, "chunked pass 1 needs AoS input and output, <= 8 tuples per thread");
+        }
+        return timer_end(c);
+    }
     // algorithmic bytes: the histogram reads the key (a whole 16-B tuple when AoS)
     // or 1-2 B of a digit column; the scatter reads and writes every tuple once
     // (16 + 16 B) plus the digit column it leaves for pass 2
@@ -587,16 +622,32 @@ int partition_side(phj_ctx* c, int s, const Plan& pl) {
     const uint32_t tile = pass_tile(c, n, pl.nb1, &wc1);
     const uint32_t tile2 = pl.npass == 2 ? pass_tile(c, n, pl.nb2, &wc2) : 0;
     const uint32_t nt1 = (n + tile - 1) / tile;
-    const uint32_t nt2 = pl.npass == 2 ? (n + tile2 - 1) / tile2 + pl.nb1 : 0;  // bound
     const bool p1_aos = pl.npass == 2 && c->tune.p1_aos && !wc1;
     // pass 1 leaves the pass-2 digit in a column (tile kernels only)
     const bool dcol = pl.npass == 2 && c->tune.dcol && !wc1 && !wc2;
     const uint32_t dbytes = pl.bits2 > 8 ? 2 : 1;
     const char* tag = s == PHJ_SIDE_BUILD ? "R" : "S";
+    // Chunked pass 1 (unordered partitions, tile kernels): pass-1 chunks are
+    // the pass-2 tiles, every digit's run of a tile fits one workgroup thread
+    // (nb1 <= block) and spans at most two chunks (tile1 == tile2).
+    const bool chunked = pl.npass == 2 && !pl.stable && c->tune.p1_chunk && dcol && p1_aos && n > 0 &&
+                         tile == tile2 && pl.nb1 <= static_cast<uint32_t>(tile_shape(c, pl.nb1).block) &&
+                         tile / tile_shape(c, pl.nb1).block <= 8 &&   // registers: the next tile is prefetched
+                         (2 * (static_cast<uint64_t>(n) / tile + kShards) + kShards * pl.nb1) * tile < (1ull << 32);
+    // pool of pass-1 chunks, one region per shard: a shard takes at most
+    // `per` tiles, its chains need at most per + nb1 chunks (each wastes at
+    // most one partial chunk) and each tile reserves one up front (<= per unused)
+    const uint32_t per = (nt1 + kShards - 1) / kShards;
+    const uint32_t pool_stride = 2 * per + pl.nb1;
+    const uint32_t maxch = per + 1;   // chunks of one chain (every tuple of a shard in one digit)
+    const size_t slots1 = chunked ? static_cast<size_t>(kShards) * pool_stride * tile : n;
+    // pass-2 tiles (bound): one partial tile per segment, or per chain when chunked
+    const uint32_t nt2 = pl.npass == 2 ? (n + tile2 - 1) / tile2 + pl.nb1 * (chunked ? kShards : 1) : 0;
+    const uint32_t nt2max = nt2 + 8;
     // workspace (grow-only; allocation is outside the timed phases on reuse)
-    PHJ_TRY(ensure(c, S.kA, static_cast<size_t>(n) * (p1_aos ? 16 : 8)));
+    PHJ_TRY(ensure(c, S.kA, slots1 * (p1_aos ? 16 : 8)));
     if (!p1_aos) PHJ_TRY(ensure(c, S.pA, static_cast<size_t>(n) * 8));
-    PHJ_TRY(ensure(c, S.hist1, static_cast<size_t>(nt1) * pl.nb1 * 4));
+    if (!chunked) PHJ_TRY(ensure(c, S.hist1, static_cast<size_t>(nt1) * pl.nb1 * 4));
     PHJ_TRY(ensure(c, S.bounds1, (static_cast<size_t>(pl.nb1) + 1) * 4));
     if (pl.npass == 2) {
         PHJ_TRY(ensure(c, S.kB, static_cast<size_t>(n) * 8));
@@ -605,10 +656,22 @@ int partition_side(phj_ctx* c, int s, const Plan& pl) {
         PHJ_TRY(ensure(c, S.hist2, (static_cast<size_t>(nt2) + 8) * pl.nb2 * 4));
         PHJ_TRY(ensure(c, S.tseg2, (static_cast<size_t>(nt2) + 8) * 4));
         PHJ_TRY(ensure(c, S.bounds, (static_cast<size_t>(pl.Ppad) + 1) * 4));
-        if (dcol) PHJ_TRY(ensure(c, S.dig, static_cast<size_t>(n) * dbytes + 64));
+        if (dcol) PHJ_TRY(ensure(c, S.dig, slots1 * dbytes + 64));
+    }
+    if (chunked) {
+        PHJ_TRY(ensure(c, S.ccur, chunk_state_bytes(pl.nb1)));
+        PHJ_TRY(ensure(c, S.tstart, static_cast<size_t>(nt2max) * 8));   // tile_start, tile_cnt
+        // entries are tagged with the pass's generation: a fresh (zeroed, tag 0)
+        // table is never mistaken for a published chunk
+        void* before = S.ctab.p;
+        PHJ_TRY(ensure(c, S.ctab, static_cast<size_t>(kShards) * pl.nb1 * maxch * 8));
+        if (S.ctab.p != before) {
+            PHJ_HIP(c, hipMemsetAsync(S.ctab.p, 0, S.ctab.bytes, c->ks));
+            S.gen = 0;
+        }
     }
     if (c->dry) {   // scan scratch of both passes, then nothing is launched
-        PHJ_TRY(scan_u32(c, nullptr, nt1 * pl.nb1, 1, nt1 * pl.nb1, c->scan_scratch));
+        if (!chunked) PHJ_TRY(scan_u32(c, nullptr, nt1 * pl.nb1, 1, nt1 * pl.nb1, c->scan_scratch));
         if (pl.npass == 2 && n) PHJ_TRY(scan_u32(c, nullptr, nt2 * pl.nb2, 1, nt2 * pl.nb2, c->scan_scratch));
         return PHJ_OK;
     }
@@ -631,14 +694,31 @@ int partition_side(phj_ctx* c, int s, const Plan& pl) {
         a.dig_wide = dbytes == 2 ? 1u : 0u;
         a.dig2_mask = pl.dmask2;
     }
+    if (chunked) {
+        a.chunk_cursor = static_cast<uint32_t*>(S.ccur.p);
+        a.chunk_tab = static_cast<unsigned long long*>(S.ctab.p);
+        a.maxch = maxch;
+        a.pool_stride = pool_stride;
+        if (++S.gen == 0) {   // tags wrapped: clear the table (tag 0 is never published)
+            PHJ_HIP(c, hipMemsetAsync(S.ctab.p, 0, S.ctab.bytes, c->ks));
+            S.gen = 1;
+        }
+        a.gen = S.gen;
+    }
     if (wc1)
         PHJ_TRY(launch_pass_wc(c, pl.hk, true, a, nt1, tile, std::string(tag) + ".p1", n, nt1 * pl.nb1));
     else
         PHJ_TRY(launch_pass(c, pl.hk, true, p1_aos, a, nt1, std::string(tag) + ".p1", n, nt1 * pl.nb1));
     uint32_t* tb2 = pl.npass == 2 ? static_cast<uint32_t*>(S.tbase2.p) : nullptr;
-    hipLaunchKernelGGL(k_pass1_finish, dim3(1), dim3(1024), 0, c->ks, a.hist, nt1, pl.nb1, n,
-                       pl.npass == 2 ? tile2 : tile, static_cast<uint32_t*>(S.bounds1.p), tb2);
-    PHJ_LAUNCHED(c, "k_pass1_finish");
+    if (chunked) {
+        hipLaunchKernelGGL(k_pass1_finish_sizes, dim3(1), dim3(1024), 0, c->ks, a.chunk_cursor, pl.nb1, n, tile2,
+                           static_cast<uint32_t*>(S.bounds1.p), tb2);
+        PHJ_LAUNCHED(c, "k_pass1_finish_sizes");
+    } else {
+        hipLaunchKernelGGL(k_pass1_finish, dim3(1), dim3(1024), 0, c->ks, a.hist, nt1, pl.nb1, n,
+                           pl.npass == 2 ? tile2 : tile, static_cast<uint32_t*>(S.bounds1.p), tb2);
+        PHJ_LAUNCHED(c, "k_pass1_finish");
+    }
     if (pl.npass == 1) {
         S.view.keys = static_cast<const int64_t*>(S.kA.p);
         S.view.payloads = static_cast<const int64_t*>(S.pA.p);
@@ -655,9 +735,21 @@ int partition_side(phj_ctx* c, int s, const Plan& pl) {
         b.tile_seg = static_cast<const uint32_t*>(S.tseg2.p);
         b.nseg = pl.nb1;
         if (n) {
-            hipLaunchKernelGGL(k_tile_seg, dim3((pl.nb1 + kWaves - 1) / kWaves), dim3(kBlock), 0, c->ks, tb2,
-                               pl.nb1, static_cast<uint32_t*>(S.tseg2.p));
-            PHJ_LAUNCHED(c, "k_tile_seg");
+            if (chunked) {
+                uint32_t* ts = static_cast<uint32_t*>(S.tstart.p);
+                uint32_t* tc = ts + nt2max;
+                hipLaunchKernelGGL(k_tile_chunks, dim3((pl.nb1 + kWaves - 1) / kWaves), dim3(kBlock), 0, c->ks, tb2,
+                                   static_cast<const uint32_t*>(S.ccur.p), pl.nb1,
+                                   static_cast<const unsigned long long*>(S.ctab.p), maxch, tile2,
+                                   static_cast<uint32_t*>(S.tseg2.p), ts, tc);
+                PHJ_LAUNCHED(c, "k_tile_chunks");
+                b.tile_start = ts;
+                b.tile_cnt = tc;
+            } else {
+                hipLaunchKernelGGL(k_tile_seg, dim3((pl.nb1 + kWaves - 1) / kWaves), dim3(kBlock), 0, c->ks, tb2,
+                                   pl.nb1, static_cast<uint32_t*>(S.tseg2.p));
+                PHJ_LAUNCHED(c, "k_tile_seg");
+            }
         }
         b.n = n;
         b.ntiles1 = 0;
@@ -1078,6 +1170,8 @@ int phj_ctx_create(int device, phj_ctx** out) {
     c->tune.subpart = env_int("PHJ_SUBPART", 1) != 0;
     c->tune.timers = env_int("PHJ_TIMERS", 1) != 0;
     c->tune.fused_kpl = env_int("PHJ_FUSED_KPL", 4) == 8 ? 8 : 4;
+    c->tune.p1_chunk = env_int("PHJ_P1_CHUNK", 1) != 0;
+    c->tune.p1_slots = env_int("PHJ_P1_SLOTS", 0);
     {
         const int ev = env_int("PHJ_EVENTS", 1);   // 0 default, 1 no system fence, 2 device release
         c->tune.ev_flags = ev == 0 ? hipEventDefault : ev == 2 ? hipEventReleaseToDevice : hipEventDisableSystemFence;
@@ -1104,11 +1198,11 @@ void phj_ctx_destroy(phj_ctx* c) {
     (void)hipStreamSynchronize(c->aux);
     for (SideState& S : c->side) {
         for (DevBuf* b : {&S.owned, &S.kA, &S.pA, &S.kB, &S.pB, &S.hist1, &S.hist2, &S.bounds1, &S.tbase2,
-                          &S.bounds, &S.partials, &S.tseg2})
+                          &S.bounds, &S.partials, &S.tseg2, &S.dig, &S.ccur, &S.ctab, &S.tstart})
             free_buf(*b);
     }
     for (DevBuf* b : {&c->scan_partials, &c->prep, &c->tkeys, &c->tpays, &c->toffs, &c->gcursor, &c->items, &c->biglist,
-                      &c->count, &c->np_tab, &c->np_pays})
+                      &c->count, &c->np_tab, &c->np_pays, &c->fitems, &c->split})
         free_buf(*b);
     for (hipEvent_t e : c->evpool) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->stream);

@@ -76,6 +76,14 @@ __device__ __forceinline__ uint32_t digit_of(uint64_t key, const DigitFn& f) {
     return static_cast<uint32_t>(partition_q<HK>(key, f) >> f.shift) & f.dmask;
 }
 
+#ifndef PHJ_SHARDS
+#define PHJ_SHARDS 16
+#endif
+constexpr uint32_t kShards = PHJ_SHARDS;  // chunked pass 1: chains per digit (shard % 8 = the XCD)
+__host__ __device__ constexpr size_t chunk_pool_word(uint32_t nb, uint32_t x) { return (static_cast<size_t>(kShards) * nb + 31) / 32 * 32 + 32 * x; }
+__host__ __device__ constexpr size_t chunk_hint_word(uint32_t nb) { return chunk_pool_word(nb, kShards); }
+__host__ __device__ constexpr size_t chunk_state_bytes(uint32_t nb) { return chunk_hint_word(nb) * 4 + static_cast<size_t>(kShards) * nb * 8; }
+
 struct PassArgs {
     const int64_t* in_keys;     // AoS: tuple base ({id,payload} pairs); SoA: key column
     const int64_t* in_pays;     // SoA payload column (unused for AoS)
@@ -96,7 +104,22 @@ struct PassArgs {
     void* out_dig;              // pass-1 scatter: writes the NEXT pass's digit per output slot
     const void* in_dig;         // pass-2 histogram: counts this column instead of hashing keys
     uint32_t dig2_mask;         // next pass's digit = q & dig2_mask
-    uint32_t pad1;
+    uint32_t gen;               // chunked pass 1: tag of this pass's chunk-table entries
+    // Chunked pass 1 (no histogram pass): the output is a pool of T-tuple
+    // chunks; every digit fills kShards chains of chunks (one per XCD, so the
+    // atomic cursors and the chunks' partial lines stay in one L2), so a
+    // partition's order is unspecified (not the reference's stable order) but
+    // its contents are exact. nullptr = the stable path.
+    // chain state (chunk_state_* below): u32 tuples claimed per chain
+    // [kShards][nbins], u32 chunks taken from each shard's pool (one 128-B line
+    // each), u64 hint per chain = max over its published chunks of
+    // ((k + 1) << 32) | id
+    uint32_t* chunk_cursor;
+    unsigned long long* chunk_tab;  // [kShards][nbins][maxch]: (gen << 32) | pool chunk id of a chain's k-th chunk
+    const uint32_t* tile_start; // segmented pass over a chunked input: first input slot of each tile ...
+    const uint32_t* tile_cnt;   // ... and its tuple count
+    uint32_t maxch;             // chunks of one chain (bound)
+    uint32_t pool_stride;       // chunks of one shard's pool
     DigitFn f;
 };
 
@@ -131,8 +154,13 @@ __device__ __forceinline__ bool locate_tile_rt(const PassArgs& a, uint32_t tile,
     L.tb_s = a.tile_base[l];
     L.tseg = tile - L.tb_s;
     L.ntiles_s = a.tile_base[l + 1] - L.tb_s;
-    L.lo = a.seg_bounds[l] + L.tseg * T;
-    L.hi = min(a.seg_bounds[l + 1], L.lo + T);
+    if (a.tile_start) {   // a chunked input: every tile is one chunk of a segment's chains
+        L.lo = a.tile_start[tile];
+        L.hi = L.lo + a.tile_cnt[tile];
+    } else {
+        L.lo = a.seg_bounds[l] + L.tseg * T;
+        L.hi = min(a.seg_bounds[l + 1], L.lo + T);
+    }
     return true;
 }
 
@@ -365,8 +393,10 @@ __global__ __launch_bounds__(256) void k_hist_col(PassArgs a) {
 
 // LDS bytes of k_scatter for a tile of T tuples, nb digits, NW waves.
 // The per-tuple digit is kept as one byte when nb <= 256 (two otherwise).
-__host__ __device__ constexpr size_t scatter_lds_bytes(int T, uint32_t nb, int NW = kWaves) {
-    return static_cast<size_t>(T) * (nb <= 256 ? 17 : 18) + static_cast<size_t>(nb) * 4 * (NW + 2) + 64;
+// A chunked pass 1 adds one word per digit. At T = 4096, nb = 256, NW = 8
+// that is 80,960 B: still two workgroups per CU.
+__host__ __device__ constexpr size_t scatter_lds_bytes(int T, uint32_t nb, int NW = kWaves, bool chunked = false) {
+    return static_cast<size_t>(T) * (nb <= 256 ? 17 : 18) + static_cast<size_t>(nb) * 4 * (NW + (chunked ? 3 : 2)) + 64;
 }
 
 // Sorted-digit array of the scatter kernels: u8 for nb <= 256, else u16.
@@ -486,6 +516,195 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(PassArgs a) {
             store_tuple<OUT_AOS>(a, o, skey[k], spay[k]);
             if (a.out_dig) store_next_digit<HK>(a, o, skey[k]);
         }
+    }
+}
+
+// Chunked pass 1 of a 2-pass partition (unordered partitions, PHJ_PART_STABLE
+// unset): the same tile sort as k_scatter, but with no histogram pass before
+// it. The output is a pool of T-slot chunks; digit d of shard x (the
+// workgroup's XCD under round-robin dispatch) fills its own chain of chunks
+// through an atomic cursor. So a partition's order is unspecified, its
+// contents exact. The relation is read once (16 B/tuple) instead of twice.
+//
+// Persistent: gridDim = kShards * slots workgroups, shard x walks tiles
+// [x * per, (x + 1) * per) with stride `slots`. The cursor round trip of tile
+// i is in flight together with the loads of tile i + 1 (issued once tile i
+// sits in LDS), so each tile waits on about one memory round trip, as the
+// stable scatter does.
+//
+// Chunk protocol (host guarantees nb <= BLOCK, so digit d = thread d, and
+// T-slot chunks, so a run spans at most two): a run that STARTS a chunk
+// takes a pool chunk (the tile's reservation first, taken one tile ahead) and
+// publishes it in the chain's table and hint; it never waits before
+// publishing. A run that continues a chunk reads the id from the hint it
+// loaded beside its cursor add, or else waits for the table entry: that
+// chunk's owner claimed earlier, so it is resident and publishes without
+// waiting, and the wait always ends.
+template <int BLOCK, int ITEMS, int HK>
+__global__ __launch_bounds__(BLOCK)
+__attribute__((amdgpu_waves_per_eu((BLOCK * ITEMS <= 4096 ? 2 : 1) * BLOCK / 256)))   // what the LDS lets share a CU
+void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
+    constexpr int NW = BLOCK / 64;
+    constexpr int T = BLOCK * ITEMS;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t nb = a.nbins;
+    int64_t* skey = reinterpret_cast<int64_t*>(smem);
+    int64_t* spay = skey + T;
+    uint32_t* wcnt = reinterpret_cast<uint32_t*>(spay + T);  // [NW][nb]
+    uint32_t* gofs = wcnt + NW * nb;                          // [nb] k <  dsplit: slot = gofs + k
+    uint32_t* dstart = gofs + nb;                             // [nb] k >= dsplit: slot = dstart + k
+    uint32_t* tmp = dstart + nb;                              // 16 words
+    const SortedDigits sdig{tmp + 16, nb <= 256};             // [T]
+    uint32_t* dsplit = static_cast<uint32_t*>(sdig.end(T));   // [nb]
+
+    const uint32_t x = blockIdx.x % kShards, slots = gridDim.x / kShards;
+    const uint32_t t_end = min(ntiles, (x + 1) * per);
+    uint32_t tile = x * per + blockIdx.x / kShards;
+    if (tile >= t_end) return;
+    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const uint32_t wbase = wave * 64 * ITEMS;
+    uint32_t* curs = a.chunk_cursor + static_cast<size_t>(x) * nb;   // this shard's chains
+    uint32_t* pool = a.chunk_cursor + chunk_pool_word(nb, x);
+    unsigned long long* hints = reinterpret_cast<unsigned long long*>(a.chunk_cursor + chunk_hint_word(nb)) + static_cast<size_t>(x) * nb;
+    auto cur = [&](uint32_t d) { return curs + d; };
+    auto hint_of = [&](uint32_t d) { return hints + d; };
+    const unsigned long long tag = static_cast<unsigned long long>(a.gen) << 32;
+
+    // Every wave issues the same memory operations on every path (clamped
+    // indices, zero adds) so the compiler's vmcnt bookkeeping stays exact and
+    // the waits below cover only what they need, not the prefetch behind them.
+    int64_t key[ITEMS], pay[ITEMS];
+    const longlong2* rel = reinterpret_cast<const longlong2*>(a.in_keys);
+    auto load = [&](uint32_t t) {
+        const uint32_t lo = t * T;
+#pragma unroll
+        for (int i = 0; i < ITEMS; i++) {
+            const longlong2 v = rel[min(lo + wbase + i * 64 + lane, a.n - 1)];
+            key[i] = v.x;
+            pay[i] = v.y;
+        }
+    };
+    load(tile);
+    uint32_t resv = 0;   // the tile's reserved pool chunk
+    if (tid == 0) resv = atomicAdd(pool, 1u);
+
+    for (;;) {
+        const uint32_t lo = tile * T, cnt = min(static_cast<uint32_t>(T), a.n - lo);
+        for (uint32_t i = tid; i < NW * nb; i += BLOCK) wcnt[i] = 0;
+        __syncthreads();
+        uint32_t dig[ITEMS], rank[ITEMS];
+        uint32_t* my = wcnt + wave * nb;
+#pragma unroll
+        for (int i = 0; i < ITEMS; i++) {
+            const uint32_t e = wbase + i * 64 + lane;
+            const bool valid = e < cnt;
+            const uint32_t d = valid ? digit_of<HK>(static_cast<uint64_t>(key[i]), a.f) : 0u;
+            const uint64_t peers = match_digit(d, valid, a.nbits);
+            dig[i] = d;
+            rank[i] = 0;
+            if (valid) {
+                const uint32_t before = my[d];
+                const uint64_t lt = peers & lanemask_lt();
+                rank[i] = before + __popcll(lt);
+                if (lt == 0) my[d] = before + __popcll(peers);
+            }
+        }
+        __syncthreads();
+        // digit totals (d = tid) -> tile-local starts; claim the run in the chain
+        uint32_t c = 0, ds = 0, v0 = 0;
+        unsigned long long hint = 0;
+        {
+            if (tid < nb) {
+#pragma unroll
+                for (int w = 0; w < NW; w++) c += wcnt[w * nb + tid];
+            }
+            uint32_t total;
+            uint32_t run = block_exclusive_scan_t<NW>(c, tmp, total);
+            ds = run;
+            if (tid < nb) {
+#pragma unroll
+                for (int w = 0; w < NW; w++) {
+                    const uint32_t v = wcnt[w * nb + tid];
+                    wcnt[w * nb + tid] = run;
+                    run += v;
+                }
+            }
+            if (tid < nb && c) {
+                v0 = atomicAdd(cur(tid), c);
+                hint = __hip_atomic_load(hint_of(tid), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (tid == 0) {
+                tmp[12] = x * a.pool_stride + resv;
+                tmp[13] = 0;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < ITEMS; i++) {
+            const uint32_t e = wbase + i * 64 + lane;
+            if (e < cnt) {
+                const uint32_t pos = my[dig[i]] + rank[i];
+                skey[pos] = key[i];
+                spay[pos] = pay[i];
+                sdig.put(pos, dig[i]);
+            }
+        }
+        // the tile is in LDS: the next tile's loads and reservation go out
+        // behind the claims, into the same registers
+        const uint32_t next = tile + slots;
+        load(min(next, t_end - 1));   // unconditional (the last one is unused): exact vmcnt waits
+        if (tid == 0 && next < t_end) resv = atomicAdd(pool, 1u);
+        if (tid < nb && c) {
+            const uint32_t d = tid;
+            const uint32_t off = v0 % T, k0 = v0 / T, k1 = (v0 + c - 1) / T;
+            unsigned long long* tab = a.chunk_tab + (static_cast<size_t>(x) * nb + d) * a.maxch;
+            auto take = [&]() -> uint32_t {
+                if (atomicAdd(&tmp[13], 1u) == 0) return tmp[12];
+                return x * a.pool_stride + atomicAdd(pool, 1u);
+            };
+            auto publish = [&](uint32_t k, uint32_t id) {
+                __hip_atomic_store(&tab[k], tag | id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                atomicMax(hint_of(d), (static_cast<unsigned long long>(k + 1) << 32) | id);
+            };
+            uint32_t id0 = 0, id1 = 0;
+            if (off == 0) {
+                id0 = take();
+                publish(k0, id0);
+            }
+            if (k1 != k0) {
+                id1 = take();
+                publish(k1, id1);
+            }
+            if (off != 0) {
+                if ((hint >> 32) == k0 + 1ull) {
+                    id0 = static_cast<uint32_t>(hint);
+                } else {
+                    unsigned long long v;
+                    while (((v = __hip_atomic_load(&tab[k0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) != a.gen)
+                        __builtin_amdgcn_s_sleep(2);
+                    id0 = static_cast<uint32_t>(v);
+                }
+            }
+            // sorted element k of digit d goes to chain slot v0 + (k - ds)
+            const uint32_t split = ds + (T - off);
+            gofs[d] = id0 * T + off - ds;      // k <  split: chunk k0
+            dstart[d] = id1 * T - split;       // k >= split: chunk k1 (uint32 wrap-around)
+            dsplit[d] = split;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < ITEMS; i++) {
+            const uint32_t k = i * BLOCK + tid;
+            if (k < cnt) {
+                const uint32_t d = sdig.get(k);
+                const uint32_t o = (k < dsplit[d] ? gofs[d] : dstart[d]) + k;
+                store_tuple<true>(a, o, skey[k], spay[k]);
+                store_next_digit<HK>(a, o, skey[k]);
+            }
+        }
+        if (next >= t_end) break;
+        tile = next;
+        __syncthreads();   // LDS reads of this tile's stores before the next tile's counts
     }
 }
 
@@ -645,6 +864,88 @@ __global__ __launch_bounds__(kBlock) void k_tile_seg(const uint32_t* tile_base, 
     if (s >= nseg) return;
     const uint32_t lo = tile_base[s], hi = tile_base[s + 1];
     for (uint32_t t = lo + (threadIdx.x & 63); t < hi; t += 64) tile_seg[t] = s;
+}
+
+// Chunked pass-1 output: segment s's tiles are the chunks of its kShards
+// chains, shard by shard, chunk by chunk: tile_seg / tile_start (first slot) /
+// tile_cnt (tuples) of each. One wave per segment.
+__global__ __launch_bounds__(kBlock) void k_tile_chunks(const uint32_t* tile_base, const uint32_t* sizes,
+                                                        uint32_t nseg, const unsigned long long* chunk_tab,
+                                                        uint32_t maxch, uint32_t T, uint32_t* tile_seg,
+                                                        uint32_t* tile_start, uint32_t* tile_cnt) {
+    const uint32_t s = blockIdx.x * kWaves + (threadIdx.x >> 6);
+    if (s >= nseg) return;
+    const uint32_t lo = tile_base[s], hi = tile_base[s + 1];
+    uint32_t sz[kShards], first[kShards + 1];
+    first[0] = 0;
+#pragma unroll
+    for (uint32_t x = 0; x < kShards; x++) {
+        sz[x] = sizes[x * nseg + s];
+        first[x + 1] = first[x] + (sz[x] + T - 1) / T;
+    }
+    for (uint32_t t = lo + (threadIdx.x & 63); t < hi; t += 64) {
+        const uint32_t r = t - lo;
+        uint32_t x = 0;
+#pragma unroll
+        for (uint32_t y = 1; y < kShards; y++) x += r >= first[y] ? 1u : 0u;
+        uint32_t szx = 0, fx = 0;
+#pragma unroll
+        for (uint32_t y = 0; y < kShards; y++) {
+            if (y == x) {
+                szx = sz[y];
+                fx = first[y];
+            }
+        }
+        const uint32_t k = r - fx;
+        tile_seg[t] = s;
+        tile_start[t] = static_cast<uint32_t>(chunk_tab[(static_cast<size_t>(x) * nseg + s) * maxch + k]) * T;
+        tile_cnt[t] = min(T, szx - k * T);
+    }
+}
+
+// After a chunked pass 1: bounds1 = exclusive scan of the digit sizes (summed
+// over the shards: the segments' offsets in the pass-2 output) and
+// tile_base2 = exclusive scan of their chunk counts. One workgroup; nb <= 1024.
+__global__ __launch_bounds__(1024) void k_pass1_finish_sizes(const uint32_t* sizes, uint32_t nb, uint32_t n,
+                                                             uint32_t T, uint32_t* bounds1, uint32_t* tile_base2) {
+    __shared__ uint32_t tmp[2][16];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint32_t v = 0, t = 0;
+    if (tid < nb) {
+#pragma unroll
+        for (uint32_t x = 0; x < kShards; x++) {
+            const uint32_t z = sizes[x * nb + tid];
+            v += z;
+            t += (z + T - 1) / T;
+        }
+    }
+    uint32_t xs = v, ys = t;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t xv = __shfl_up(xs, o, 64), yv = __shfl_up(ys, o, 64);
+        if (lane >= (uint32_t)o) {
+            xs += xv;
+            ys += yv;
+        }
+    }
+    if (lane == 63) {
+        tmp[0][wave] = xs;
+        tmp[1][wave] = ys;
+    }
+    __syncthreads();
+    uint32_t bx = 0, by = 0;
+    for (uint32_t w = 0; w < wave; w++) {
+        bx += tmp[0][w];
+        by += tmp[1][w];
+    }
+    if (tid < nb) {
+        bounds1[tid] = bx + xs - v;
+        tile_base2[tid] = by + ys - t;
+    }
+    if (tid == 1023) {
+        bounds1[nb] = n;
+        tile_base2[nb] = by + ys;
+    }
 }
 
 // Final bounds after a segmented pass 2: bounds[s * nb2 + d].

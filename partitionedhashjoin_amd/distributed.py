@@ -19,6 +19,8 @@ this orchestration with the gloo backend.
 """
 from __future__ import annotations
 
+import os
+
 from dataclasses import dataclass
 
 import numpy as np
@@ -213,8 +215,12 @@ def distributed_join(engine, params, nR: int, nS: int, rank: int, world: int, di
     if world == 1:
         # no exchange waits on R: issue the long S partition first so the GPU
         # is busy while the host issues R's (small) kernels on the R stream
-        engine.partition(1, params)
-        view = engine.partition(0, params)
+        if os.environ.get("PHJ_W1_ORDER", "sr") == "rs":
+            view = engine.partition(0, params)
+            engine.partition(1, params)
+        else:
+            engine.partition(1, params)
+            view = engine.partition(0, params)
         engine.build_ready()
         cnt = engine.join_local(params, view)
         total = local = int(cnt.item())

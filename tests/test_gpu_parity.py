@@ -51,20 +51,53 @@ def test_partition_layout_matches_oracle(ctx, bits, nparts, hk, n):
     rng = np.random.default_rng(n + 17 * nparts + bits[0])
     rel = np.stack([rng.integers(-50_000, 50_000, n, dtype=np.int64),
                     np.arange(n, dtype=np.int64)], axis=1)
-    p = phj.radix_params(bits=bits, num_partitions=nparts, hash=hk, seed=SEED)
-    ctx.upload(phj.SIDE_PROBE, rel)
-    v = ctx.partition(phj.SIDE_PROBE, p)
-    keys, pays, bounds = ctx.download_partitioned(v)
     if nparts:
         P, radix = nparts, False
     else:
         P, radix = 1 << (bits[0] + bits[1]), True
     out, obounds = O.partition(rel, P, radix, _hash_kind(hk), SEED, workers=3)
-    assert np.array_equal(keys, out[:, 0])
-    assert np.array_equal(pays, out[:, 1])
-    assert v.num_partitions >= P
-    assert np.array_equal(bounds[:P + 1].astype(np.uint64), obounds)
-    assert np.all(bounds[P:] == n)
+    ctx.upload(phj.SIDE_PROBE, rel)
+    for stable in (True, False):
+        p = phj.radix_params(bits=bits, num_partitions=nparts, hash=hk, seed=SEED, stable=stable)
+        v = ctx.partition(phj.SIDE_PROBE, p)
+        keys, pays, bounds = ctx.download_partitioned(v)
+        assert v.num_partitions >= P
+        assert np.array_equal(bounds[:P + 1].astype(np.uint64), obounds)
+        assert np.all(bounds[P:] == n)
+        if stable:   # the reference's exact layout
+            assert np.array_equal(keys, out[:, 0])
+            assert np.array_equal(pays, out[:, 1])
+        else:        # same tuples in every partition, order inside a partition unspecified
+            assert_same_partitions(keys, pays, bounds, out, obounds)
+
+
+def assert_same_partitions(keys, pays, bounds, out, obounds):
+    """Partition by partition, the device tuples are a permutation of the
+    oracle's (the unordered layout of include/phj.h PHJ_PART_STABLE)."""
+    sizes = np.diff(np.asarray(obounds, dtype=np.int64))
+    pid = np.repeat(np.arange(len(sizes)), sizes)
+    got = np.lexsort((pays, keys, pid))
+    ref = np.lexsort((out[:, 1], out[:, 0], pid))
+    assert np.array_equal(keys[got], out[ref, 0])
+    assert np.array_equal(pays[got], out[ref, 1])
+
+
+@pytest.mark.parametrize("n", [4096 * 3, 1_000_003])
+def test_unordered_partition_under_skew(ctx, n):
+    # chunked pass 1: a hot key fills many chunks of one digit's chain, runs
+    # straddle chunk boundaries, and every other digit ends in a partial chunk
+    rng = np.random.default_rng(n)
+    keys = rng.integers(-(1 << 40), 1 << 40, n, dtype=np.int64)
+    keys[rng.random(n) < 0.4] = 7
+    rel = np.stack([keys, np.arange(n, dtype=np.int64)], axis=1)
+    ctx.upload(phj.SIDE_PROBE, rel)
+    for bits, hk in (((8, 8), phj.HASH_MURMUR3), ((4, 9), phj.HASH_XXH3), ((9, 2), phj.HASH_XXH3)):
+        out, ob = O.partition(rel, 1 << (bits[0] + bits[1]), True, _hash_kind(hk), SEED, workers=2)
+        for _ in range(2):   # a second pass reuses the chunk table (next generation)
+            v = ctx.partition(phj.SIDE_PROBE, phj.radix_params(bits, hash=hk, seed=SEED))
+            k, pay, b = ctx.download_partitioned(v)
+            assert np.array_equal(b[:len(ob)].astype(np.uint64), ob)
+            assert_same_partitions(k, pay, b, out, ob)
 
 
 def _gpu_count(ctx, R, S, params):

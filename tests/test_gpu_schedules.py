@@ -7,15 +7,18 @@ nontemporal stores (PHJ_NT), pass-1 output layout (PHJ_P1_AOS), the pass-2
 digit column (PHJ_DCOL), tile order
 (PHJ_XCD_REMAP), write-combining scatter (PHJ_WC), the one-pass limit of
 hash % P (PHJ_ONEPASS_MAX), the join's sub-partitioning of large partitions
-(PHJ_SUBPART), fused LDS join vs HBM tables (PHJ_FUSED), the
+(PHJ_SUBPART), the chunked pass 1 of unordered partitions (PHJ_P1_CHUNK) and its
+persistent workgroups per shard (PHJ_P1_SLOTS), fused LDS join vs HBM tables (PHJ_FUSED), the
 partitioned bucket tables vs CSR tables (PHJ_PTAB) and the CSR probe
 schedule (PHJ_PROBE_WAVE, PHJ_PROBE_ITEMS). Each is
-checked against the oracle's stable partition and semi-join count.
+checked against the oracle's stable partition (or, for the unordered layout,
+the same tuples in every partition) and semi-join count.
 """
 import numpy as np
 import pytest
 
 import partitionedhashjoin_amd as phj
+from test_gpu_parity import assert_same_partitions
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -47,6 +50,9 @@ SCHEDULES = [
     {"PHJ_R_AUX": "0"},
     {"PHJ_TIMERS": "0"},
     {"PHJ_FUSED_KPL": "8"},
+    {"PHJ_P1_CHUNK": "0"},
+    {"PHJ_P1_SLOTS": "-1"},                    # chunked pass 1: one tile per workgroup
+    {"PHJ_P1_SLOTS": "3"},                     # chunked pass 1: long persistent walks
 ]
 
 CASES = [((8, 8), 0, phj.HASH_MURMUR3), ((11, 0), 0, phj.HASH_XXH3), ((1, 0), 1000, phj.HASH_XXH3),
@@ -73,17 +79,21 @@ def test_partition_layout(tuned_ctx, n):
     keys = rng.integers(-80_000, 80_000, n, dtype=np.int64)
     keys[rng.random(n) < 0.3] = 42
     rel = np.stack([keys, np.arange(n, dtype=np.int64)], axis=1)
+    tuned_ctx.upload(phj.SIDE_PROBE, rel)
     for bits, nparts, hk in CASES:
-        p = phj.radix_params(bits=bits, num_partitions=nparts, hash=hk, seed=SEED)
-        tuned_ctx.upload(phj.SIDE_PROBE, rel)
-        v = tuned_ctx.partition(phj.SIDE_PROBE, p)
-        k, pay, bounds = tuned_ctx.download_partitioned(v)
         P, radix = (nparts, False) if nparts else (1 << (bits[0] + bits[1]), True)
         ok = O.HASH_MURMUR3 if hk == phj.HASH_MURMUR3 else O.HASH_XXH3
         out, ob = O.partition(rel, P, radix, ok, SEED, workers=2)
-        assert np.array_equal(k, out[:, 0]), (bits, nparts)
-        assert np.array_equal(pay, out[:, 1]), (bits, nparts)
-        assert np.array_equal(bounds[:P + 1].astype(np.uint64), ob), (bits, nparts)
+        for stable in (True, False):
+            p = phj.radix_params(bits=bits, num_partitions=nparts, hash=hk, seed=SEED, stable=stable)
+            v = tuned_ctx.partition(phj.SIDE_PROBE, p)
+            k, pay, bounds = tuned_ctx.download_partitioned(v)
+            assert np.array_equal(bounds[:P + 1].astype(np.uint64), ob), (bits, nparts, stable)
+            if stable:
+                assert np.array_equal(k, out[:, 0]), (bits, nparts)
+                assert np.array_equal(pay, out[:, 1]), (bits, nparts)
+            else:
+                assert_same_partitions(k, pay, bounds, out, ob)
 
 
 def test_join_counts(tuned_ctx):
