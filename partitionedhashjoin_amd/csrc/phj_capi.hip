@@ -60,6 +60,8 @@ struct Tuning {
     int fused_kpl = 4;    // fused join: S keys per lane per probe round (4 or 8)
     bool p1_chunk = true; // 2-pass, unordered partitions: chunked pass 1 without a histogram pass
     int p1_slots = 0;     // chunked pass 1: workgroups per shard (0 = fill the chip once, -1 = one per tile)
+    int p1_tps = static_cast<int>(kTilesPerShard);   // chunked pass 1: tiles per shard (sets the shard count)
+    int p1_min_tiles = 32768;  // chunked pass 1: smallest relation (in 4096-tuple tiles, ~134M tuples)
 };
 
 int env_int(const char* name, int dflt) {
@@ -454,16 +456,16 @@ int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const st
             // persistent: as many workgroups per shard as fit the chip at once
             // (two per CU at 81 KB of LDS), never more than the shard's tiles
             const uint32_t ntiles = static_cast<uint32_t>((n + T - 1) / T);
-            const uint32_t per = (ntiles + kShards - 1) / kShards;
+            const uint32_t per = (ntiles + a.nshards - 1) / a.nshards;
             const uint32_t fit = std::max<uint32_t>(1, static_cast<uint32_t>(160 * 1024 / sc_lds));
-            uint32_t slots = std::max<uint32_t>(1, std::min<uint32_t>(per, fit * c->num_cus / kShards));
+            uint32_t slots = std::max<uint32_t>(1, std::min<uint32_t>(per, fit * c->num_cus / a.nshards));
             if (c->tune.p1_slots > 0) slots = std::min<uint32_t>(per, c->tune.p1_slots);
             if (c->tune.p1_slots < 0) slots = per;   // one tile per workgroup
             if (hk == kMurmur3)
-                hipLaunchKernelGGL((k_scatter_chunked<BLOCK, ITEMS, kMurmur3>), dim3(slots * kShards), dim3(BLOCK), sc_lds,
+                hipLaunchKernelGGL((k_scatter_chunked<BLOCK, ITEMS, kMurmur3>), dim3(slots * a.nshards), dim3(BLOCK), sc_lds,
                                    c->ks, a, ntiles, per);
             else
-                hipLaunchKernelGGL((k_scatter_chunked<BLOCK, ITEMS, kXXH3>), dim3(slots * kShards), dim3(BLOCK), sc_lds,
+                hipLaunchKernelGGL((k_scatter_chunked<BLOCK, ITEMS, kXXH3>), dim3(slots * a.nshards), dim3(BLOCK), sc_lds,
                                    c->ks, a, ntiles, per);
             PHJ_LAUNCHED(c, sname);
         } else {
@@ -630,19 +632,27 @@ int partition_side(phj_ctx* c, int s, const Plan& pl) {
     // Chunked pass 1 (unordered partitions, tile kernels): pass-1 chunks are
     // the pass-2 tiles, every digit's run of a tile fits one workgroup thread
     // (nb1 <= block) and spans at most two chunks (tile1 == tile2).
+    // Measured: it pays at 200M tuples (16 chains per digit) and
+    // loses to the stable pass below ~100M, where fewer shards (more
+    // workgroups per cursor line) or more partial chunks cost more than the
+    // histogram read saves; so it starts at p1_min_tiles tiles.
     const bool chunked = pl.npass == 2 && !pl.stable && c->tune.p1_chunk && dcol && p1_aos && n > 0 &&
+                         nt1 >= static_cast<uint32_t>(c->tune.p1_min_tiles) &&
                          tile == tile2 && pl.nb1 <= static_cast<uint32_t>(tile_shape(c, pl.nb1).block) &&
                          tile / tile_shape(c, pl.nb1).block <= 8 &&   // registers: the next tile is prefetched
                          (2 * (static_cast<uint64_t>(n) / tile + kShards) + kShards * pl.nb1) * tile < (1ull << 32);
+    // chains per digit: ~kTilesPerShard tiles each, a power of two <= kShards
+    uint32_t nshards = 1;
+    while (nshards < kShards && static_cast<uint64_t>(nshards) * c->tune.p1_tps < nt1) nshards <<= 1;
     // pool of pass-1 chunks, one region per shard: a shard takes at most
     // `per` tiles, its chains need at most per + nb1 chunks (each wastes at
     // most one partial chunk) and each tile reserves one up front (<= per unused)
-    const uint32_t per = (nt1 + kShards - 1) / kShards;
+    const uint32_t per = (nt1 + nshards - 1) / nshards;
     const uint32_t pool_stride = 2 * per + pl.nb1;
     const uint32_t maxch = per + 1;   // chunks of one chain (every tuple of a shard in one digit)
-    const size_t slots1 = chunked ? static_cast<size_t>(kShards) * pool_stride * tile : n;
+    const size_t slots1 = chunked ? static_cast<size_t>(nshards) * pool_stride * tile : n;
     // pass-2 tiles (bound): one partial tile per segment, or per chain when chunked
-    const uint32_t nt2 = pl.npass == 2 ? (n + tile2 - 1) / tile2 + pl.nb1 * (chunked ? kShards : 1) : 0;
+    const uint32_t nt2 = pl.npass == 2 ? (n + tile2 - 1) / tile2 + pl.nb1 * (chunked ? nshards : 1) : 0;
     const uint32_t nt2max = nt2 + 8;
     // workspace (grow-only; allocation is outside the timed phases on reuse)
     PHJ_TRY(ensure(c, S.kA, slots1 * (p1_aos ? 16 : 8)));
@@ -664,7 +674,7 @@ int partition_side(phj_ctx* c, int s, const Plan& pl) {
         // entries are tagged with the pass's generation: a fresh (zeroed, tag 0)
         // table is never mistaken for a published chunk
         void* before = S.ctab.p;
-        PHJ_TRY(ensure(c, S.ctab, static_cast<size_t>(kShards) * pl.nb1 * maxch * 8));
+        PHJ_TRY(ensure(c, S.ctab, static_cast<size_t>(nshards) * pl.nb1 * maxch * 8));
         if (S.ctab.p != before) {
             PHJ_HIP(c, hipMemsetAsync(S.ctab.p, 0, S.ctab.bytes, c->ks));
             S.gen = 0;
@@ -699,6 +709,7 @@ int partition_side(phj_ctx* c, int s, const Plan& pl) {
         a.chunk_tab = static_cast<unsigned long long*>(S.ctab.p);
         a.maxch = maxch;
         a.pool_stride = pool_stride;
+        a.nshards = nshards;
         if (++S.gen == 0) {   // tags wrapped: clear the table (tag 0 is never published)
             PHJ_HIP(c, hipMemsetAsync(S.ctab.p, 0, S.ctab.bytes, c->ks));
             S.gen = 1;
@@ -711,7 +722,7 @@ int partition_side(phj_ctx* c, int s, const Plan& pl) {
         PHJ_TRY(launch_pass(c, pl.hk, true, p1_aos, a, nt1, std::string(tag) + ".p1", n, nt1 * pl.nb1));
     uint32_t* tb2 = pl.npass == 2 ? static_cast<uint32_t*>(S.tbase2.p) : nullptr;
     if (chunked) {
-        hipLaunchKernelGGL(k_pass1_finish_sizes, dim3(1), dim3(1024), 0, c->ks, a.chunk_cursor, pl.nb1, n, tile2,
+        hipLaunchKernelGGL(k_pass1_finish_sizes, dim3(1), dim3(1024), 0, c->ks, a.chunk_cursor, pl.nb1, nshards, n, tile2,
                            static_cast<uint32_t*>(S.bounds1.p), tb2);
         PHJ_LAUNCHED(c, "k_pass1_finish_sizes");
     } else {
@@ -739,7 +750,7 @@ int partition_side(phj_ctx* c, int s, const Plan& pl) {
                 uint32_t* ts = static_cast<uint32_t*>(S.tstart.p);
                 uint32_t* tc = ts + nt2max;
                 hipLaunchKernelGGL(k_tile_chunks, dim3((pl.nb1 + kWaves - 1) / kWaves), dim3(kBlock), 0, c->ks, tb2,
-                                   static_cast<const uint32_t*>(S.ccur.p), pl.nb1,
+                                   static_cast<const uint32_t*>(S.ccur.p), pl.nb1, nshards,
                                    static_cast<const unsigned long long*>(S.ctab.p), maxch, tile2,
                                    static_cast<uint32_t*>(S.tseg2.p), ts, tc);
                 PHJ_LAUNCHED(c, "k_tile_chunks");
@@ -1172,6 +1183,8 @@ int phj_ctx_create(int device, phj_ctx** out) {
     c->tune.fused_kpl = env_int("PHJ_FUSED_KPL", 4) == 8 ? 8 : 4;
     c->tune.p1_chunk = env_int("PHJ_P1_CHUNK", 1) != 0;
     c->tune.p1_slots = env_int("PHJ_P1_SLOTS", 0);
+    c->tune.p1_tps = std::max(1, env_int("PHJ_P1_TPS", static_cast<int>(kTilesPerShard)));
+    c->tune.p1_min_tiles = std::max(0, env_int("PHJ_P1_MIN_TILES", 32768));
     {
         const int ev = env_int("PHJ_EVENTS", 1);   // 0 default, 1 no system fence, 2 device release
         c->tune.ev_flags = ev == 0 ? hipEventDefault : ev == 2 ? hipEventReleaseToDevice : hipEventDisableSystemFence;

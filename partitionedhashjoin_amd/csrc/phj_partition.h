@@ -76,10 +76,13 @@ __device__ __forceinline__ uint32_t digit_of(uint64_t key, const DigitFn& f) {
     return static_cast<uint32_t>(partition_q<HK>(key, f) >> f.shift) & f.dmask;
 }
 
-#ifndef PHJ_SHARDS
-#define PHJ_SHARDS 16
-#endif
-constexpr uint32_t kShards = PHJ_SHARDS;  // chunked pass 1: chains per digit (shard % 8 = the XCD)
+// Chunked pass 1: up to kShards chains per digit (PassArgs::nshards of them;
+// with 8 or 16, shard % 8 is the XCD under round-robin dispatch). The host
+// picks about one shard per kTilesPerShard tiles: enough chains that no
+// cursor line takes too many atomics, few enough that partial last chunks
+// stay a small share of the pass-2 tiles.
+constexpr uint32_t kShards = 16;
+constexpr uint32_t kTilesPerShard = 3072;
 __host__ __device__ constexpr size_t chunk_pool_word(uint32_t nb, uint32_t x) { return (static_cast<size_t>(kShards) * nb + 31) / 32 * 32 + 32 * x; }
 __host__ __device__ constexpr size_t chunk_hint_word(uint32_t nb) { return chunk_pool_word(nb, kShards); }
 __host__ __device__ constexpr size_t chunk_state_bytes(uint32_t nb) { return chunk_hint_word(nb) * 4 + static_cast<size_t>(kShards) * nb * 8; }
@@ -106,7 +109,7 @@ struct PassArgs {
     uint32_t dig2_mask;         // next pass's digit = q & dig2_mask
     uint32_t gen;               // chunked pass 1: tag of this pass's chunk-table entries
     // Chunked pass 1 (no histogram pass): the output is a pool of T-tuple
-    // chunks; every digit fills kShards chains of chunks (one per XCD, so the
+    // chunks; every digit fills nshards chains of chunks (one per XCD, so the
     // atomic cursors and the chunks' partial lines stay in one L2), so a
     // partition's order is unspecified (not the reference's stable order) but
     // its contents are exact. nullptr = the stable path.
@@ -120,6 +123,8 @@ struct PassArgs {
     const uint32_t* tile_cnt;   // ... and its tuple count
     uint32_t maxch;             // chunks of one chain (bound)
     uint32_t pool_stride;       // chunks of one shard's pool
+    uint32_t nshards;           // chains per digit (<= kShards)
+    uint32_t pad3;
     DigitFn f;
 };
 
@@ -526,7 +531,7 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(PassArgs a) {
 // through an atomic cursor. So a partition's order is unspecified, its
 // contents exact. The relation is read once (16 B/tuple) instead of twice.
 //
-// Persistent: gridDim = kShards * slots workgroups, shard x walks tiles
+// Persistent: gridDim = nshards * slots workgroups, shard x walks tiles
 // [x * per, (x + 1) * per) with stride `slots`. The cursor round trip of tile
 // i is in flight together with the loads of tile i + 1 (issued once tile i
 // sits in LDS), so each tile waits on about one memory round trip, as the
@@ -557,9 +562,9 @@ void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
     const SortedDigits sdig{tmp + 16, nb <= 256};             // [T]
     uint32_t* dsplit = static_cast<uint32_t*>(sdig.end(T));   // [nb]
 
-    const uint32_t x = blockIdx.x % kShards, slots = gridDim.x / kShards;
+    const uint32_t x = blockIdx.x % a.nshards, slots = gridDim.x / a.nshards;
     const uint32_t t_end = min(ntiles, (x + 1) * per);
-    uint32_t tile = x * per + blockIdx.x / kShards;
+    uint32_t tile = x * per + blockIdx.x / a.nshards;
     if (tile >= t_end) return;
     const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const uint32_t wbase = wave * 64 * ITEMS;
@@ -870,9 +875,10 @@ __global__ __launch_bounds__(kBlock) void k_tile_seg(const uint32_t* tile_base, 
 // chains, shard by shard, chunk by chunk: tile_seg / tile_start (first slot) /
 // tile_cnt (tuples) of each. One wave per segment.
 __global__ __launch_bounds__(kBlock) void k_tile_chunks(const uint32_t* tile_base, const uint32_t* sizes,
-                                                        uint32_t nseg, const unsigned long long* chunk_tab,
-                                                        uint32_t maxch, uint32_t T, uint32_t* tile_seg,
-                                                        uint32_t* tile_start, uint32_t* tile_cnt) {
+                                                        uint32_t nseg, uint32_t nshards,
+                                                        const unsigned long long* chunk_tab, uint32_t maxch,
+                                                        uint32_t T, uint32_t* tile_seg, uint32_t* tile_start,
+                                                        uint32_t* tile_cnt) {
     const uint32_t s = blockIdx.x * kWaves + (threadIdx.x >> 6);
     if (s >= nseg) return;
     const uint32_t lo = tile_base[s], hi = tile_base[s + 1];
@@ -880,7 +886,7 @@ __global__ __launch_bounds__(kBlock) void k_tile_chunks(const uint32_t* tile_bas
     first[0] = 0;
 #pragma unroll
     for (uint32_t x = 0; x < kShards; x++) {
-        sz[x] = sizes[x * nseg + s];
+        sz[x] = x < nshards ? sizes[x * nseg + s] : 0u;
         first[x + 1] = first[x] + (sz[x] + T - 1) / T;
     }
     for (uint32_t t = lo + (threadIdx.x & 63); t < hi; t += 64) {
@@ -906,14 +912,14 @@ __global__ __launch_bounds__(kBlock) void k_tile_chunks(const uint32_t* tile_bas
 // After a chunked pass 1: bounds1 = exclusive scan of the digit sizes (summed
 // over the shards: the segments' offsets in the pass-2 output) and
 // tile_base2 = exclusive scan of their chunk counts. One workgroup; nb <= 1024.
-__global__ __launch_bounds__(1024) void k_pass1_finish_sizes(const uint32_t* sizes, uint32_t nb, uint32_t n,
-                                                             uint32_t T, uint32_t* bounds1, uint32_t* tile_base2) {
+__global__ __launch_bounds__(1024) void k_pass1_finish_sizes(const uint32_t* sizes, uint32_t nb, uint32_t nshards,
+                                                             uint32_t n, uint32_t T, uint32_t* bounds1,
+                                                             uint32_t* tile_base2) {
     __shared__ uint32_t tmp[2][16];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t v = 0, t = 0;
     if (tid < nb) {
-#pragma unroll
-        for (uint32_t x = 0; x < kShards; x++) {
+        for (uint32_t x = 0; x < nshards; x++) {
             const uint32_t z = sizes[x * nb + tid];
             v += z;
             t += (z + T - 1) / T;

@@ -36,3 +36,21 @@ def ctx():
     c = phj.Context(0)
     yield c
     c.close()
+
+
+@pytest.fixture(scope="session")
+def chunk_ctx(ctx):
+    """A context that takes the chunked (histogram-free) pass 1 at every size
+    (by default it starts at ~134M tuples; PHJ_P1_MIN_TILES, read at creation)."""
+    import partitionedhashjoin_amd as phj
+    old = os.environ.get("PHJ_P1_MIN_TILES")
+    os.environ["PHJ_P1_MIN_TILES"] = "0"
+    try:
+        c = phj.Context(0)
+    finally:
+        if old is None:
+            del os.environ["PHJ_P1_MIN_TILES"]
+        else:
+            os.environ["PHJ_P1_MIN_TILES"] = old
+    yield c
+    c.close()

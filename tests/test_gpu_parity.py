@@ -47,7 +47,7 @@ PART_CASES = [
 
 @pytest.mark.parametrize("bits,nparts,hk", PART_CASES)
 @pytest.mark.parametrize("n", [0, 1, 2047, 2048, 2049, 100_003])
-def test_partition_layout_matches_oracle(ctx, bits, nparts, hk, n):
+def test_partition_layout_matches_oracle(ctx, chunk_ctx, bits, nparts, hk, n):
     rng = np.random.default_rng(n + 17 * nparts + bits[0])
     rel = np.stack([rng.integers(-50_000, 50_000, n, dtype=np.int64),
                     np.arange(n, dtype=np.int64)], axis=1)
@@ -57,10 +57,11 @@ def test_partition_layout_matches_oracle(ctx, bits, nparts, hk, n):
         P, radix = 1 << (bits[0] + bits[1]), True
     out, obounds = O.partition(rel, P, radix, _hash_kind(hk), SEED, workers=3)
     ctx.upload(phj.SIDE_PROBE, rel)
-    for stable in (True, False):
+    chunk_ctx.upload(phj.SIDE_PROBE, rel)
+    for c, stable in ((ctx, True), (ctx, False), (chunk_ctx, False)):
         p = phj.radix_params(bits=bits, num_partitions=nparts, hash=hk, seed=SEED, stable=stable)
-        v = ctx.partition(phj.SIDE_PROBE, p)
-        keys, pays, bounds = ctx.download_partitioned(v)
+        v = c.partition(phj.SIDE_PROBE, p)
+        keys, pays, bounds = c.download_partitioned(v)
         assert v.num_partitions >= P
         assert np.array_equal(bounds[:P + 1].astype(np.uint64), obounds)
         assert np.all(bounds[P:] == n)
@@ -83,7 +84,8 @@ def assert_same_partitions(keys, pays, bounds, out, obounds):
 
 
 @pytest.mark.parametrize("n", [4096 * 3, 1_000_003])
-def test_unordered_partition_under_skew(ctx, n):
+def test_unordered_partition_under_skew(chunk_ctx, n):
+    ctx = chunk_ctx
     # chunked pass 1: a hot key fills many chunks of one digit's chain, runs
     # straddle chunk boundaries, and every other digit ends in a partial chunk
     rng = np.random.default_rng(n)

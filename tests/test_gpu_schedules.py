@@ -8,7 +8,7 @@ digit column (PHJ_DCOL), tile order
 (PHJ_XCD_REMAP), write-combining scatter (PHJ_WC), the one-pass limit of
 hash % P (PHJ_ONEPASS_MAX), the join's sub-partitioning of large partitions
 (PHJ_SUBPART), the chunked pass 1 of unordered partitions (PHJ_P1_CHUNK) and its
-persistent workgroups per shard (PHJ_P1_SLOTS), fused LDS join vs HBM tables (PHJ_FUSED), the
+persistent workgroups per shard (PHJ_P1_SLOTS) and shard count (PHJ_P1_TPS), fused LDS join vs HBM tables (PHJ_FUSED), the
 partitioned bucket tables vs CSR tables (PHJ_PTAB) and the CSR probe
 schedule (PHJ_PROBE_WAVE, PHJ_PROBE_ITEMS). Each is
 checked against the oracle's stable partition (or, for the unordered layout,
@@ -51,8 +51,11 @@ SCHEDULES = [
     {"PHJ_TIMERS": "0"},
     {"PHJ_FUSED_KPL": "8"},
     {"PHJ_P1_CHUNK": "0"},
-    {"PHJ_P1_SLOTS": "-1"},                    # chunked pass 1: one tile per workgroup
-    {"PHJ_P1_SLOTS": "3"},                     # chunked pass 1: long persistent walks
+    {"PHJ_P1_MIN_TILES": "0"},                                  # chunked pass 1 at every size
+    {"PHJ_P1_MIN_TILES": "0", "PHJ_P1_SLOTS": "-1"},            # one tile per workgroup
+    {"PHJ_P1_MIN_TILES": "0", "PHJ_P1_SLOTS": "3"},             # long persistent walks
+    {"PHJ_P1_MIN_TILES": "0", "PHJ_P1_TPS": "4"},               # 16 shards on small relations
+    {"PHJ_P1_MIN_TILES": "0", "PHJ_P1_TPS": "8", "PHJ_P1_SLOTS": "1"},  # 8 shards, one workgroup each
 ]
 
 CASES = [((8, 8), 0, phj.HASH_MURMUR3), ((11, 0), 0, phj.HASH_XXH3), ((1, 0), 1000, phj.HASH_XXH3),
