@@ -640,15 +640,16 @@ int partition_side(phj_ctx* c, int s, const Plan& pl) {
                          nt1 >= static_cast<uint32_t>(c->tune.p1_min_tiles) &&
                          tile == tile2 && pl.nb1 <= static_cast<uint32_t>(tile_shape(c, pl.nb1).block) &&
                          tile / tile_shape(c, pl.nb1).block <= 8 &&   // registers: the next tile is prefetched
-                         (2 * (static_cast<uint64_t>(n) / tile + kShards) + kShards * pl.nb1) * tile < (1ull << 32);
+                         (3 * (static_cast<uint64_t>(n) / tile + kShards) + kShards * pl.nb1) * tile < (1ull << 32);
     // chains per digit: ~kTilesPerShard tiles each, a power of two <= kShards
     uint32_t nshards = 1;
     while (nshards < kShards && static_cast<uint64_t>(nshards) * c->tune.p1_tps < nt1) nshards <<= 1;
     // pool of pass-1 chunks, one region per shard: a shard takes at most
-    // `per` tiles, its chains need at most per + nb1 chunks (each wastes at
-    // most one partial chunk) and each tile reserves one up front (<= per unused)
+    // `per` tiles, each with two chunks reserved up front (k_scatter_chunked;
+    // unused ones are never touched), then at most per + nb1 chunks for its
+    // chains' other starts (each chain wastes at most one partial chunk)
     const uint32_t per = (nt1 + nshards - 1) / nshards;
-    const uint32_t pool_stride = 2 * per + pl.nb1;
+    const uint32_t pool_stride = 3 * per + pl.nb1;
     const uint32_t maxch = per + 1;   // chunks of one chain (every tuple of a shard in one digit)
     const size_t slots1 = chunked ? static_cast<size_t>(nshards) * pool_stride * tile : n;
     // pass-2 tiles (bound): one partial tile per segment, or per chain when chunked

@@ -84,7 +84,8 @@ __device__ __forceinline__ uint32_t digit_of(uint64_t key, const DigitFn& f) {
 constexpr uint32_t kShards = 16;
 constexpr uint32_t kTilesPerShard = 3072;
 __host__ __device__ constexpr size_t chunk_pool_word(uint32_t nb, uint32_t x) { return (static_cast<size_t>(kShards) * nb + 31) / 32 * 32 + 32 * x; }
-__host__ __device__ constexpr size_t chunk_hint_word(uint32_t nb) { return chunk_pool_word(nb, kShards); }
+__host__ __device__ constexpr size_t chunk_ticket_word(uint32_t nb, uint32_t x) { return chunk_pool_word(nb, kShards + x); }
+__host__ __device__ constexpr size_t chunk_hint_word(uint32_t nb) { return chunk_pool_word(nb, 2 * kShards); }
 __host__ __device__ constexpr size_t chunk_state_bytes(uint32_t nb) { return chunk_hint_word(nb) * 4 + static_cast<size_t>(kShards) * nb * 8; }
 
 struct PassArgs {
@@ -539,7 +540,7 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(PassArgs a) {
 //
 // Chunk protocol (host guarantees nb <= BLOCK, so digit d = thread d, and
 // T-slot chunks, so a run spans at most two): a run that STARTS a chunk
-// takes a pool chunk (the tile's reservation first, taken one tile ahead) and
+// takes a pool chunk (the tile's two static reservations first) and
 // publishes it in the chain's table and hint; it never waits before
 // publishing. A run that continues a chunk reads the id from the hint it
 // loaded beside its cursor add, or else waits for the table entry: that
@@ -563,10 +564,10 @@ void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
     uint32_t* dsplit = static_cast<uint32_t*>(sdig.end(T));   // [nb]
 
     const uint32_t x = blockIdx.x % a.nshards, slots = gridDim.x / a.nshards;
+    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const uint32_t t_end = min(ntiles, (x + 1) * per);
     uint32_t tile = x * per + blockIdx.x / a.nshards;
     if (tile >= t_end) return;
-    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const uint32_t wbase = wave * 64 * ITEMS;
     uint32_t* curs = a.chunk_cursor + static_cast<size_t>(x) * nb;   // this shard's chains
     uint32_t* pool = a.chunk_cursor + chunk_pool_word(nb, x);
@@ -590,8 +591,6 @@ void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
         }
     };
     load(tile);
-    uint32_t resv = 0;   // the tile's reserved pool chunk
-    if (tid == 0) resv = atomicAdd(pool, 1u);
 
     for (;;) {
         const uint32_t lo = tile * T, cnt = min(static_cast<uint32_t>(T), a.n - lo);
@@ -639,7 +638,9 @@ void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
                 hint = __hip_atomic_load(hint_of(tid), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             if (tid == 0) {
-                tmp[12] = x * a.pool_stride + resv;
+                // the tile's reserved pool chunks are static: shard x's pool keeps
+                // its first 2 * per chunks for its tiles, two each
+                tmp[12] = x * a.pool_stride + 2 * (tile - x * per);
                 tmp[13] = 0;
             }
         }
@@ -657,15 +658,15 @@ void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
         // the tile is in LDS: the next tile's loads and reservation go out
         // behind the claims, into the same registers
         const uint32_t next = tile + slots;
-        load(min(next, t_end - 1));   // unconditional (the last one is unused): exact vmcnt waits
-        if (tid == 0 && next < t_end) resv = atomicAdd(pool, 1u);
+        load(next < t_end ? next : tile);   // unconditional (a last one goes unused): exact vmcnt waits
         if (tid < nb && c) {
             const uint32_t d = tid;
             const uint32_t off = v0 % T, k0 = v0 / T, k1 = (v0 + c - 1) / T;
             unsigned long long* tab = a.chunk_tab + (static_cast<size_t>(x) * nb + d) * a.maxch;
             auto take = [&]() -> uint32_t {
-                if (atomicAdd(&tmp[13], 1u) == 0) return tmp[12];
-                return x * a.pool_stride + atomicAdd(pool, 1u);
+                const uint32_t r = atomicAdd(&tmp[13], 1u);
+                if (r < 2) return tmp[12] + r;
+                return x * a.pool_stride + 2 * per + atomicAdd(pool, 1u);
             };
             auto publish = [&](uint32_t k, uint32_t id) {
                 __hip_atomic_store(&tab[k], tag | id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
