@@ -750,7 +750,7 @@ int partition_side(phj_ctx* c, int s, const Plan& pl) {
             if (chunked) {
                 uint32_t* ts = static_cast<uint32_t*>(S.tstart.p);
                 uint32_t* tc = ts + nt2max;
-                hipLaunchKernelGGL(k_tile_chunks, dim3((pl.nb1 + kWaves - 1) / kWaves), dim3(kBlock), 0, c->ks, tb2,
+                hipLaunchKernelGGL(k_tile_chunks, dim3((pl.nb1 * nshards + kWaves - 1) / kWaves), dim3(kBlock), 0, c->ks, tb2,
                                    static_cast<const uint32_t*>(S.ccur.p), pl.nb1, nshards,
                                    static_cast<const unsigned long long*>(S.ctab.p), maxch, tile2,
                                    static_cast<uint32_t*>(S.tseg2.p), ts, tc);

@@ -872,41 +872,30 @@ __global__ __launch_bounds__(kBlock) void k_tile_seg(const uint32_t* tile_base, 
     for (uint32_t t = lo + (threadIdx.x & 63); t < hi; t += 64) tile_seg[t] = s;
 }
 
-// Chunked pass-1 output: segment s's tiles are the chunks of its kShards
+// Chunked pass-1 output: segment s's tiles are the chunks of its nshards
 // chains, shard by shard, chunk by chunk: tile_seg / tile_start (first slot) /
-// tile_cnt (tuples) of each. One wave per segment.
+// tile_cnt (tuples) of each. One wave per chain (segment s, shard x): lane x'
+// reads chain (s, x')'s size for the chain's first tile, then the lanes write
+// the chain's chunks.
 __global__ __launch_bounds__(kBlock) void k_tile_chunks(const uint32_t* tile_base, const uint32_t* sizes,
                                                         uint32_t nseg, uint32_t nshards,
                                                         const unsigned long long* chunk_tab, uint32_t maxch,
                                                         uint32_t T, uint32_t* tile_seg, uint32_t* tile_start,
                                                         uint32_t* tile_cnt) {
-    const uint32_t s = blockIdx.x * kWaves + (threadIdx.x >> 6);
-    if (s >= nseg) return;
-    const uint32_t lo = tile_base[s], hi = tile_base[s + 1];
-    uint32_t sz[kShards], first[kShards + 1];
-    first[0] = 0;
+    const uint32_t w = blockIdx.x * kWaves + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (w >= nseg * nshards) return;
+    const uint32_t s = w / nshards, x = w - s * nshards;
+    const uint32_t z = lane < x ? sizes[lane * nseg + s] : 0u;   // chains before x in this segment
+    uint32_t before = (z + T - 1) / T;
 #pragma unroll
-    for (uint32_t x = 0; x < kShards; x++) {
-        sz[x] = x < nshards ? sizes[x * nseg + s] : 0u;
-        first[x + 1] = first[x] + (sz[x] + T - 1) / T;
-    }
-    for (uint32_t t = lo + (threadIdx.x & 63); t < hi; t += 64) {
-        const uint32_t r = t - lo;
-        uint32_t x = 0;
-#pragma unroll
-        for (uint32_t y = 1; y < kShards; y++) x += r >= first[y] ? 1u : 0u;
-        uint32_t szx = 0, fx = 0;
-#pragma unroll
-        for (uint32_t y = 0; y < kShards; y++) {
-            if (y == x) {
-                szx = sz[y];
-                fx = first[y];
-            }
-        }
-        const uint32_t k = r - fx;
-        tile_seg[t] = s;
-        tile_start[t] = static_cast<uint32_t>(chunk_tab[(static_cast<size_t>(x) * nseg + s) * maxch + k]) * T;
-        tile_cnt[t] = min(T, szx - k * T);
+    for (int o = 32; o > 0; o >>= 1) before += __shfl_xor(before, o, 64);
+    const uint32_t szx = sizes[x * nseg + s], nch = (szx + T - 1) / T;
+    const uint32_t t0 = tile_base[s] + before;
+    const unsigned long long* tab = chunk_tab + (static_cast<size_t>(x) * nseg + s) * maxch;
+    for (uint32_t k = lane; k < nch; k += 64) {
+        tile_seg[t0 + k] = s;
+        tile_start[t0 + k] = static_cast<uint32_t>(tab[k]) * T;
+        tile_cnt[t0 + k] = min(T, szx - k * T);
     }
 }
 
