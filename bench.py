@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, cpus) - 1")
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes")
+    ap.add_argument("--exchange", action="store_true",
+                    help="at one GPU, run the N>1 step (RCCL all-gather + all-reduce) on a world of one")
     return ap.parse_args()
 
 
@@ -134,6 +136,11 @@ def cpu_baseline(ctx, nR, nS, threads, verbose):
 
 def main():
     args = parse()
+    # stdout carries exactly one JSON line: libraries that print banners there
+    # (RCCL prints its version on communicator init) are sent to stderr
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -144,13 +151,17 @@ def main():
     import partitionedhashjoin_amd as phj
     from partitionedhashjoin_amd.distributed import HipShardEngine, distributed_join
 
-    if world > 1:
+    exchange = world > 1 or args.exchange
+    if exchange:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29571")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     nR, nS = args.primary, args.secondary
     params, alpha, workload = config_params(phj, args.config)
-    if world > 1 and params.algo != phj.ALGO_RADIX:
+    if exchange and params.algo != phj.ALGO_RADIX:
         raise SystemExit("multi-GPU bench runs the radix configs (c2, c5)")
     engine = HipShardEngine(local_rank)
     engine.generate(nR, nS, alpha, GEN_SEED, rank, world)
@@ -163,8 +174,8 @@ def main():
     def step():
         if radix:
             # per-kernel timers accumulate on the device; read once after the timed loop
-            return distributed_join(engine, params, nR, nS, rank, world, dist if world > 1 else None,
-                                    timers=False)
+            return distributed_join(engine, params, nR, nS, rank, world, dist if exchange else None,
+                                    timers=False, force_exchange=exchange)
         r = engine.ctx.join(params)
 
         class _R:
@@ -236,7 +247,8 @@ def main():
             "config": {"workload": workload, "primary": nR, "secondary": nS,
                        "radix_bits": list(params.radix_bits) if params.algo == phj.ALGO_RADIX else None,
                        "hash": "murmur3" if params.hash == phj.HASH_MURMUR3 else "xxh3",
-                       "skew": alpha, "parallelism": f"range-shard x{world}"},
+                       "skew": alpha, "parallelism": f"range-shard x{world}"
+                       + (" (exchange path)" if exchange and world == 1 else "")},
             "matches": int(matches),
             "expected_matches": inrange,
             "correct": int(matches) == inrange,
@@ -253,8 +265,8 @@ def main():
             cb = cpu_baseline(engine.ctx, nR, nS, threads, args.verbose)
             out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample")}
             out["cpu_matches_gpu"] = cb["matches"] == int(matches)
-        print(json.dumps(out), flush=True)
-    if world > 1:
+        print(json.dumps(out), file=json_out, flush=True)
+    if exchange:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -201,18 +201,20 @@ def _all_reduce(dist, t):
 
 
 def distributed_join(engine, params, nR: int, nS: int, rank: int, world: int, dist=None,
-                     timers: bool = True):
+                     timers: bool = True, force_exchange: bool = False):
     """Join the range-sharded relations already resident on every rank.
 
     One step: partition R (R stream); pack it; start the all-gather (RCCL,
     asynchronous); partition S meanwhile (main stream); wait for the gather;
     build + probe; all-reduce the count. The host waits once, for the
-    final count. With world == 1 no collective runs. timers=False leaves the
+    final count. With world == 1 no collective runs unless force_exchange
+    (which drives the N>1 branch, RCCL included, on a world of one: the
+    one-GPU test of the exchange path). timers=False leaves the
     per-kernel timers accumulating in the engine (read them once, after many
     steps, with engine.timers()).
     """
     torch = engine.torch
-    if world == 1:
+    if world == 1 and not force_exchange:
         # no exchange waits on R: issue the long S partition first so the GPU
         # is busy while the host issues R's (small) kernels on the R stream
         if os.environ.get("PHJ_W1_ORDER", "sr") == "rs":

@@ -70,3 +70,38 @@ def test_single_rank_generation_matches_sharded_generation():
             parts.append(full.download(1))
     import numpy as np
     assert np.array_equal(whole, np.concatenate(parts))
+
+
+def _nccl_worker(rank, port, nR, nS, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        import partitionedhashjoin_amd as phj
+        from partitionedhashjoin_amd.distributed import HipShardEngine, distributed_join
+        eng = HipShardEngine(0)
+        off = nR // 4
+        eng.ctx_r.generate_sequential(0, nR, 1 + off, 0)
+        eng.ctx.generate_zipf(1, nS, 1.05, 1, nR, 5, 0)
+        eng.share_build()
+        expect = eng.ctx.count_in_range(1, 1 + off, nR)
+        got = [distributed_join(eng, phj.radix_params((8, 8)), nR, nS, 0, 1, dist,
+                                force_exchange=True).matches for _ in range(3)]
+        out[0] = (got, expect)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_exchange_branch_world_one():
+    """The N>1 step (pack, asynchronous RCCL all-gather issued from the R
+    stream, S issued from the second host thread, work.wait, multi-segment
+    join, RCCL all-reduce) over the real nccl backend on a world of one: the
+    8-GPU bench runs exactly this code with more ranks."""
+    nR, nS = 1_000_003, 20_000_001
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_nccl_worker, args=(_free_port(), nR, nS, out), nprocs=1)
+    got, expect = out[0]
+    assert 0 < expect < nS
+    assert got == [expect] * 3
