@@ -27,8 +27,8 @@ using namespace phj;
 
 namespace {
 
-constexpr int kNPProbeItems = 4;
 constexpr double kNPDefaultRatio = 2.0;             // slots per build tuple
+constexpr uint32_t kNPRegionBuckets = 1024;           // NoPartitioning region build: buckets per region (LDS 60 B each)
 
 struct DevBuf {
     void* p = nullptr;
@@ -62,6 +62,9 @@ struct Tuning {
     int p1_slots = 0;     // chunked pass 1: workgroups per shard (0 = fill the chip once, -1 = one per tile)
     int p1_tps = static_cast<int>(kTilesPerShard);   // chunked pass 1: tiles per shard (sets the shard count)
     int p1_min_tiles = 32768;  // chunked pass 1: smallest relation (in 4096-tuple tiles, ~134M tuples)
+    int np_nt = 1;        // NoPartitioning probe: 1 nontemporal S loads, 2 also the bucket loads
+    int np_items = 4;     // NoPartitioning probe: S keys per thread per round (4 or 8)
+    bool np_region = true;   // NoPartitioning build: partition R into table regions, build each in LDS
 };
 
 int env_int(const char* name, int dflt) {
@@ -134,6 +137,7 @@ struct phj_ctx {
     SideState side[2];
     DevBuf scan_partials, prep, tkeys, tpays, toffs, gcursor, items, count, biglist;
     DevBuf np_tab, np_pays;
+    DevBuf np_ovf, np_ovfb, np_ovfn;   // region build: overflow tuples, their start buckets, count
     DevBuf fitems, split;   // fused join: item slots; wave clocks {build, probe} since the last timer reset
     std::vector<hipEvent_t> evpool;
     size_t evnext = 0;
@@ -1064,43 +1068,101 @@ int join_nopart(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
     if (ratio < 1.0) return set_err(c, PHJ_ERR_INVALID, "table_ratio must be >= 1");
     const double nbd = std::ceil(static_cast<double>(R.n) * ratio / kNPSlots);
     if (nbd >= 4294967295.0) return set_err(c, PHJ_ERR_RANGE, "table too large");
-    const uint32_t nb = std::max<uint32_t>(1, static_cast<uint32_t>(nbd));
+    const uint32_t nb0 = std::max<uint32_t>(1, static_cast<uint32_t>(nbd));
+    // region build: 2^rbits regions of <= kNPRegionBuckets buckets (LDS-sized)
+    NPHome g{nb0, nb0, 0, 0};
+    if (c->tune.np_region) {
+        g.rbits = std::min<uint32_t>(22, std::max<uint32_t>(1, ceil_log2((nb0 + kNPRegionBuckets - 1) / kNPRegionBuckets)));
+        g.nbr = (nb0 + (1u << g.rbits) - 1) >> g.rbits;
+        const uint64_t nbw = static_cast<uint64_t>(g.nbr) << g.rbits;
+        if (nbw >= 4294967295ull || g.nbr > 2 * kNPRegionBuckets) return set_err(c, PHJ_ERR_RANGE, "table too large");
+        g.nb = static_cast<uint32_t>(nbw);
+    }
+    const uint32_t nb = g.nb;
     PHJ_TRY(ensure(c, c->np_tab, static_cast<size_t>(nb) * sizeof(NPBucket)));
     PHJ_TRY(ensure(c, c->np_pays, static_cast<size_t>(nb) * kNPSlots * 8));
     PHJ_TRY(ensure(c, c->count, 8));
+    Plan rp;
+    if (g.rbits) {
+        PHJ_TRY(ensure(c, c->np_ovf, R.n * 16));
+        PHJ_TRY(ensure(c, c->np_ovfb, R.n * 4));
+        PHJ_TRY(ensure(c, c->np_ovfn, 4));
+        phj_join_params pp = *p;
+        pp.algo = PHJ_ALGO_RADIX;
+        pp.num_partitions = 0;
+        pp.flags = 0;
+        pp.radix_bits[1] = static_cast<uint8_t>(g.rbits <= 8 ? 0 : g.rbits / 2);
+        pp.radix_bits[0] = static_cast<uint8_t>(g.rbits - pp.radix_bits[1]);
+        PHJ_TRY(make_plan(c, &pp, rp));
+        if (c->dry) return partition_side(c, PHJ_SIDE_BUILD, rp);
+    }
     if (c->dry) return PHJ_OK;
     hipEvent_t e0, e1, e2;
     const uint32_t nR = static_cast<uint32_t>(R.n);
     PHJ_TRY(mark(c, &e0));
-    PHJ_TRY(timer_begin(c, "np.build", static_cast<uint64_t>(nR) * 32 + static_cast<uint64_t>(nb) * 64));
-    PHJ_HIP(c, hipMemsetAsync(c->np_tab.p, 0, static_cast<size_t>(nb) * sizeof(NPBucket), c->ks));
-    const uint32_t bg = (nR + kBlock - 1) / kBlock;
-    if (p->hash == PHJ_HASH_MURMUR3)
-        hipLaunchKernelGGL((k_np_build<kMurmur3>), dim3(bg), dim3(kBlock), 0, c->ks,
-                           reinterpret_cast<const longlong2*>(R.rel), nR, static_cast<NPBucket*>(c->np_tab.p),
-                           static_cast<int64_t*>(c->np_pays.p), nb, p->hash_seed);
-    else
-        hipLaunchKernelGGL((k_np_build<kXXH3>), dim3(bg), dim3(kBlock), 0, c->ks,
-                           reinterpret_cast<const longlong2*>(R.rel), nR, static_cast<NPBucket*>(c->np_tab.p),
-                           static_cast<int64_t*>(c->np_pays.p), nb, p->hash_seed);
-    PHJ_LAUNCHED(c, "k_np_build");
-    PHJ_TRY(timer_end(c));
+    if (g.rbits) {
+        // the partition is part of the build (its R.* timers show it)
+        PHJ_TRY(partition_side(c, PHJ_SIDE_BUILD, rp));
+        const phj_partitioned& v = R.view;
+        PHJ_TRY(timer_begin(c, "np.build", static_cast<uint64_t>(nR) * 32 + static_cast<uint64_t>(nb) * 64));
+        PHJ_HIP(c, hipMemsetAsync(c->np_ovfn.p, 0, 4, c->ks));
+        const size_t lds = static_cast<size_t>(g.nbr) * (kNPSlots * 8 + 4);
+        auto* ovn = static_cast<uint32_t*>(c->np_ovfn.p);
+        auto* ov = static_cast<longlong2*>(c->np_ovf.p);
+        auto* ovb = static_cast<uint32_t*>(c->np_ovfb.p);
+        auto* tab = static_cast<NPBucket*>(c->np_tab.p);
+        auto* pays = static_cast<int64_t*>(c->np_pays.p);
+        const dim3 grid(1u << g.rbits);
+        if (p->hash == PHJ_HASH_MURMUR3)
+            hipLaunchKernelGGL((k_np_build_region<kMurmur3>), grid, dim3(kBlock), lds, c->ks, v.keys, v.payloads,
+                               v.bounds, g, tab, pays, p->hash_seed, ovn, ov, ovb);
+        else
+            hipLaunchKernelGGL((k_np_build_region<kXXH3>), grid, dim3(kBlock), lds, c->ks, v.keys, v.payloads,
+                               v.bounds, g, tab, pays, p->hash_seed, ovn, ov, ovb);
+        PHJ_LAUNCHED(c, "k_np_build_region");
+        hipLaunchKernelGGL(k_np_build_overflow, dim3(64), dim3(kBlock), 0, c->ks, ovn, ov, ovb, tab, pays, nb);
+        PHJ_LAUNCHED(c, "k_np_build_overflow");
+        PHJ_TRY(timer_end(c));
+    } else {
+        PHJ_TRY(timer_begin(c, "np.build", static_cast<uint64_t>(nR) * 32 + static_cast<uint64_t>(nb) * 64));
+        PHJ_HIP(c, hipMemsetAsync(c->np_tab.p, 0, static_cast<size_t>(nb) * sizeof(NPBucket), c->ks));
+        const uint32_t bg = (nR + kBlock - 1) / kBlock;
+        if (p->hash == PHJ_HASH_MURMUR3)
+            hipLaunchKernelGGL((k_np_build<kMurmur3>), dim3(bg), dim3(kBlock), 0, c->ks,
+                               reinterpret_cast<const longlong2*>(R.rel), nR, static_cast<NPBucket*>(c->np_tab.p),
+                               static_cast<int64_t*>(c->np_pays.p), nb, p->hash_seed);
+        else
+            hipLaunchKernelGGL((k_np_build<kXXH3>), dim3(bg), dim3(kBlock), 0, c->ks,
+                               reinterpret_cast<const longlong2*>(R.rel), nR, static_cast<NPBucket*>(c->np_tab.p),
+                               static_cast<int64_t*>(c->np_pays.p), nb, p->hash_seed);
+        PHJ_LAUNCHED(c, "k_np_build");
+        PHJ_TRY(timer_end(c));
+    }
     PHJ_TRY(mark(c, &e1));
     PHJ_HIP(c, hipMemsetAsync(c->count.p, 0, 8, c->ks));
     if (S.n > 0) {
-        const uint64_t per = static_cast<uint64_t>(kBlock) * kNPProbeItems;
+        const uint64_t per = static_cast<uint64_t>(kBlock) * c->tune.np_items;
         const uint32_t pg = static_cast<uint32_t>(std::min<uint64_t>((S.n + per - 1) / per, 8192));
         PHJ_TRY(timer_begin(c, "np.probe", S.n * 16 + static_cast<uint64_t>(nb) * 64));
+        const auto* S_rel = reinterpret_cast<const longlong2*>(S.rel);
+        const auto* tab = static_cast<const NPBucket*>(c->np_tab.p);
+        auto* cnt = static_cast<unsigned long long*>(c->count.p);
+#define PHJ_NP_PROBE(HKV, IT, NTV) \
+    hipLaunchKernelGGL((k_np_probe<HKV, IT, NTV>), dim3(pg), dim3(kBlock), 0, c->ks, S_rel, S.n, tab, g, p->hash_seed, cnt)
+#define PHJ_NP_PROBE_H(HKV)                                                      \
+    do {                                                                         \
+        if (c->tune.np_items == 8) {                                             \
+            if (c->tune.np_nt == 2) PHJ_NP_PROBE(HKV, 8, 2); else if (c->tune.np_nt) PHJ_NP_PROBE(HKV, 8, 1); else PHJ_NP_PROBE(HKV, 8, 0); \
+        } else {                                                                 \
+            if (c->tune.np_nt == 2) PHJ_NP_PROBE(HKV, 4, 2); else if (c->tune.np_nt) PHJ_NP_PROBE(HKV, 4, 1); else PHJ_NP_PROBE(HKV, 4, 0); \
+        }                                                                        \
+    } while (0)
         if (p->hash == PHJ_HASH_MURMUR3)
-            hipLaunchKernelGGL((k_np_probe<kMurmur3, kNPProbeItems>), dim3(pg), dim3(kBlock), 0, c->ks,
-                               reinterpret_cast<const longlong2*>(S.rel), S.n,
-                               static_cast<const NPBucket*>(c->np_tab.p), nb, p->hash_seed,
-                               static_cast<unsigned long long*>(c->count.p));
+            PHJ_NP_PROBE_H(kMurmur3);
         else
-            hipLaunchKernelGGL((k_np_probe<kXXH3, kNPProbeItems>), dim3(pg), dim3(kBlock), 0, c->ks,
-                               reinterpret_cast<const longlong2*>(S.rel), S.n,
-                               static_cast<const NPBucket*>(c->np_tab.p), nb, p->hash_seed,
-                               static_cast<unsigned long long*>(c->count.p));
+            PHJ_NP_PROBE_H(kXXH3);
+#undef PHJ_NP_PROBE_H
+#undef PHJ_NP_PROBE
         PHJ_LAUNCHED(c, "k_np_probe");
         PHJ_TRY(timer_end(c));
     }
@@ -1183,6 +1245,9 @@ int phj_ctx_create(int device, phj_ctx** out) {
     c->tune.timers = env_int("PHJ_TIMERS", 1) != 0;
     c->tune.fused_kpl = env_int("PHJ_FUSED_KPL", 4) == 8 ? 8 : 4;
     c->tune.p1_chunk = env_int("PHJ_P1_CHUNK", 1) != 0;
+    c->tune.np_nt = std::min(2, std::max(0, env_int("PHJ_NP_NT", 1)));
+    c->tune.np_items = env_int("PHJ_NP_ITEMS", 4) == 8 ? 8 : 4;
+    c->tune.np_region = env_int("PHJ_NP_REGION", 1) != 0;
     c->tune.p1_slots = env_int("PHJ_P1_SLOTS", 0);
     c->tune.p1_tps = std::max(1, env_int("PHJ_P1_TPS", static_cast<int>(kTilesPerShard)));
     c->tune.p1_min_tiles = std::max(0, env_int("PHJ_P1_MIN_TILES", 32768));
@@ -1216,7 +1281,7 @@ void phj_ctx_destroy(phj_ctx* c) {
             free_buf(*b);
     }
     for (DevBuf* b : {&c->scan_partials, &c->prep, &c->tkeys, &c->tpays, &c->toffs, &c->gcursor, &c->items, &c->biglist,
-                      &c->count, &c->np_tab, &c->np_pays, &c->fitems, &c->split})
+                      &c->count, &c->np_tab, &c->np_pays, &c->np_ovf, &c->np_ovfb, &c->np_ovfn, &c->fitems, &c->split})
         free_buf(*b);
     for (hipEvent_t e : c->evpool) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->stream);

@@ -872,54 +872,109 @@ __global__ __launch_bounds__(kBlock) void k_np_build(const longlong2* R, uint32_
     }
 }
 
-template <int HK, int ITEMS>
-__global__ __launch_bounds__(kBlock) void k_np_probe(const longlong2* S, uint64_t nS,
-                                                     const NPBucket* tab, uint32_t nb,
-                                                     uint64_t seed, unsigned long long* count) {
-    __shared__ uint32_t red[kWaves];
-    uint32_t hits = 0;
-    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kBlock * ITEMS;
-    for (uint64_t base = static_cast<uint64_t>(blockIdx.x) * kBlock * ITEMS; base < nS; base += stride) {
-        int64_t k[ITEMS];
+// Region layout of the NoPartitioning table (the default build): the table is
+// 2^rbits regions of nbr buckets; a key's region is the low rbits of its hash
+// (exactly the radix partition q = h & (2^rbits - 1)) and its home bucket
+// inside the region comes from the high 32 bits. Linear probing still walks
+// b, b + 1, ... over the whole table, so a full last bucket of a region
+// continues in the next region. rbits == 0: one region of nb buckets (the
+// atomic build's plain multiply-shift home).
+struct NPHome {
+    uint32_t nb, nbr, rbits, pad;
+};
+
+__device__ __forceinline__ uint32_t np_home_r(uint64_t h, const NPHome& g) {
+    if (g.rbits == 0) return np_home(h, g.nb);
+    const uint32_t r = static_cast<uint32_t>(h) & ((1u << g.rbits) - 1);
+    return r * g.nbr + static_cast<uint32_t>(((h >> 32) * static_cast<uint64_t>(g.nbr)) >> 32);
+}
+
+// Region build: R radix-partitioned on q = h & (2^rbits - 1) beforehand
+// (partition_side), one workgroup per region builds that region's buckets in
+// LDS (LDS atomics claim slots; no device-scope atomics, which on MI355X go
+// to the memory side: the atomic build runs at ~14 G inserts/s) and writes the
+// region out as whole 64-B buckets. A tuple that walks past the region's last
+// bucket goes to an overflow list, inserted afterwards by k_np_build_overflow
+// from the next region's first bucket (the probe walks the same way).
+// LDS: nbr * (4 + 56) bytes.
+template <int HK>
+__global__ __launch_bounds__(kBlock) void k_np_build_region(const int64_t* keys, const int64_t* pays_in,
+                                                            const uint32_t* bounds, NPHome g, NPBucket* tab,
+                                                            int64_t* pays, uint64_t seed, uint32_t* ovf_n,
+                                                            longlong2* ovf, uint32_t* ovf_b) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t nbr = g.nbr, r = blockIdx.x;
+    int64_t* lkey = reinterpret_cast<int64_t*>(smem);
+    uint32_t* lfill = reinterpret_cast<uint32_t*>(lkey + static_cast<size_t>(nbr) * kNPSlots);
+    for (uint32_t i = threadIdx.x; i < nbr * kNPSlots; i += kBlock) lkey[i] = 0;
+    for (uint32_t i = threadIdx.x; i < nbr; i += kBlock) lfill[i] = 0;
+    __syncthreads();
+    const uint32_t lo = bounds[r], hi = bounds[r + 1];
+    const size_t b0 = static_cast<size_t>(r) * nbr;
+    // 4 tuples per thread per round: their loads and hashes before the LDS claims
+    constexpr int IT = 4;
+    for (uint32_t i0 = lo + threadIdx.x; i0 < hi; i0 += IT * kBlock) {
+        int64_t k[IT], v[IT];
 #pragma unroll
-        for (int j = 0; j < ITEMS; j++) {
-            const uint64_t idx = base + static_cast<uint64_t>(j) * kBlock + threadIdx.x;
-            k[j] = idx < nS ? S[idx].x : 0;
+        for (int j = 0; j < IT; j++) {
+            const uint32_t i = i0 + j * kBlock;
+            k[j] = i < hi ? keys[i] : 0;
+            v[j] = i < hi ? pays_in[i] : 0;
         }
 #pragma unroll
-        for (int j = 0; j < ITEMS; j++) {
-            const uint64_t idx = base + static_cast<uint64_t>(j) * kBlock + threadIdx.x;
-            if (idx < nS) {
-                const int64_t key = k[j];
-                uint32_t b = np_home(hash64<HK>(static_cast<uint64_t>(key), seed), nb);
-                for (uint32_t step = 0; step < nb; step++) {
-                    const longlong2* bp = reinterpret_cast<const longlong2*>(tab + b);
-                    const longlong2 q0 = bp[0], q1 = bp[1], q2 = bp[2], q3 = bp[3];
-                    const uint32_t fill = static_cast<uint32_t>(q3.y);
-                    const uint32_t c = fill < kNPSlots ? fill : kNPSlots;
-                    const bool hit = (c > 0 && q0.x == key) || (c > 1 && q0.y == key) ||
-                                     (c > 2 && q1.x == key) || (c > 3 && q1.y == key) ||
-                                     (c > 4 && q2.x == key) || (c > 5 && q2.y == key) ||
-                                     (c > 6 && q3.x == key);
-                    if (hit) {
-                        hits++;
-                        break;
-                    }
-                    if (fill < kNPSlots) break;
-                    b = (b + 1 == nb) ? 0 : b + 1;
+        for (int j = 0; j < IT; j++) {
+            if (i0 + j * kBlock >= hi) break;
+            const uint64_t h = hash64<HK>(static_cast<uint64_t>(k[j]), seed);
+            uint32_t b = static_cast<uint32_t>(((h >> 32) * static_cast<uint64_t>(nbr)) >> 32);
+            for (;;) {
+                const uint32_t slot = atomicAdd(&lfill[b], 1u);
+                if (slot < kNPSlots) {
+                    lkey[b * kNPSlots + slot] = k[j];
+                    pays[(b0 + b) * kNPSlots + slot] = v[j];
+                    break;
+                }
+                if (++b == nbr) {   // past the region: insert later from the next region
+                    const uint32_t o = atomicAdd(ovf_n, 1u);
+                    ovf[o] = make_longlong2(k[j], v[j]);
+                    ovf_b[o] = static_cast<uint32_t>((b0 + nbr) % g.nb);
+                    break;
                 }
             }
         }
     }
-    uint32_t x = hits;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x += __shfl_down(x, o, 64);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = x;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long t = 0;
-        for (int w = 0; w < kWaves; w++) t += red[w];
-        if (t) atomicAdd(count, t);
+    // whole buckets out: 4 lanes per 64-B bucket, consecutive buckets contiguous
+    longlong2* out = reinterpret_cast<longlong2*>(tab + b0);
+    for (uint32_t i = threadIdx.x; i < nbr * 4; i += kBlock) {
+        const uint32_t b = i >> 2, w = i & 3;
+        longlong2 v;
+        if (w < 3) {
+            v = make_longlong2(lkey[b * kNPSlots + 2 * w], lkey[b * kNPSlots + 2 * w + 1]);
+        } else {
+            v = make_longlong2(lkey[b * kNPSlots + 6], static_cast<int64_t>(lfill[b]));
+        }
+        out[i] = v;
+    }
+}
+
+// The overflow list of k_np_build_region, inserted with device atomics (rare:
+// about one tuple per few regions at the default 1.25 ratio).
+__global__ __launch_bounds__(kBlock) void k_np_build_overflow(const uint32_t* ovf_n, const longlong2* ovf,
+                                                              const uint32_t* ovf_b, NPBucket* tab, int64_t* pays,
+                                                              uint32_t nb) {
+    const uint32_t n = *ovf_n;
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+        const longlong2 t = ovf[i];
+        uint32_t b = ovf_b[i];
+        for (uint32_t step = 0; step < nb; step++) {
+            const uint32_t slot = atomicAdd(&tab[b].fill, 1u);
+            if (slot < kNPSlots) {
+                tab[b].key[slot] = t.x;
+                pays[static_cast<size_t>(b) * kNPSlots + slot] = t.y;
+                break;
+            }
+            b = (b + 1 == nb) ? 0 : b + 1;
+        }
     }
 }
 
@@ -938,6 +993,79 @@ __device__ __forceinline__ bool np_lookup(const NPBucket* tab, uint32_t nb, uint
         b = (b + 1 == nb) ? 0 : b + 1;
     }
     return false;
+}
+
+// NT: the probe keys are streamed with nontemporal loads, so the 3.2 GB of S
+// passing through does not evict the table's hot buckets from L2 / MALL (the
+// table is ~114 MB at 10M build tuples; under Zipf most probes hit a few
+// thousand buckets).
+template <int HK, int ITEMS, int NT>
+__global__ __launch_bounds__(kBlock) void k_np_probe(const longlong2* S, uint64_t nS,
+                                                     const NPBucket* tab, NPHome g,
+                                                     uint64_t seed, unsigned long long* count) {
+    const uint32_t nb = g.nb;
+    __shared__ uint32_t red[kWaves];
+    uint32_t hits = 0;
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kBlock * ITEMS;
+    for (uint64_t base = static_cast<uint64_t>(blockIdx.x) * kBlock * ITEMS; base < nS; base += stride) {
+        int64_t k[ITEMS];
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const uint64_t idx = base + static_cast<uint64_t>(j) * kBlock + threadIdx.x;
+            if constexpr (NT > 0)
+                k[j] = idx < nS ? __builtin_nontemporal_load(&S[idx].x) : 0;
+            else
+                k[j] = idx < nS ? S[idx].x : 0;
+        }
+        // every home bucket of the round is requested before any is compared:
+        // ITEMS random 64-B reads in flight per thread, not one
+        uint32_t b[ITEMS];
+        longlong2 q[ITEMS][4];
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            b[j] = np_home_r(hash64<HK>(static_cast<uint64_t>(k[j]), seed), g);
+            const longlong2* bp = reinterpret_cast<const longlong2*>(tab + b[j]);
+            if constexpr (NT > 1) {
+                typedef long long v2i __attribute__((ext_vector_type(2)));
+                const v2i* vp = reinterpret_cast<const v2i*>(bp);
+#pragma unroll
+                for (int w = 0; w < 4; w++) {
+                    const v2i a = __builtin_nontemporal_load(vp + w);
+                    q[j][w] = make_longlong2(a.x, a.y);
+                }
+            } else {
+#pragma unroll
+                for (int w = 0; w < 4; w++) q[j][w] = bp[w];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const uint64_t idx = base + static_cast<uint64_t>(j) * kBlock + threadIdx.x;
+            if (idx < nS) {
+                const int64_t key = k[j];
+                const uint32_t fill = static_cast<uint32_t>(q[j][3].y);
+                const uint32_t c = fill < kNPSlots ? fill : kNPSlots;
+                const bool hit = (c > 0 && q[j][0].x == key) || (c > 1 && q[j][0].y == key) ||
+                                 (c > 2 && q[j][1].x == key) || (c > 3 && q[j][1].y == key) ||
+                                 (c > 4 && q[j][2].x == key) || (c > 5 && q[j][2].y == key) ||
+                                 (c > 6 && q[j][3].x == key);
+                if (hit)
+                    hits++;
+                else if (fill >= kNPSlots)   // full home bucket: continue in the next ones (rare)
+                    hits += np_lookup(tab, nb, b[j] + 1 == nb ? 0 : b[j] + 1, key) ? 1u : 0u;
+            }
+        }
+    }
+    uint32_t x = hits;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_down(x, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (int w = 0; w < kWaves; w++) t += red[w];
+        if (t) atomicAdd(count, t);
+    }
 }
 
 // ---------------------------------------------------------------------------
