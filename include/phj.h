@@ -156,6 +156,27 @@ int phj_join(phj_ctx *ctx, const phj_join_params *p, phj_join_result *r);
  * and a first phj_join after phj_prepare allocates nothing. Optional. */
 int phj_prepare(phj_ctx *ctx, const phj_join_params *p);
 
+/* ---- materialised join ---- */
+/* Common::JoinedTuple (src/Common/Table.hpp:27-33): {id, payloadA, payloadB}, 24 B. */
+typedef struct phj_joined {
+    int64_t id;
+    int64_t payload_a; /* build (tableA) payload of the first match: HashTable::Get (LinearProbing.hpp:160-180) */
+    int64_t payload_b; /* probe (tableB) payload */
+} phj_joined;
+/* The join of phj_join (same params, same count), materialised: one row per
+ * probe tuple with a match, into a ctx-owned device buffer. This is the
+ * Table<JoinedTuple> the reference's Run() declares but returns empty
+ * (NoPartitioning/HashJoin.hpp:186, RadixCluster/HashJoin.hpp:240). Rows are
+ * in the probe side's storage order (input order for NoPartitioning,
+ * partition order for the radix join). The radix form needs one build
+ * segment. Synchronous; r->matches = number of rows. */
+int phj_join_materialize(phj_ctx *ctx, const phj_join_params *p, phj_join_result *r);
+/* The rows of the last phj_join_materialize: device pointer (ctx-owned, valid
+ * until the next materialised join) and count. */
+const phj_joined *phj_joined_rows(phj_ctx *ctx, uint64_t *n);
+/* Copy the first n rows of the last phj_join_materialize to host memory. */
+int phj_joined_download(phj_ctx *ctx, phj_joined *host, uint64_t n);
+
 /* ---- building blocks (multi-GPU: range-sharded relations, RCCL exchange) ---- */
 /* Radix-partition the bound relation of `side`; fills `out` with ctx-owned views.
  * Asynchronous on the ctx stream (order later work on the same stream). */

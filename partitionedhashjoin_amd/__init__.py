@@ -140,6 +140,23 @@ class Context:
         self._check(self._L.phj_join(self._h, C.byref(params), C.byref(r)))
         return r
 
+    def join_materialize(self, params: JoinParams) -> JoinResult:
+        """phj_join_materialize: the join's rows (JoinedTuple) in a device buffer;
+        r.matches rows. Read them with joined()."""
+        r = JoinResult()
+        self._check(self._L.phj_join_materialize(self._h, C.byref(params), C.byref(r)))
+        return r
+
+    def joined(self, n: int | None = None) -> np.ndarray:
+        """Rows of the last materialised join as an (n, 3) int64 array
+        {id, payloadA (build), payloadB (probe)}."""
+        total = C.c_uint64(0)
+        self._L.phj_joined_rows(self._h, C.byref(total))
+        n = total.value if n is None else n
+        out = np.zeros((n, 3), dtype=np.int64)
+        self._check(self._L.phj_joined_download(self._h, out.ctypes.data_as(C.c_void_p), n))
+        return out
+
     def partition(self, side: int, params: JoinParams) -> Partitioned:
         v = Partitioned()
         self._check(self._L.phj_partition(self._h, side, C.byref(params), C.byref(v)))

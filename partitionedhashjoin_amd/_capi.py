@@ -36,7 +36,7 @@ EXPORTED = [
     "phj_relation_generate_sequential", "phj_relation_generate_zipf",
     "phj_relation_count_in_range", "phj_join", "phj_partition", "phj_join_partitioned",
     "phj_partitioned_download", "phj_hash_keys", "phj_timers_report", "phj_join_partitioned_async",
-    "phj_prepare",
+    "phj_prepare", "phj_join_materialize", "phj_joined_rows", "phj_joined_download",
 ]
 
 
@@ -119,6 +119,9 @@ def load():
         "phj_timers_report": (i, [P, C.POINTER(JoinResult)]),
         "phj_join_partitioned_async": (i, [P, C.POINTER(JoinParams), i, C.POINTER(Partitioned), P]),
         "phj_prepare": (i, [P, C.POINTER(JoinParams)]),
+        "phj_join_materialize": (i, [P, C.POINTER(JoinParams), C.POINTER(JoinResult)]),
+        "phj_joined_rows": (P, [P, C.POINTER(u64)]),
+        "phj_joined_download": (i, [P, P, u64]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

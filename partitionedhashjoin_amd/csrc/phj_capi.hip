@@ -20,6 +20,7 @@
 
 #include "../../include/phj.h"
 #include "phj_join.h"
+#include "phj_mat.h"
 #include "phj_partition.h"
 #include "phj_partition_wc.h"
 
@@ -138,7 +139,9 @@ struct phj_ctx {
     DevBuf scan_partials, prep, tkeys, tpays, toffs, gcursor, items, count, biglist;
     DevBuf np_tab, np_pays;
     DevBuf np_ovf, np_ovfb, np_ovfn;   // region build: overflow tuples, their start buckets, count
-    DevBuf fitems, split;   // fused join: item slots; wave clocks {build, probe} since the last timer reset
+    DevBuf fitems, split;
+    DevBuf mat_mark, mat_cnt, mat_rows;   // materialised join: per-probe match, block offsets, rows
+    uint64_t mat_n = 0;   // fused join: item slots; wave clocks {build, probe} since the last timer reset
     std::vector<hipEvent_t> evpool;
     size_t evnext = 0;
     std::vector<TimerRec> timers;
@@ -1055,7 +1058,9 @@ int get_count(phj_ctx* c, uint64_t* out) {
     return PHJ_OK;
 }
 
-int join_nopart(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
+// marks != nullptr: the probe also writes, per probe tuple, its match's payload
+// slot (phj_join_materialize)
+int join_nopart(phj_ctx* c, const phj_join_params* p, phj_join_result* r, uint32_t* marks = nullptr) {
     SideState& R = c->side[PHJ_SIDE_BUILD];
     SideState& S = c->side[PHJ_SIDE_PROBE];
     if (p->hash != PHJ_HASH_XXH3 && p->hash != PHJ_HASH_MURMUR3)
@@ -1157,7 +1162,15 @@ int join_nopart(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
             if (c->tune.np_nt == 2) PHJ_NP_PROBE(HKV, 4, 2); else if (c->tune.np_nt) PHJ_NP_PROBE(HKV, 4, 1); else PHJ_NP_PROBE(HKV, 4, 0); \
         }                                                                        \
     } while (0)
-        if (p->hash == PHJ_HASH_MURMUR3)
+        if (marks) {
+            const uint32_t mg = static_cast<uint32_t>(std::min<uint64_t>((S.n + kBlock - 1) / kBlock, 8192));
+            if (p->hash == PHJ_HASH_MURMUR3)
+                hipLaunchKernelGGL((k_np_probe_mark<kMurmur3>), dim3(mg), dim3(kBlock), 0, c->ks, S_rel, S.n, tab, g,
+                                   p->hash_seed, marks, cnt);
+            else
+                hipLaunchKernelGGL((k_np_probe_mark<kXXH3>), dim3(mg), dim3(kBlock), 0, c->ks, S_rel, S.n, tab, g,
+                                   p->hash_seed, marks, cnt);
+        } else if (p->hash == PHJ_HASH_MURMUR3)
             PHJ_NP_PROBE_H(kMurmur3);
         else
             PHJ_NP_PROBE_H(kXXH3);
@@ -1197,6 +1210,89 @@ void drop_relation(phj_ctx* c, int side) {
 uint64_t partition_bytes(const Plan& pl, uint64_t n) {
     // hist (16 B AoS read) + scatter (16 read + 16 write); pass 2: hist 8 + scatter 32
     return n * (16 + 32) + (pl.npass == 2 ? n * (8 + 32) : 0);
+}
+
+// Rows of a marked probe (phj_mat.h): block counts, exclusive scan, write.
+int mat_compact(phj_ctx* c, uint64_t nS, const longlong2* s_aos, const int64_t* sk, const int64_t* sp,
+                const int64_t* rpay) {
+    const uint32_t nblk = static_cast<uint32_t>((nS + kMatBlock - 1) / kMatBlock);
+    PHJ_TRY(ensure(c, c->mat_cnt, (static_cast<size_t>(nblk) + 1) * 4));
+    PHJ_TRY(ensure(c, c->mat_rows, std::max<uint64_t>(1, nS) * sizeof(JoinedRow)));
+    auto* cnt = static_cast<uint32_t*>(c->mat_cnt.p);
+    const auto* mark = static_cast<const uint32_t*>(c->mat_mark.p);
+    PHJ_TRY(timer_begin(c, "mat.write", nS * 20 + static_cast<uint64_t>(nS) * 4));
+    PHJ_HIP(c, hipMemsetAsync(cnt, 0, (static_cast<size_t>(nblk) + 1) * 4, c->ks));
+    if (nblk) {
+        hipLaunchKernelGGL(k_mat_count, dim3(nblk), dim3(kBlock), 0, c->ks, mark, nS, cnt);
+        PHJ_LAUNCHED(c, "k_mat_count");
+    }
+    PHJ_TRY(scan_u32(c, cnt, nblk + 1, 1, nblk + 1));
+    if (nblk) {
+        hipLaunchKernelGGL(k_mat_write, dim3(nblk), dim3(kBlock), 0, c->ks, mark, nS, s_aos, sk, sp, rpay, cnt,
+                           static_cast<JoinedRow*>(c->mat_rows.p));
+        PHJ_LAUNCHED(c, "k_mat_write");
+    }
+    return timer_end(c);
+}
+
+int join_radix_mark(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
+    Plan pl;
+    PHJ_TRY(make_plan(c, p, pl));
+    SideState& R = c->side[PHJ_SIDE_BUILD];
+    SideState& S = c->side[PHJ_SIDE_PROBE];
+    const uint32_t requested = pl.Ppad;
+    refine_plan(c, pl, R.n);
+    const uint32_t P = pl.Ppad;
+    if (!c->tune.fused || (R.n + P - 1) / P * 3 > static_cast<uint64_t>(kFusedTcap) * 2)
+        return set_err(c, PHJ_ERR_INVALID, "materialised radix join needs the fused LDS join (PHJ_FUSED, PHJ_SUBPART)");
+    hipEvent_t t0, t1, p1;
+    PHJ_TRY(mark(c, &t0));
+    PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, pl));
+    PHJ_TRY(partition_side(c, PHJ_SIDE_BUILD, pl));
+    PHJ_TRY(mark(c, &t1));
+    const uint64_t nS = S.view.n;
+    const size_t nslots = nS / kFusedChunk + P + 1;
+    PHJ_TRY(ensure(c, c->fitems, nslots * sizeof(FusedItem)));
+    PHJ_TRY(ensure(c, c->count, 16));
+    PHJ_TRY(ensure(c, c->mat_mark, std::max<uint64_t>(1, nS) * 4));
+    PHJ_HIP(c, hipMemsetAsync(c->count.p, 0, 8, c->ks));
+    PHJ_HIP(c, hipMemsetAsync(c->mat_mark.p, 0xff, std::max<uint64_t>(1, nS) * 4, c->ks));
+    PHJ_TRY(timer_begin(c, "mat.join", R.n * 8 + nS * 12));
+    hipLaunchKernelGGL(k_fused_items, dim3((P + kWaves - 1) / kWaves), dim3(kBlock), 0, c->ks, S.view.bounds, P,
+                       static_cast<FusedItem*>(c->fitems.p));
+    PHJ_LAUNCHED(c, "k_fused_items");
+    FusedArgs fa{};
+    fa.L.nseg = 1;
+    fa.L.P = P;
+    fa.L.seg[0].keys = R.view.keys;
+    fa.L.seg[0].pays = R.view.payloads;
+    fa.L.seg[0].bounds = R.view.bounds;
+    fa.skeys = S.view.keys;
+    fa.sbounds = S.view.bounds;
+    fa.items = static_cast<const FusedItem*>(c->fitems.p);
+    fa.nitems = static_cast<uint32_t>(nslots - 1);
+    fa.count = static_cast<unsigned long long*>(c->count.p);
+    fa.seed = pl.seed;
+    const uint32_t grid = static_cast<uint32_t>(
+        std::max<size_t>(1, std::min<size_t>((nslots + kWaves - 1) / kWaves, static_cast<size_t>(4) * c->num_cus)));
+    auto* mk = static_cast<uint32_t*>(c->mat_mark.p);
+    if (pl.hk == kMurmur3)
+        hipLaunchKernelGGL(k_join_fused_mark<kMurmur3>, dim3(grid), dim3(kBlock), 0, c->ks, fa, mk);
+    else
+        hipLaunchKernelGGL(k_join_fused_mark<kXXH3>, dim3(grid), dim3(kBlock), 0, c->ks, fa, mk);
+    PHJ_LAUNCHED(c, "k_join_fused_mark");
+    PHJ_TRY(timer_end(c));
+    PHJ_TRY(mat_compact(c, nS, nullptr, S.view.keys, S.view.payloads, R.view.payloads));
+    PHJ_TRY(mark(c, &p1));
+    uint64_t m = 0;
+    PHJ_TRY(get_count(c, &m));
+    r->matches = m;
+    r->partition_ms = elapsed(c, t0, t1);
+    r->probe_ms = elapsed(c, t1, p1);
+    r->total_ms = elapsed(c, t0, p1);
+    r->num_partitions = requested;
+    r->algorithmic_bytes = partition_bytes(pl, R.n) + partition_bytes(pl, S.n) + R.n * 8 + nS * 12 + m * 24;
+    return fill_timers(c, r);
 }
 
 }  // namespace
@@ -1281,7 +1377,7 @@ void phj_ctx_destroy(phj_ctx* c) {
             free_buf(*b);
     }
     for (DevBuf* b : {&c->scan_partials, &c->prep, &c->tkeys, &c->tpays, &c->toffs, &c->gcursor, &c->items, &c->biglist,
-                      &c->count, &c->np_tab, &c->np_pays, &c->np_ovf, &c->np_ovfb, &c->np_ovfn, &c->fitems, &c->split})
+                      &c->count, &c->np_tab, &c->np_pays, &c->np_ovf, &c->np_ovfb, &c->np_ovfn, &c->fitems, &c->split, &c->mat_mark, &c->mat_cnt, &c->mat_rows})
         free_buf(*b);
     for (hipEvent_t e : c->evpool) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->stream);
@@ -1585,6 +1681,57 @@ int phj_partitioned_download(phj_ctx* c, const phj_partitioned* v, int64_t* keys
         return at.type == hipMemoryTypeDevice;
     };
     if (!(on_device(keys) && on_device(payloads) && on_device(bounds))) PHJ_HIP(c, hipStreamSynchronize(c->ks));
+    return PHJ_OK;
+}
+
+static_assert(sizeof(phj_joined) == 24 && sizeof(JoinedRow) == sizeof(phj_joined), "JoinedTuple layout");
+
+int phj_join_materialize(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
+    if (!c || !r) return PHJ_ERR_INVALID;
+    (void)hipGetLastError();
+    if (!p) return set_err(c, PHJ_ERR_INVALID, "null params");
+    PHJ_HIP(c, hipSetDevice(c->device));
+    std::memset(r, 0, sizeof(*r));
+    reset_timers(c);
+    c->mat_n = 0;
+    if (p->algo == PHJ_ALGO_NO_PARTITIONING) {
+        SideState& S = c->side[PHJ_SIDE_PROBE];
+        if (S.n >= (1ull << 32)) return set_err(c, PHJ_ERR_RANGE, "probe side above 2^32 tuples");
+        PHJ_TRY(ensure(c, c->mat_mark, std::max<uint64_t>(1, S.n) * 4));
+        PHJ_TRY(join_nopart(c, p, r, static_cast<uint32_t*>(c->mat_mark.p)));
+        hipEvent_t e0, e1;
+        PHJ_TRY(mark(c, &e0));
+        PHJ_TRY(mat_compact(c, S.n, reinterpret_cast<const longlong2*>(S.rel), nullptr, nullptr,
+                            static_cast<const int64_t*>(c->np_pays.p)));
+        PHJ_TRY(mark(c, &e1));
+        PHJ_HIP(c, hipStreamSynchronize(c->ks));
+        r->probe_ms += elapsed(c, e0, e1);
+        r->total_ms += elapsed(c, e0, e1);
+        r->algorithmic_bytes += r->matches * 24;
+        PHJ_TRY(fill_timers(c, r));
+    } else if (p->algo == PHJ_ALGO_RADIX) {
+        PHJ_TRY(join_radix_mark(c, p, r));
+    } else {
+        return set_err(c, PHJ_ERR_INVALID, "Unrecognized join algorithm");
+    }
+    c->mat_n = r->matches;
+    return PHJ_OK;
+}
+
+const phj_joined* phj_joined_rows(phj_ctx* c, uint64_t* n) {
+    if (!c) return nullptr;
+    if (n) *n = c->mat_n;
+    return static_cast<const phj_joined*>(c->mat_rows.p);
+}
+
+int phj_joined_download(phj_ctx* c, phj_joined* host, uint64_t n) {
+    if (!c) return PHJ_ERR_INVALID;
+    if (n > c->mat_n) return set_err(c, PHJ_ERR_RANGE, "more rows requested than the last materialised join made");
+    if (n == 0) return PHJ_OK;
+    if (!host) return set_err(c, PHJ_ERR_INVALID, "null destination");
+    PHJ_HIP(c, hipSetDevice(c->device));
+    PHJ_HIP(c, hipMemcpyAsync(host, c->mat_rows.p, n * sizeof(phj_joined), hipMemcpyDeviceToHost, c->stream));
+    PHJ_HIP(c, hipStreamSynchronize(c->stream));
     return PHJ_OK;
 }
 
