@@ -70,6 +70,7 @@ struct GpuConfiguration {
     uint64_t Seed = 20240601;        // data generator seed
     bool GenerateOnDevice = false;
     double TableRatio = 0.0;         // NoPartitioning slots per tuple (0: default)
+    bool Materialize = false;        // --materialize on: Run() returns the joined rows (phj_join_materialize)
 };
 
 struct Configuration {

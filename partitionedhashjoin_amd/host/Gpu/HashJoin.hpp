@@ -9,7 +9,9 @@
 // phj_ctx: device, stream, workspace). Run() hands &(*table)[0] / GetSize()
 // to the C ABI (include/phj.h), runs partition / build / probe on the MI355X,
 // drives the timer with the device-measured phase times and, like the
-// reference, returns an empty Table<JoinedTuple> (counts only); the matched
+// reference, returns an empty Table<JoinedTuple> (counts only) unless
+// GpuConfiguration::Materialize asks for the rows (phj_join_materialize:
+// one JoinedTuple per matching probe tuple, copied back); the matched
 // count is logged ("Joined N tuples", RadixCluster/HashJoin.hpp:320-321),
 // added to the results as `matches`, and kept in GetNumberOfJoinedTuples().
 // C ABI errors surface as std::runtime_error / std::invalid_argument, which the
@@ -63,6 +65,21 @@ namespace internal {
 
 inline std::chrono::nanoseconds ms_to_ns(double ms) {
     return std::chrono::nanoseconds(static_cast<int64_t>(std::llround(ms * 1e6)));
+}
+
+// phj_join or, with rows requested, phj_join_materialize + the rows copied
+// into the returned table
+inline std::shared_ptr<Common::Table<Common::JoinedTuple>> join(Device& dev, const phj_join_params& p,
+                                                                phj_join_result& r, bool materialize) {
+    if (!materialize) {
+        dev.Check(phj_join(dev.Get(), &p, &r));
+        return std::make_shared<Common::Table<Common::JoinedTuple>>(Common::generate_uuid());
+    }
+    static_assert(sizeof(Common::JoinedTuple) == sizeof(phj_joined), "JoinedTuple layout");
+    dev.Check(phj_join_materialize(dev.Get(), &p, &r));
+    auto out = std::make_shared<Common::Table<Common::JoinedTuple>>(r.matches, Common::generate_uuid());
+    dev.Check(phj_joined_download(dev.Get(), reinterpret_cast<phj_joined*>(out->Data()), r.matches));
+    return out;
 }
 
 inline void add_device_results(Common::IHashJoinTimer& timer, const phj_join_result& r) {
@@ -121,7 +138,7 @@ class HashJoiner {
         // workspace allocation stays outside the timed phases, as the reference's
         // partitioned-table allocation does (RadixCluster/HashJoin.hpp:195-198)
         m_device->Check(phj_prepare(m_device->Get(), &p));
-        m_device->Check(phj_join(m_device->Get(), &p, &r));
+        auto joined = internal::join(*m_device, p, r, m_gpu.Materialize);
         // partition: wall of both partition pipelines; build / probe: device phases
         timer->SetPartitionPhaseDuration(internal::ms_to_ns(r.partition_ms));
         timer->SetBuildPhaseDuration(internal::ms_to_ns(r.build_ms));
@@ -132,7 +149,7 @@ class HashJoiner {
         m_last = r;
         LOG(m_logger, Common::debug) << "Joined  " << r.matches << " tuples";
         LOG(m_logger, Common::debug) << "Finished hash partitioning.";
-        return std::make_shared<Common::Table<Common::JoinedTuple>>(Common::generate_uuid());
+        return joined;
     }
 
     uint64_t GetNumberOfJoinedTuples() const { return m_joined; }
@@ -188,7 +205,7 @@ class HashJoiner {
         // workspace allocation stays outside the timed phases, as the reference's
         // partitioned-table allocation does (RadixCluster/HashJoin.hpp:195-198)
         m_device->Check(phj_prepare(m_device->Get(), &p));
-        m_device->Check(phj_join(m_device->Get(), &p, &r));
+        auto joined = internal::join(*m_device, p, r, m_gpu.Materialize);
         timer->SetBuildPhaseDuration(internal::ms_to_ns(r.build_ms));
         // the reference's probe figure runs from the build start (Results.hpp:202)
         timer->SetProbePhaseDuration(internal::ms_to_ns(r.build_ms + r.probe_ms));
@@ -199,7 +216,7 @@ class HashJoiner {
         m_last = r;
         LOG(m_logger, Common::debug) << "Joined " << r.matches << " tuples.";
         LOG(m_logger, Common::debug) << "Finished hash partitioning.";
-        return std::make_shared<Common::Table<Common::JoinedTuple>>(Common::generate_uuid());
+        return joined;
     }
 
     uint64_t GetNumberOfJoinedTuples() const { return m_joined; }

@@ -60,7 +60,20 @@ const char* kHelp =
     "  --seed arg (=20240601)              Seed of the relation generators.\n"
     "  --hash-seed arg                     Hasher seed (default: random).\n"
     "  --generate arg (=host)              host | device.\n"
-    "  --table-ratio arg                   No-partitioning table slots per build tuple.\n";
+    "  --table-ratio arg                   No-partitioning table slots per build tuple.\n"
+    "  --materialize arg (=off)            on | off: return the joined rows (Table<JoinedTuple>).\n";
+
+// --materialize on: the rows Run() returned (count, and a checksum of their
+// columns so a caller can compare runs without the rows themselves)
+void report_rows(const Common::Table<Common::JoinedTuple>& rows, Common::IHashJoinTimer& timer, bool materialize) {
+    if (!materialize) return;
+    uint64_t sum = 0;
+    for (size_t i = 0; i < rows.GetSize(); i++)
+        sum += static_cast<uint64_t>(rows[i].id) * 3 + static_cast<uint64_t>(rows[i].payloadA) * 5 +
+               static_cast<uint64_t>(rows[i].payloadB) * 7;
+    timer.AddResult("rows", std::to_string(rows.GetSize()));
+    timer.AddResult("rows_checksum", std::to_string(sum));
+}
 
 template <typename T>
 T parse_number(const std::string& name, const std::string& v) {
@@ -77,7 +90,8 @@ Common::Configuration parseArguments(int argc, char** argv) {
         {"-u", "unit"}, {"-o", "output"}, {"-f", "filename"}, {"-p", "partitions"}, {"-h", "help"}};
     static const std::set<std::string> known = {"help", "primary", "secondary", "skew", "log", "join", "format",
                                                 "unit", "output", "filename", "partitions", "device", "hash",
-                                                "radix-bits", "seed", "hash-seed", "generate", "table-ratio"};
+                                                "radix-bits", "seed", "hash-seed", "generate", "table-ratio",
+                                                "materialize"};
     Common::Configuration c{};
     c.OutputFormatConfig.TimeUnit = "ms";
     c.OutputConfig.File.Name = "hashjoin.txt";
@@ -124,6 +138,11 @@ Common::Configuration parseArguments(int argc, char** argv) {
         if (vm.count("partitions"))
             c.RadixClusteringConfig.NumberOfPartitions = parse_number<size_t>("partitions", vm["partitions"]);
         if (vm.count("device")) c.GpuConfig.Device = parse_number<int>("device", vm["device"]);
+        if (vm.count("materialize")) {
+            if (vm["materialize"] == "on") c.GpuConfig.Materialize = true;
+            else if (vm["materialize"] != "off")
+                throw std::invalid_argument("the argument ('" + vm["materialize"] + "') for option '--materialize' is invalid");
+        }
         c.GpuConfig.Hash = PHJ_HASH_XXH3;
         if (vm.count("hash")) {
             if (vm["hash"] == "xxh3" || vm["hash"] == "xxhash") c.GpuConfig.Hash = PHJ_HASH_XXH3;
@@ -234,8 +253,8 @@ int main(int argc, char** argv) {
                                                                                   hasher);
                     Gpu::NoPartitioning::HashJoiner<decltype(factory)> joiner(configuration.NoPartitioningConfig, device,
                                                                              factory, configuration.GpuConfig);
-                    if (tableA) joiner.Run(tableA, tableB, timer);
-                    else joiner.RunResident(timer);
+                    auto joined = tableA ? joiner.Run(tableA, tableB, timer) : joiner.RunResident(timer);
+                    report_rows(*joined, *timer, configuration.GpuConfig.Materialize);
                 };
                 if (configuration.GpuConfig.Hash == PHJ_HASH_MURMUR3) run(Common::Murmur3Hasher(hashSeed));
                 else run(Common::XXHasher(hashSeed));
@@ -262,8 +281,8 @@ int main(int argc, char** argv) {
                                                                                   hasher);
                     Gpu::RadixClustering::HashJoiner<decltype(factory), H> joiner(
                         configuration.RadixClusteringConfig, device, hasher, factory, configuration.GpuConfig);
-                    if (tableA) joiner.Run(tableA, tableB, timer);
-                    else joiner.RunResident(timer);
+                    auto joined = tableA ? joiner.Run(tableA, tableB, timer) : joiner.RunResident(timer);
+                    report_rows(*joined, *timer, configuration.GpuConfig.Materialize);
                 };
                 if (configuration.GpuConfig.Hash == PHJ_HASH_MURMUR3) run(Common::Murmur3Hasher(hashSeed));
                 else run(Common::XXHasher(hashSeed));

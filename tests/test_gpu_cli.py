@@ -4,6 +4,8 @@ import json
 import os
 import subprocess
 
+import numpy as np
+
 import pytest
 
 from oracle import oracle as O
@@ -55,3 +57,18 @@ def test_cli_primary_one_terminates_like_reference(tmp_path):
                         "-f", str(tmp_path / "x.txt")], capture_output=True, text=True, timeout=120)
     assert r.returncode != 0
     assert "Range for Zipf generation is incorrectly specified" in r.stderr
+
+
+@pytest.mark.parametrize("join", ["radix-partitioning", "no-partitioning"])
+def test_cli_materialize_rows(tmp_path, join):
+    # --materialize on: Run() returns one JoinedTuple per probe tuple; Sequential
+    # R has unique keys, so payloadA = id - 1 and the row checksum is exact
+    nR, nS, seed = 100_000, 1_500_000, 77
+    res, _ = run_cli(tmp_path, "--primary", str(nR), "--secondary", str(nS), "--seed", str(seed),
+                     "--join", join, "--materialize", "on")
+    R, S = O.generate_tables(nR, nS, 1.05, seed)
+    ids = S[:, 0].astype(np.uint64)
+    want = int((ids * np.uint64(3) + (ids - np.uint64(1)) * np.uint64(5)
+                + S[:, 1].astype(np.uint64) * np.uint64(7)).sum(dtype=np.uint64))
+    assert int(res["device"]["rows"]) == int(res["device"]["matches"]) == nS
+    assert int(res["device"]["rows_checksum"]) == want
