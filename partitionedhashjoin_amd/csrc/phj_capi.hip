@@ -1163,7 +1163,7 @@ int join_nopart(phj_ctx* c, const phj_join_params* p, phj_join_result* r, uint32
         }                                                                        \
     } while (0)
         if (marks) {
-            const uint32_t mg = static_cast<uint32_t>(std::min<uint64_t>((S.n + kBlock - 1) / kBlock, 8192));
+            const uint32_t mg = static_cast<uint32_t>(std::min<uint64_t>((S.n + 4 * kBlock - 1) / (4 * kBlock), 8192));
             if (p->hash == PHJ_HASH_MURMUR3)
                 hipLaunchKernelGGL((k_np_probe_mark<kMurmur3>), dim3(mg), dim3(kBlock), 0, c->ks, S_rel, S.n, tab, g,
                                    p->hash_seed, marks, cnt);

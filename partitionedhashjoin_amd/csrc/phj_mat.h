@@ -52,14 +52,42 @@ __global__ __launch_bounds__(kBlock) void k_np_probe_mark(const longlong2* S, ui
                                                           NPHome g, uint64_t seed, uint32_t* match,
                                                           unsigned long long* count) {
     __shared__ uint32_t red[kWaves];
+    constexpr int IT = 4;   // as k_np_probe: every home bucket of a round requested before any compare
     uint32_t hits = 0;
-    for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; i < nS;
-         i += static_cast<uint64_t>(gridDim.x) * kBlock) {
-        const int64_t key = __builtin_nontemporal_load(&S[i].x);
-        const uint32_t b = np_home_r(hash64<HK>(static_cast<uint64_t>(key), seed), g);
-        const uint32_t m = np_lookup_slot(tab, g.nb, b, key);
-        match[i] = m;
-        hits += m != kNoMatch;
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kBlock * IT;
+    for (uint64_t base = static_cast<uint64_t>(blockIdx.x) * kBlock * IT; base < nS; base += stride) {
+        int64_t k[IT];
+        uint32_t b[IT];
+        longlong2 q[IT][4];
+#pragma unroll
+        for (int j = 0; j < IT; j++) {
+            const uint64_t i = base + static_cast<uint64_t>(j) * kBlock + threadIdx.x;
+            k[j] = i < nS ? __builtin_nontemporal_load(&S[i].x) : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < IT; j++) {
+            b[j] = np_home_r(hash64<HK>(static_cast<uint64_t>(k[j]), seed), g);
+            const longlong2* bp = reinterpret_cast<const longlong2*>(tab + b[j]);
+#pragma unroll
+            for (int w = 0; w < 4; w++) q[j][w] = bp[w];
+        }
+#pragma unroll
+        for (int j = 0; j < IT; j++) {
+            const uint64_t i = base + static_cast<uint64_t>(j) * kBlock + threadIdx.x;
+            if (i >= nS) continue;
+            const int64_t key = k[j];
+            const uint32_t fill = static_cast<uint32_t>(q[j][3].y);
+            const uint32_t c = fill < kNPSlots ? fill : kNPSlots;
+            const int64_t ks[kNPSlots] = {q[j][0].x, q[j][0].y, q[j][1].x, q[j][1].y, q[j][2].x, q[j][2].y, q[j][3].x};
+            uint32_t m = kNoMatch;
+#pragma unroll
+            for (int s = kNPSlots - 1; s >= 0; s--)   // the first equal slot wins
+                if (static_cast<uint32_t>(s) < c && ks[s] == key) m = b[j] * kNPSlots + s;
+            if (m == kNoMatch && fill >= kNPSlots)   // full home bucket: walk on (rare)
+                m = np_lookup_slot(tab, g.nb, b[j] + 1 == g.nb ? 0 : b[j] + 1, key);
+            match[i] = m;
+            hits += m != kNoMatch;
+        }
     }
     uint32_t x = hits;
 #pragma unroll
