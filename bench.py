@@ -149,7 +149,7 @@ def main():
     import torch
     import torch.distributed as dist
     import partitionedhashjoin_amd as phj
-    from partitionedhashjoin_amd.distributed import HipShardEngine, distributed_join
+    from partitionedhashjoin_amd.distributed import HipShardEngine, distributed_join, distributed_join_nopart
 
     exchange = world > 1 or args.exchange
     if exchange:
@@ -161,8 +161,6 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     nR, nS = args.primary, args.secondary
     params, alpha, workload = config_params(phj, args.config)
-    if exchange and params.algo != phj.ALGO_RADIX:
-        raise SystemExit("multi-GPU bench runs the radix configs (c2, c5)")
     engine = HipShardEngine(local_rank)
     engine.generate(nR, nS, alpha, GEN_SEED, rank, world)
     torch.cuda.synchronize()
@@ -176,6 +174,8 @@ def main():
             # per-kernel timers accumulate on the device; read once after the timed loop
             return distributed_join(engine, params, nR, nS, rank, world, dist if exchange else None,
                                     timers=False, force_exchange=exchange)
+        if exchange:   # NoPartitioning over shards: replicated build side (all-gather of R)
+            return distributed_join_nopart(engine, params, nR, nS, rank, world, dist, force_exchange=True)
         r = engine.ctx.join(params)
 
         class _R:

@@ -171,6 +171,30 @@ class HipShardEngine:
     def count_in_range(self, side, lo, hi):
         return (self.ctx_r if side == 0 else self.ctx).count_in_range(side, lo, hi)
 
+    def build_shard(self):
+        """This rank's build shard as an (n, 2) int64 device tensor (a view of
+        the R context's relation, no copy)."""
+        ptr, n = self.ctx_r.relation_ptr(0)
+
+        class _Cai:
+            __cuda_array_interface__ = {"shape": (int(n), 2), "typestr": "<i8", "data": (int(ptr or 0), False),
+                                        "version": 2, "strides": None}
+        if n == 0:
+            return self.torch.zeros((0, 2), dtype=self.torch.int64, device=self.device)
+        return self.torch.as_tensor(_Cai(), device=self.device)
+
+    def join_nopart_replicated(self, params, full_r):
+        """NoPartitioning join of the local S shard against the whole build
+        relation `full_r` ((|R|, 2) device tensor); returns the local count
+        as a device tensor."""
+        self.torch.cuda.current_stream().synchronize()
+        self.ctx.bind_device(0, full_r.data_ptr(), full_r.shape[0], keepalive=full_r)
+        r = self.ctx.join(params)
+        m = r.matches
+        self.last_timers = r.timers()
+        self.share_build()
+        return self.torch.tensor([m], dtype=self.torch.int64, device=self.device)
+
 
 class _null:
     def __enter__(self):
@@ -254,6 +278,36 @@ def distributed_join(engine, params, nR: int, nS: int, rank: int, world: int, di
     total = int(cnt.item())
     local = int(local.item())
     return DistResult(matches=total, local_matches=local, timers=engine.timers() if timers else [])
+
+
+def distributed_join_nopart(engine, params, nR: int, nS: int, rank: int, world: int, dist=None,
+                            force_exchange: bool = False):
+    """NoPartitioning over range-sharded relations: the build
+    relation is replicated with one all-gather of the R shards (padded to the
+    largest shard, then compacted), every rank builds the global table
+    locally and probes its own S shard, and the counts are summed with an
+    all-reduce. S never leaves its GPU. force_exchange runs the collectives
+    on a world of one (the one-GPU test of this path)."""
+    torch = engine.torch
+    shard = engine.build_shard()
+    if world == 1 and not force_exchange:
+        cnt = engine.join_nopart_replicated(params, shard)
+        total = local = int(cnt.item())
+        return DistResult(matches=total, local_matches=local, timers=getattr(engine, "last_timers", []))
+    sizes = [hi - lo for lo, hi in (shard_range(nR, r, world) for r in range(world))]
+    maxn = max(sizes)
+    send = shard.new_zeros((maxn, 2))
+    send[:shard.shape[0]].copy_(shard)
+    recv = shard.new_empty((world * maxn, 2))
+    work = _all_gather(dist, recv, send)
+    if work is not None:
+        work.wait()
+    full = torch.cat([recv[g * maxn:g * maxn + sizes[g]] for g in range(world)])
+    cnt = engine.join_nopart_replicated(params, full)
+    local = cnt.clone()
+    _all_reduce(dist, cnt)
+    return DistResult(matches=int(cnt.item()), local_matches=int(local.item()),
+                      timers=getattr(engine, "last_timers", []))
 
 
 def unpack_segments_numpy(recv, sizes, maxn, P):

@@ -14,7 +14,7 @@ import torch.multiprocessing as mp
 
 import partitionedhashjoin_amd as phj
 from oracle import oracle as O
-from partitionedhashjoin_amd.distributed import (distributed_join, max_shard, pack_layout, shard_range,
+from partitionedhashjoin_amd.distributed import (distributed_join, distributed_join_nopart, max_shard, pack_layout, shard_range,
                                                  unpack_segments_numpy)
 
 
@@ -75,6 +75,13 @@ class OracleShardEngine:
     def timers(self):
         return []
 
+    def build_shard(self):
+        return torch.from_numpy(np.ascontiguousarray(self.rel[0]))
+
+    def join_nopart_replicated(self, params, full_r):
+        R = full_r.numpy()
+        return torch.tensor([O.join_nopart(R, self.rel[1]).matches], dtype=torch.int64)
+
     def build_ready(self):
         pass
 
@@ -96,6 +103,21 @@ def _worker(rank, world, port, nR, nS, alpha, seed, bits, nparts, out):
         eng = OracleShardEngine(R[rlo:rhi], S[slo:shi])
         p = phj.radix_params(bits, num_partitions=nparts, hash=phj.HASH_MURMUR3, seed=1234)
         res = distributed_join(eng, p, nR, nS, rank, world, dist)
+        out[rank] = (res.matches, res.local_matches)
+    finally:
+        dist.destroy_process_group()
+
+
+def _np_worker(rank, world, port, nR, nS, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        R, S = _tables(nR, nS, 1.25, 9)
+        rlo, rhi = shard_range(nR, rank, world)
+        slo, shi = shard_range(nS, rank, world)
+        eng = OracleShardEngine(R[rlo:rhi], S[slo:shi])
+        res = distributed_join_nopart(eng, phj.nopart_params(), nR, nS, rank, world, dist)
         out[rank] = (res.matches, res.local_matches)
     finally:
         dist.destroy_process_group()
@@ -134,3 +156,15 @@ def test_single_rank_path():
     eng = OracleShardEngine(R, S)
     res = distributed_join(eng, phj.radix_params((3, 3)), 5000, 40_000, 0, 1, None)
     assert res.matches == O.semijoin_count(R, S)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_distributed_nopart_gloo(world):
+    nR, nS = 20_001, 150_007
+    R, S = _tables(nR, nS, 1.25, 9)
+    expect = O.semijoin_count(R, S)
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_np_worker, args=(world, _free_port(), nR, nS, out), nprocs=world)
+    assert {out[r][0] for r in range(world)} == {expect}
+    assert sum(out[r][1] for r in range(world)) == expect

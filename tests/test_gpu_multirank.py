@@ -105,3 +105,44 @@ def test_rccl_exchange_branch_world_one():
     got, expect = out[0]
     assert 0 < expect < nS
     assert got == [expect] * 3
+
+
+def _np_worker(rank, world, port, backend, nR, nS, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    if backend == "nccl":
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import partitionedhashjoin_amd as phj
+        from partitionedhashjoin_amd.distributed import HipShardEngine, distributed_join_nopart, shard_range
+        eng = HipShardEngine(0)
+        off = nR // 3
+        rlo, rhi = shard_range(nR, rank, world)
+        slo, shi = shard_range(nS, rank, world)
+        eng.ctx_r.generate_sequential(0, rhi - rlo, 1 + off, rlo)
+        eng.ctx.generate_zipf(1, shi - slo, 1.25, 1, nR, 31, slo)
+        eng.share_build()
+        expect_local = eng.ctx.count_in_range(1, 1 + off, nR)
+        for _ in range(2):
+            res = distributed_join_nopart(eng, phj.nopart_params(), nR, nS, rank, world, dist,
+                                          force_exchange=True)
+        out[rank] = (res.matches, expect_local, res.local_matches)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("backend,world", [("gloo", 2), ("gloo", 3), ("nccl", 1)])
+def test_nopart_replicated_build_multirank(backend, world):
+    """NoPartitioning over range shards: all-gather of the R shards, global
+    table per rank, local S probe, count all-reduce."""
+    nR, nS = 300_001, 4_000_003
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_np_worker, args=(world, _free_port(), backend, nR, nS, out), nprocs=world)
+    expect = sum(out[r][1] for r in range(world))
+    assert 0 < expect < nS
+    assert {out[r][0] for r in range(world)} == {expect}
+    assert all(out[r][2] == out[r][1] for r in range(world))
