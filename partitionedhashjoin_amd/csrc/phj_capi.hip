@@ -58,7 +58,7 @@ struct Tuning {
     int ptab = 1;         // partitioned bucket tables: 0 never, 1 very large partitions, 2 always
     bool subpart = true;  // phj_join: sub-partition large partitions for the fused join
     bool timers = true;   // per-kernel timer events (phase events are always recorded)
-    int fused_kpl = 4;    // fused join: S keys per lane per probe round (4 or 8)
+    int fused_kpl = 4;    // fused join: S keys per lane per probe round (2, 4 or 8)
     bool p1_chunk = true; // 2-pass, unordered partitions: chunked pass 1 without a histogram pass
     int p1_slots = 0;     // chunked pass 1: workgroups per shard (0 = fill the chip once, -1 = one per tile)
     int p1_tps = static_cast<int>(kTilesPerShard);   // chunked pass 1: tiles per shard (sets the shard count)
@@ -853,7 +853,10 @@ int build_and_probe(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned*
         fa.cycles = static_cast<unsigned long long*>(c->split.p);
         fa.seed = pl.seed;
         const void* kfn;
-        if (c->tune.fused_kpl == 8)
+        if (c->tune.fused_kpl == 2)
+            kfn = pl.hk == kMurmur3 ? reinterpret_cast<const void*>(&k_join_fused<kMurmur3, 2, kFusedTcap>)
+                                    : reinterpret_cast<const void*>(&k_join_fused<kXXH3, 2, kFusedTcap>);
+        else if (c->tune.fused_kpl == 8)
             kfn = pl.hk == kMurmur3 ? reinterpret_cast<const void*>(&k_join_fused<kMurmur3, 8, kFusedTcap>)
                                     : reinterpret_cast<const void*>(&k_join_fused<kXXH3, 8, kFusedTcap>);
         else
@@ -1339,7 +1342,10 @@ int phj_ctx_create(int device, phj_ctx** out) {
     c->tune.ptab = env_int("PHJ_PTAB", 1);
     c->tune.subpart = env_int("PHJ_SUBPART", 1) != 0;
     c->tune.timers = env_int("PHJ_TIMERS", 1) != 0;
-    c->tune.fused_kpl = env_int("PHJ_FUSED_KPL", 4) == 8 ? 8 : 4;
+    {
+        const int k = env_int("PHJ_FUSED_KPL", 4);
+        c->tune.fused_kpl = (k == 2 || k == 8) ? k : 4;
+    }
     c->tune.p1_chunk = env_int("PHJ_P1_CHUNK", 1) != 0;
     c->tune.np_nt = std::min(2, std::max(0, env_int("PHJ_NP_NT", 1)));
     c->tune.np_items = env_int("PHJ_NP_ITEMS", 4) == 8 ? 8 : 4;

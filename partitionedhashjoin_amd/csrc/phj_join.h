@@ -678,7 +678,7 @@ __device__ __forceinline__ void fused_load_s(const int64_t* skeys, uint32_t lo, 
 // 5 waves per SIMD at KPL = 4 (92 VGPRs, no spill): the S loads in flight
 // per CU, not the arithmetic, bound this kernel
 template <int HK, int KPL, int TCAP>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KPL <= 4 ? 5 : 3, 8))) void k_join_fused(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KPL <= 2 ? 6 : (KPL <= 4 ? 5 : 3), 8))) void k_join_fused(
     FusedArgs a) {
     constexpr int RPL = TCAP / 64;                 // build keys per lane per round
     constexpr int OCAP = TCAP / 2 + 1;             // bucket offsets (table_buckets(TCAP) + 1)
