@@ -51,6 +51,7 @@ struct Tuning {
     int probe_wave = 1;   // wave-per-item probe: 0 never, 1 small partitions (auto), 2 always
     int block = 512;      // threads per workgroup of the tile kernels (256, 512 or 1024; tile_shape)
     bool nt_store = false; // nontemporal scatter stores
+    int nt_load = 1;       // nontemporal tuple loads in the partition passes: 1 pass 1, 2 both
     bool dcol = true;     // 2-pass: pass 1 writes the pass-2 digit column
     unsigned ev_flags = hipEventDisableSystemFence;  // timer / ordering events
     bool fused = true;    // radix join: fused per-partition LDS build + probe when partitions are small
@@ -550,6 +551,9 @@ int launch_pass(phj_ctx* c, int hk, bool in_aos, bool out_aos, PassArgs a, uint3
         default: return set_err(c, PHJ_ERR_INVALID, "unsupported pass layout");     \
     }
     a.nt_store = c->tune.nt_store ? 1u : 0u;
+    // nontemporal tuple loads: 1 = pass 1 only (the relation itself), 2 = every pass
+    a.nt_load = (c->tune.nt_load == 2 || (c->tune.nt_load == 1 && prefix.size() >= 3 &&
+                                         prefix.compare(prefix.size() - 3, 3, ".p1") == 0)) ? 1u : 0u;
     if (sh.block == 256 && sh.tile == 2048) PHJ_PASS_CASES(256, 8)
     if (sh.block == 256 && sh.tile == 4096) PHJ_PASS_CASES(256, 16)
     if (sh.block == 512 && sh.tile == 2048) PHJ_PASS_CASES(512, 4)
@@ -1336,6 +1340,7 @@ int phj_ctx_create(int device, phj_ctx** out) {
     c->tune.probe_wave = env_int("PHJ_PROBE_WAVE", 1);
     c->tune.block = env_int("PHJ_BLOCK", 512);
     c->tune.nt_store = env_int("PHJ_NT", 0) != 0;
+    c->tune.nt_load = std::min(2, std::max(0, env_int("PHJ_NT_LOAD", 1)));
     c->tune.dcol = env_int("PHJ_DCOL", 1) != 0;
     c->tune.fused = env_int("PHJ_FUSED", 1) != 0;
     c->tune.onepass_max = std::max(1, env_int("PHJ_ONEPASS_MAX", 256));

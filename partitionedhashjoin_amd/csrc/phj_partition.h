@@ -104,6 +104,7 @@ struct PassArgs {
     uint32_t nbits;
     uint32_t xcd_remap;         // 1: give each XCD a contiguous run of tiles (grid % 8 == 0)
     uint32_t nt_store;          // 1: scatter stores bypass the caches' allocate (nontemporal)
+    uint32_t nt_load;           // 1: tuple loads are nontemporal (keep L2 for the scatter's partial lines)
     uint32_t dig_wide;          // digit column element: 0 = u8, 1 = u16
     void* out_dig;              // pass-1 scatter: writes the NEXT pass's digit per output slot
     const void* in_dig;         // pass-2 histogram: counts this column instead of hashing keys
@@ -237,6 +238,13 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* t
 template <bool AOS>
 __device__ __forceinline__ void load_tuple(const PassArgs& a, uint32_t idx, int64_t& k, int64_t& p) {
     if constexpr (AOS) {
+        if (a.nt_load) {
+            typedef long long v2i __attribute__((ext_vector_type(2)));
+            const v2i t = __builtin_nontemporal_load(reinterpret_cast<const v2i*>(a.in_keys) + idx);
+            k = t.x;
+            p = t.y;
+            return;
+        }
         const longlong2 t = reinterpret_cast<const longlong2*>(a.in_keys)[idx];
         k = t.x;
         p = t.y;
@@ -585,9 +593,17 @@ void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
         const uint32_t lo = t * T;
 #pragma unroll
         for (int i = 0; i < ITEMS; i++) {
-            const longlong2 v = rel[min(lo + wbase + i * 64 + lane, a.n - 1)];
-            key[i] = v.x;
-            pay[i] = v.y;
+            const uint32_t ix = min(lo + wbase + i * 64 + lane, a.n - 1);
+            if (a.nt_load) {
+                typedef long long v2i __attribute__((ext_vector_type(2)));
+                const v2i v = __builtin_nontemporal_load(reinterpret_cast<const v2i*>(rel) + ix);
+                key[i] = v.x;
+                pay[i] = v.y;
+            } else {
+                const longlong2 v = rel[ix];
+                key[i] = v.x;
+                pay[i] = v.y;
+            }
         }
     };
     load(tile);
