@@ -44,7 +44,7 @@ def parse():
     ap.add_argument("--primary", type=int, default=NR)
     ap.add_argument("--secondary", type=int, default=NS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, cpus) - 1")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: the core share - 1 (cpu_threads)")
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes")
     ap.add_argument("--exchange", action="store_true",
@@ -104,33 +104,87 @@ def pmc_traffic(args, verbose):
     return pmc.hbm_bytes(per)
 
 
+def host_cpu():
+    """The host's CPU model and the core share this process may use: nproc
+    (os.cpu_count: the whole machine), the affinity mask and the cgroup CPU
+    quota (a GPU box grants one GPU's share of a larger machine)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    nproc = os.cpu_count() or 1
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = nproc
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    return {"model": model, "nproc": nproc, "affinity": affinity, "cgroup_quota": quota}
+
+
+def cpu_threads(cpu):
+    """The reference sizes its pool hardware_concurrency() - 1 (src/main.cpp:235).
+    On a GPU box nproc counts the whole machine while one GPU's share is 16
+    cores (the pool's rule), so the pool is min(nproc, affinity, quota, 16) - 1."""
+    share = min(x for x in (cpu["nproc"], cpu["affinity"], cpu["cgroup_quota"] or 10**9, 16))
+    return max(1, share - 1)
+
+
 def cpu_baseline(ctx, nR, nS, threads, verbose):
-    """The oracle's restatement of RadixCluster -p 1024 (XXH3) on this host's cores,
-    over the same device-generated relations (copied back), once."""
+    """The oracle's restatement of the reference's three published CPU legs
+    (results/1.05/figure.dat cols 2, 3 and 8: NoPartitioning, RadixCluster
+    -p 32 and -p 1024, XXH3, LinearProbing 3-slot 1.25x) on this host's cores,
+    over the same device-generated relations (copied back), once each.
+    `value` is the best RadixCluster leg (-p 1024, the reference's best
+    published configuration); every leg is in `legs`."""
     from oracle import oracle as O
-    import numpy as np
     R = ctx.download(0)
     S = ctx.download(1)
-    res = O.join_radix(R, S, P=1024, radix=False, part_hash=O.HASH_XXH3, part_seed=1,
-                       table_hash=O.HASH_XXH3, table_seed=2, ratio=1.25, workers=threads)
-    # Run()'s wall from SetPartitioningPhaseBegin to the end of Join(): the
-    # partitioned copies are allocated before the timer, as in the reference
-    # (RadixCluster/HashJoin.hpp:195-198)
-    wall = res.wall_ms * 1e-3
+    cpu = host_cpu()
+    legs = {}
+    # RadixCluster: Run()'s wall from SetPartitioningPhaseBegin to the end of
+    # Join(); the partitioned copies are allocated before the timer, as in the
+    # reference (RadixCluster/HashJoin.hpp:195-198)
+    for P in (1024, 32):
+        res = O.join_radix(R, S, P=P, radix=False, part_hash=O.HASH_XXH3, part_seed=1,
+                           table_hash=O.HASH_XXH3, table_seed=2, ratio=1.25, workers=threads)
+        legs[f"radix_p{P}"] = {"ms": res.wall_ms, "partition_ms": res.partition_ms, "build_ms": res.build_ms,
+                               "probe_ms": res.probe_ms, "matches": int(res.matches),
+                               "tuples_per_s": (nR + nS) / (res.wall_ms * 1e-3)}
+    # NoPartitioning: the reference reports probe from the build start
+    # (Results.hpp:202), i.e. build + probe, the table allocation included
+    res = O.join_nopart(R, S, hash_kind=O.HASH_XXH3, seed=2, ratio=1.25, workers=threads)
+    legs["nopartitioning"] = {"ms": res.probe_ms, "build_ms": res.build_ms, "probe_ms": res.probe_ms,
+                              "matches": int(res.matches), "tuples_per_s": (nR + nS) / (res.probe_ms * 1e-3)}
     del R, S
     if verbose:
-        print(f"cpu baseline: {res.as_dict()}", file=sys.stderr)
+        print(f"cpu baseline: {legs} on {cpu}", file=sys.stderr)
+    best = legs["radix_p1024"]
+    desc = "; ".join(f"{k} {v['ms']:.0f} ms" for k, v in legs.items())
     return {
-        "value": (nR + nS) / wall,
+        "value": best["tuples_per_s"],
         "unit": "tuples/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"full {nR // 10**6}M⋈{nS // 10**6}M workload, 1 run of the oracle's "
-                  f"RadixCluster restatement (-p 1024, XXH3, LinearProbing 3-slot 1.25x) "
-                  f"with {threads} worker threads; wall {wall * 1e3:.0f} ms "
-                  f"(partition {res.partition_ms:.0f} / build {res.build_ms:.0f} / "
-                  f"probe {res.probe_ms:.0f} ms, reference phase semantics)",
-        "matches": int(res.matches),
+        "sample": f"full {nR // 10**6}M⋈{nS // 10**6}M workload (the bench's relations copied back), one run "
+                  f"per leg of the oracle's restatement of the reference's published CPU legs, XXH3, "
+                  f"LinearProbing 3-slot 1.25x, {threads} worker threads (hardware_concurrency()-1 over "
+                  f"this box's {min(16, cpu['affinity'])}-core share; nproc {cpu['nproc']}, {cpu['model']}): "
+                  f"{desc}; value = radix -p 1024 (reference phase semantics)",
+        "legs": legs,
+        "host": cpu,
+        "matches": {k: v["matches"] for k, v in legs.items()},
     }
 
 
@@ -261,10 +315,12 @@ def main():
             "kernels_traffic_bytes": {k: int(v) for k, v in sorted(traffic.items())} or None,
         }
         if world == 1 and not args.no_cpu_baseline:
-            threads = args.cpu_threads or max(1, min(16, os.cpu_count() or 1) - 1)
+            threads = args.cpu_threads or cpu_threads(host_cpu())
             cb = cpu_baseline(engine.ctx, nR, nS, threads, args.verbose)
             out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample")}
-            out["cpu_matches_gpu"] = cb["matches"] == int(matches)
+            out["cpu_legs"] = cb["legs"]
+            out["cpu_host"] = cb["host"]
+            out["cpu_matches_gpu"] = all(m == int(matches) for m in cb["matches"].values())
         print(json.dumps(out), file=json_out, flush=True)
     if exchange:
         dist.barrier()

@@ -1094,6 +1094,10 @@ int join_nopart(phj_ctx* c, const phj_join_params* p, phj_join_result* r, uint32
         g.nb = static_cast<uint32_t>(nbw);
     }
     const uint32_t nb = g.nb;
+    // the materialising probe stores a match as the uint32 slot b * 7 + s, and
+    // kNoMatch (0xffffffff) must stay out of that range
+    if (marks && static_cast<uint64_t>(nb) * kNPSlots >= kNoMatch)
+        return set_err(c, PHJ_ERR_RANGE, "materialised NoPartitioning join: table above 2^32 - 1 slots");
     PHJ_TRY(ensure(c, c->np_tab, static_cast<size_t>(nb) * sizeof(NPBucket)));
     PHJ_TRY(ensure(c, c->np_pays, static_cast<size_t>(nb) * kNPSlots * 8));
     PHJ_TRY(ensure(c, c->count, 8));

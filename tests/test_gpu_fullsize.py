@@ -1,0 +1,125 @@
+"""Full-size parity (10M⋈200M, BASELINE.json configs C2, C4, C5) with a known,
+non-trivial miss fraction, plus config C1 (NoPartitioning 1M⋈16M, XXH3).
+
+With the default generators every S key lies in [1, |R|], so the semi-join
+count is always |S| and a join that matched every in-range
+key would pass. Here the build side starts at 1 + SHIFT instead of 1 (the
+hottest Zipf keys 1..SHIFT miss: ~19% of S at s=1.05, ~40% at s=1.25) and
+every 7th probe key is negated (never in R), so the expected count is far
+from |S|. It is checked three ways on the same device-generated relations:
+the device range count of the surviving keys, the oracle's independent
+sort-and-search semi-join count on the downloaded relations, and the numpy
+closed form. The join takes the default large-relation path (the chunked,
+histogram-free pass 1 starts at ~134M tuples, so S takes it here).
+
+The full-size partitioned layout is checked too: bounds bit-exact against the
+oracle's stable partition (src/RadixCluster/HashJoin.hpp:333-440) and every
+partition's contents by per-partition checksums (the chunked pass 1 leaves
+the order inside a partition unspecified; the reference never reads it).
+"""
+import numpy as np
+import pytest
+
+import partitionedhashjoin_amd as phj
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+NR, NS = 10_000_000, 200_000_000
+SHIFT = 3
+NEG_EVERY = 7
+GEN_SEED = 20240601
+SEED = 0x1234_5678_9ABC_DEF1
+THREADS = 16
+
+
+def _workload(ctx, nR, nS, alpha, shift=SHIFT, neg_every=NEG_EVERY):
+    """R = Sequential from 1 + shift; S = Zipf(alpha) over [1, nR] (device
+    generators), then every neg_every-th S key negated (host round trip).
+    Returns the host copies and the expected count (closed form)."""
+    ctx.generate_sequential(phj.SIDE_BUILD, nR, 1 + shift)
+    ctx.generate_zipf(phj.SIDE_PROBE, nS, alpha, 1, nR, GEN_SEED)
+    R = ctx.download(phj.SIDE_BUILD)
+    S = ctx.download(phj.SIDE_PROBE)
+    if neg_every:
+        S[::neg_every, 0] = -S[::neg_every, 0]
+        ctx.upload(phj.SIDE_PROBE, S)
+    keys = S[:, 0]
+    expect = int(np.count_nonzero((keys > shift) & (keys <= nR + shift)))
+    return R, S, expect
+
+
+def _check_count(ctx, R, S, expect, params):
+    nR = R.shape[0]
+    # device range count: keys of S inside R's key range [1 + SHIFT, nR + SHIFT]
+    assert ctx.count_in_range(phj.SIDE_PROBE, 1 + SHIFT, nR + SHIFT) == expect
+    assert O.semijoin_count(R, S, threads=THREADS) == expect
+    got = ctx.join(params).matches
+    assert got == expect, (got, expect, S.shape[0])
+    return got
+
+
+@pytest.mark.parametrize("name,params,alpha", [
+    ("C2-radix-8+8-murmur3-s1.05", phj.radix_params((8, 8), hash=phj.HASH_MURMUR3, seed=SEED), 1.05),
+    ("C4-nopart-xxh3-s1.05", phj.nopart_params(hash=phj.HASH_XXH3, seed=SEED), 1.05),
+    ("C5-radix-8+8-murmur3-s1.25", phj.radix_params((8, 8), hash=phj.HASH_MURMUR3, seed=SEED), 1.25),
+])
+def test_full_size_counts_with_misses(ctx, name, params, alpha):
+    R, S, expect = _workload(ctx, NR, NS, alpha)
+    # a real miss fraction: the hot keys 1..SHIFT and a seventh of S miss
+    assert 0.4 * NS < expect < 0.85 * NS
+    _check_count(ctx, R, S, expect, params)
+    # the reference's own best CPU configuration (-p 1024, XXH3) on the same relations
+    if name.startswith("C2"):
+        p1024 = phj.radix_params(num_partitions=1024, hash=phj.HASH_XXH3, seed=SEED)
+        assert ctx.join(p1024).matches == expect
+
+
+def _pair_sums(keys, pays, bounds):
+    """Per-partition wrapping sums of two tuple mixes (uint64)."""
+    k = keys.view(np.uint64)
+    p = pays.view(np.uint64)
+    out = []
+    with np.errstate(over="ignore"):
+        for mix in (k * np.uint64(0x9E3779B97F4A7C15) + p,
+                    (k ^ (p << np.uint64(1))) * np.uint64(0xC2B2AE3D27D4EB4F) + k):
+            cs = np.zeros(mix.size + 1, dtype=np.uint64)
+            np.cumsum(mix, dtype=np.uint64, out=cs[1:])
+            b = bounds.astype(np.int64)
+            out.append(cs[b[1:]] - cs[b[:-1]])
+    return out
+
+
+def test_full_size_chunked_partition_layout(ctx):
+    # C2's pass structure on the full 200M-tuple S: chunked pass 1 + pass 2
+    _, S, _ = _workload(ctx, NR, NS, 1.05, shift=0, neg_every=0)
+    p = phj.radix_params((8, 8), hash=phj.HASH_MURMUR3, seed=SEED)
+    v = ctx.partition(phj.SIDE_PROBE, p)
+    keys, pays, bounds = ctx.download_partitioned(v)
+    ref, rb = O.partition(S, 1 << 16, True, O.HASH_MURMUR3, SEED, workers=THREADS)
+    assert np.array_equal(bounds.astype(np.uint64), rb)
+    got = _pair_sums(keys, pays, bounds)
+    exp = _pair_sums(np.ascontiguousarray(ref[:, 0]), np.ascontiguousarray(ref[:, 1]), rb)
+    for g, e in zip(got, exp):
+        assert np.array_equal(g, e)
+    # payload = input index (Zipf::FillTable): every tuple exactly once overall
+    assert np.count_nonzero(np.bincount(pays, minlength=NS) != 1) == 0
+
+
+def test_c1_nopartitioning_1m_16m(ctx):
+    # BASELINE config C1: NoPartitioning, 1M⋈16M, XXH3 (CLI default skew 1.05).
+    # The survey's count is 16 000 000 on default inputs; with misses the GPU,
+    # the oracle's single-thread NoPartitioning restatement and the closed form agree.
+    nR, nS = 1_000_000, 16_000_000
+    R, S = O.generate_tables(nR, nS, 1.05, seed=GEN_SEED, threads=THREADS)
+    params = phj.nopart_params(hash=phj.HASH_XXH3, seed=SEED)
+    ctx.upload(phj.SIDE_BUILD, R)
+    ctx.upload(phj.SIDE_PROBE, S)
+    assert ctx.join(params).matches == nS == O.join_nopart(R, S, workers=1).matches
+    S[::NEG_EVERY, 0] = -S[::NEG_EVERY, 0]
+    R[:, 0] += SHIFT
+    expect = int(np.count_nonzero((S[:, 0] > SHIFT) & (S[:, 0] <= nR + SHIFT)))
+    ctx.upload(phj.SIDE_BUILD, R)
+    ctx.upload(phj.SIDE_PROBE, S)
+    assert O.join_nopart(R, S, workers=1).matches == expect
+    assert ctx.join(params).matches == expect

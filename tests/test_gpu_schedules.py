@@ -56,6 +56,13 @@ SCHEDULES = [
     {"PHJ_P1_MIN_TILES": "0", "PHJ_P1_SLOTS": "3"},             # long persistent walks
     {"PHJ_P1_MIN_TILES": "0", "PHJ_P1_TPS": "4"},               # 16 shards on small relations
     {"PHJ_P1_MIN_TILES": "0", "PHJ_P1_TPS": "8", "PHJ_P1_SLOTS": "1"},  # 8 shards, one workgroup each
+    {"PHJ_FUSED_KPL": "2"},                                     # 2 S keys per lane, 6 waves/SIMD
+    {"PHJ_NT_LOAD": "0"},                                       # no nontemporal tuple loads
+    {"PHJ_NT_LOAD": "2", "PHJ_P1_MIN_TILES": "0"},              # nontemporal loads in both passes
+    {"PHJ_NP_NT": "0"},                                         # NoPartitioning probe: cached S loads
+    {"PHJ_NP_NT": "2"},                                         # ... nontemporal bucket loads too
+    {"PHJ_NP_ITEMS": "8"},                                      # ... 8 S keys per thread per round
+    {"PHJ_NP_REGION": "0"},                                     # ... device-atomic build
 ]
 
 CASES = [((8, 8), 0, phj.HASH_MURMUR3), ((11, 0), 0, phj.HASH_XXH3), ((1, 0), 1000, phj.HASH_XXH3),
@@ -110,5 +117,7 @@ def test_join_counts(tuned_ctx):
               phj.radix_params(num_partitions=32, hash=phj.HASH_XXH3, seed=SEED),
               phj.radix_params(num_partitions=1, hash=phj.HASH_MURMUR3, seed=SEED),
               phj.radix_params(num_partitions=777, hash=phj.HASH_XXH3, seed=SEED),
-              phj.radix_params((6, 0), hash=phj.HASH_XXH3, seed=SEED)):
+              phj.radix_params((6, 0), hash=phj.HASH_XXH3, seed=SEED),
+              phj.nopart_params(hash=phj.HASH_XXH3, seed=SEED),
+              phj.nopart_params(hash=phj.HASH_MURMUR3, seed=SEED, table_ratio=1.0)):
         assert tuned_ctx.join(p).matches == expect

@@ -170,3 +170,18 @@ def test_joins_agree_on_generated_tables(alpha):
         assert r.partition_ms >= 0 and r.build_ms >= 0 and r.probe_ms >= 0
     S[::3, 0] *= -1
     assert O.join_radix(R, S, P=256, radix=True, part_hash=O.HASH_MURMUR3).matches == O.semijoin_count(R, S)
+
+
+def test_c1_nopartitioning_single_thread_1m_16m():
+    # BASELINE config C1: NoPartitioning, 1M ⋈ 16M, XXH3, the CPU reference path
+    # single-threaded (src/main.cpp:81-108 with one worker). SURVEY.md §8(c)
+    # observed count 16 000 000 on the reference's own compiled join.
+    R, S = O.generate_tables(1_000_000, 16_000_000, 1.05, seed=20240601)
+    r = O.join_nopart(R, S, hash_kind=O.HASH_XXH3, seed=0x9E3779B97F4A7C15, workers=1)
+    assert r.workers == 1
+    assert r.matches == 16_000_000 == O.semijoin_count(R, S)
+    # with misses (keys 1..3 leave R, a seventh of S negated) the count follows
+    R[:, 0] += 3
+    S[::7, 0] = -S[::7, 0]
+    expect = int(np.count_nonzero((S[:, 0] > 3) & (S[:, 0] <= 1_000_003)))
+    assert O.join_nopart(R, S, workers=1).matches == expect == O.semijoin_count(R, S)
