@@ -13,8 +13,9 @@ src/main.cpp:254 vs :100-102).
 N=1:  python bench.py [--steps K --warmup W]
 N>1:  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
       Both relations are range-sharded (strong scaling: the 10M⋈200M
-      workload is fixed); the partitioned build side is all-gathered over
-      RCCL (partitionedhashjoin_amd/distributed.py).
+      workload is fixed); each rank's context (phj_ctx_create_rank) runs the
+      multi-GPU member step in libphj_hip.so: the partitioned build keys are
+      all-gathered and the count all-reduced over RCCL (csrc/phj_group.h).
 
 Rank 0 prints ONE JSON line. `roofline` is for the dominant kernel (longest
 per-step device time), from hipEvents on the stream the kernels run on;
@@ -203,7 +204,7 @@ def main():
     import torch
     import torch.distributed as dist
     import partitionedhashjoin_amd as phj
-    from partitionedhashjoin_amd.distributed import HipShardEngine, distributed_join, distributed_join_nopart
+    from partitionedhashjoin_amd.distributed import generate_shards, rank_context
 
     exchange = world > 1 or args.exchange
     if exchange:
@@ -215,27 +216,21 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     nR, nS = args.primary, args.secondary
     params, alpha, workload = config_params(phj, args.config)
-    engine = HipShardEngine(local_rank)
-    engine.generate(nR, nS, alpha, GEN_SEED, rank, world)
+    # the join is one C call per step on this rank's context: a single-device
+    # phj_join at N=1; at N>1 (or --exchange) the multi-GPU member step of
+    # csrc/phj_group.h (R partition + RCCL all-gather of the build keys beside
+    # the S partition, fused join, RCCL all-reduce of the count)
+    ctx = rank_context(local_rank, rank, world, dist if exchange else None, exchange=args.exchange)
+    generate_shards(ctx, nR, nS, alpha, GEN_SEED, rank, world)
     torch.cuda.synchronize()
     # correctness gate at full size: every generated S key lies in [1, |R|]
-    local_inrange = engine.ctx.count_in_range(1, 1, nR)
+    local_inrange = ctx.count_in_range(1, 1, nR)
+    ctx.prepare(params)   # workspace allocated outside the timed region
 
     radix = params.algo == phj.ALGO_RADIX
 
     def step():
-        if radix:
-            # per-kernel timers accumulate on the device; read once after the timed loop
-            return distributed_join(engine, params, nR, nS, rank, world, dist if exchange else None,
-                                    timers=False, force_exchange=exchange)
-        if exchange:   # NoPartitioning over shards: replicated build side (all-gather of R)
-            return distributed_join_nopart(engine, params, nR, nS, rank, world, dist, force_exchange=True)
-        r = engine.ctx.join(params)
-
-        class _R:
-            matches = r.matches
-            timers = r.timers()
-        return _R
+        return ctx.join(params)
 
     for _ in range(args.warmup):
         step()
@@ -246,11 +241,10 @@ def main():
         torch.cuda.synchronize()
 
     barrier()
-    if radix:
-        engine.timers()   # drop the warm-up records
     t0 = time.perf_counter()
     acc = {}
     matches = None
+    exch = 0.0
 
     def accumulate(timers):
         for name, ms, nbytes in timers:
@@ -261,27 +255,39 @@ def main():
     for _ in range(args.steps):
         res = step()
         matches = res.matches
-        accumulate(res.timers)
+        exch += res.exchange_ms
+        accumulate(res.timers())
     barrier()
     elapsed = time.perf_counter() - t0
-    if radix:
-        accumulate(engine.timers())   # sums over the timed steps (hipEvents on the engine stream)
+
+    def allsum(x):
+        if world == 1:
+            return int(x)
+        t = torch.tensor([int(x)], dtype=torch.int64, device="cuda")
+        dist.all_reduce(t)
+        return int(t.item())
+
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        c = torch.tensor([local_inrange], dtype=torch.int64, device="cuda")
-        dist.all_reduce(c)
-        inrange = int(c.item())
-    else:
-        inrange = local_inrange
+    inrange = allsum(local_inrange)
+    # a non-trivial full-size check after the timed region (the default inputs'
+    # answer is always |S|): R shifted to [1 + SHIFT, |R| + SHIFT] makes the
+    # hottest Zipf keys miss; the join must count exactly the S keys in range
+    shift = 3
+    generate_shards(ctx, nR, nS, alpha, GEN_SEED, rank, world, start=1 + shift)
+    shifted_expect = allsum(ctx.count_in_range(1, 1 + shift, nR))
+    shifted_got = ctx.join(params).matches
+    shifted_ok = shifted_got == shifted_expect and shifted_expect < inrange
+    generate_shards(ctx, nR, nS, alpha, GEN_SEED, rank, world)
 
     if rank == 0:
         per_step = {k: (v[0] / args.steps, v[1] / args.steps) for k, v in acc.items()}
         # the dominant kernel of the critical path: the R partition runs on its
         # own stream beside S, and at N=1 its first timer also spans the wait for
         # the persistent S scatter to free the CUs
-        crit = {k: v for k, v in per_step.items() if not k.startswith("R.")} or per_step
+        crit = {k: v for k, v in per_step.items() if not k.startswith("R.") and k != "exchange"} or per_step
         dom_name, (dom_ms, dom_bytes) = max(crit.items(), key=lambda kv: kv[1][0])
         achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
         value = (nR + nS) * args.steps / elapsed
@@ -305,7 +311,9 @@ def main():
                        + (" (exchange path)" if exchange and world == 1 else "")},
             "matches": int(matches),
             "expected_matches": inrange,
-            "correct": int(matches) == inrange,
+            "shifted_check": {"build_start": 1 + shift, "expected": shifted_expect, "matches": shifted_got},
+            "correct": int(matches) == inrange and shifted_ok,
+            "exchange_ms": exch / args.steps if exchange else None,
             "roofline": {"bound": "hbm", "kernel": dom_name, "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic.get(dom_name), "algorithmic_bytes": dom_bytes,
@@ -316,12 +324,13 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             threads = args.cpu_threads or cpu_threads(host_cpu())
-            cb = cpu_baseline(engine.ctx, nR, nS, threads, args.verbose)
+            cb = cpu_baseline(ctx, nR, nS, threads, args.verbose)
             out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample")}
             out["cpu_legs"] = cb["legs"]
             out["cpu_host"] = cb["host"]
             out["cpu_matches_gpu"] = all(m == int(matches) for m in cb["matches"].values())
         print(json.dumps(out), file=json_out, flush=True)
+    ctx.close()
     if exchange:
         dist.barrier()
         dist.destroy_process_group()

@@ -15,8 +15,13 @@
  * only the functions below: plain pointers and sizes, no exceptions, no
  * torch types. Conventions: 0 = PHJ_OK, negative = error (message via
  * phj_last_error). A context owns every device buffer it allocates (grow
- * only, allocated outside the timed phases), is bound to one HIP device and
- * one stream, and is not thread-safe.
+ * only, allocated outside the timed phases) and is not thread-safe. It spans
+ * one device (one stream) or several (SURVEY.md §8(b),(e)): the relations
+ * are range-sharded across the devices, phj_join runs the multi-GPU join
+ * (partition the shards, RCCL all-gather of the partitioned build keys over
+ * xGMI, local build + probe, all-reduce of the count) and one worker thread
+ * per local device issues its work, as the reference's thread pool carries
+ * its parallelism (src/main.cpp:235-241).
  */
 #ifndef PHJ_H
 #define PHJ_H
@@ -27,7 +32,7 @@
 extern "C" {
 #endif
 
-#define PHJ_ABI_VERSION 1
+#define PHJ_ABI_VERSION 2
 
 /* Common::Tuple (src/Common/Table.hpp:20-25): alignas(16) {int64 id; int64 payload}. */
 typedef struct phj_tuple {
@@ -93,6 +98,7 @@ typedef struct phj_join_result {
     double probe_ms;             /* probe alone (the reference's NoPartitioning probe also
                                     counts its build, Results.hpp:202; see phj host driver) */
     double total_ms;             /* first kernel start .. count on host */
+    double exchange_ms;          /* multi-device: the build-side exchange (RCCL all-gather), 0 on one device */
     uint64_t algorithmic_bytes;  /* HBM bytes the algorithm must move */
     uint32_t num_partitions;     /* final partition count (radix) */
     uint32_t num_timers;
@@ -116,10 +122,43 @@ typedef struct phj_partitioned {
 } phj_partitioned;
 
 /* ---- context ---- */
-int phj_ctx_create(int device, phj_ctx **out);
+/* One context over `ngpus` HIP devices (devs[i] = device of rank i; NULL means
+ * 0 .. ngpus-1), SURVEY.md §8(b). ngpus == 1 gives a single-device context.
+ * With ngpus > 1 every relation call takes the whole relation and range-shards
+ * it (rank r holds rows [r*n/ngpus, (r+1)*n/ngpus)), and phj_join / phj_prepare
+ * run the multi-GPU join with RCCL collectives (at most 16 ranks). This is the
+ * reference's Run() with its thread pool (src/main.cpp:235-241, dispatch
+ * :260-276) replaced by devices. */
+int phj_ctx_create(int ngpus, const int *devs, phj_ctx **out);
+/* flags for phj_ctx_create_ex */
+#define PHJ_CTX_EXCHANGE 0x1 /* take the multi-GPU path even on one device (an RCCL world of one) */
+#define PHJ_CTX_LOCAL 0x2    /* exchange by device copies between this process's members instead of
+                                RCCL; devices may repeat (rehearses N ranks on one GPU) */
+int phj_ctx_create_ex(int ngpus, const int *devs, uint32_t flags, phj_ctx **out);
+/* A single-device context (ABI v1's phj_ctx_create(device)). */
+int phj_ctx_create_device(int device, phj_ctx **out);
+/* One device of a multi-process job (one process per GPU, e.g. torchrun):
+ * rank 0 makes an id with phj_comm_unique_id and hands it to every rank (any
+ * channel); each rank creates its context with it. On such a context every
+ * call is collective (all ranks make the same calls in the same order), the
+ * relation calls take this rank's shard (generators: rows [first_index,
+ * first_index + n) of the global relation), and phj_join returns the global
+ * count. */
+#define PHJ_UNIQUE_ID_BYTES 128
+int phj_comm_unique_id(uint8_t *id /* [PHJ_UNIQUE_ID_BYTES] */);
+int phj_ctx_create_rank(int device, int nranks, int rank, const uint8_t *id, phj_ctx **out);
+/* ranks of the job, global rank of this context's first device, devices in this context */
+int phj_ctx_info(const phj_ctx *ctx, int *world, int *rank0, int *nlocal);
+/* Host-only: rows [lo, hi) of an n-row relation held by `rank` of `world` ranks
+ * (the range sharding of every multi-device context). */
+void phj_shard_range(uint64_t n, int rank, int world, uint64_t *lo, uint64_t *hi);
 void phj_ctx_destroy(phj_ctx *ctx);
 const char *phj_last_error(const phj_ctx *ctx);
-/* Run on an external stream (e.g. torch.cuda.current_stream()); NULL = ctx-owned stream. */
+/* Run on an external stream (e.g. torch.cuda.current_stream()); NULL = ctx-owned stream.
+ * Multi-device contexts: only with one local device. The building blocks below
+ * (phj_partition ... phj_hash_keys) likewise act on the single local device of a
+ * rank context and return PHJ_ERR_STATE on a context with several local devices;
+ * phj_join_materialize is single-device only. */
 int phj_ctx_set_stream(phj_ctx *ctx, void *hip_stream);
 int phj_ctx_synchronize(phj_ctx *ctx);
 int phj_abi_version(void);
@@ -129,7 +168,8 @@ int phj_abi_version(void);
 int phj_relation_upload(phj_ctx *ctx, int side, const phj_tuple *host, uint64_t n);
 /* Borrow a device relation (caller keeps it alive while the ctx uses it). */
 int phj_relation_bind_device(phj_ctx *ctx, int side, const phj_tuple *dev, uint64_t n);
-/* Device pointer of the bound relation (NULL if none). */
+/* Device pointer of the bound relation (NULL if none; NULL with *n = the rows
+ * of all local devices on a context with several). */
 const phj_tuple *phj_relation_device_ptr(phj_ctx *ctx, int side, uint64_t *n);
 /* Copy the bound relation back to host (n tuples). */
 int phj_relation_download(phj_ctx *ctx, int side, phj_tuple *host, uint64_t n);

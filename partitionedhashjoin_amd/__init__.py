@@ -14,10 +14,10 @@ import ctypes as C
 import numpy as np
 
 from . import _capi
-from ._capi import (ALGO_NO_PARTITIONING, ALGO_RADIX, HASH_MURMUR3, HASH_XXH3, SIDE_BUILD,
+from ._capi import (ALGO_NO_PARTITIONING, ALGO_RADIX, CTX_EXCHANGE, CTX_LOCAL, HASH_MURMUR3, HASH_XXH3, SIDE_BUILD,
                     SIDE_PROBE, JoinParams, JoinResult, Partitioned, PhjError)
 
-__all__ = ["Context", "radix_params", "nopart_params", "JoinParams", "JoinResult",
+__all__ = ["Context", "shard_range", "comm_unique_id", "CTX_EXCHANGE", "CTX_LOCAL", "radix_params", "nopart_params", "JoinParams", "JoinResult",
            "Partitioned", "PhjError", "ALGO_RADIX", "ALGO_NO_PARTITIONING", "HASH_XXH3",
            "HASH_MURMUR3", "SIDE_BUILD", "SIDE_PROBE", "DEFAULT_SEED"]
 
@@ -53,18 +53,69 @@ def nopart_params(hash=HASH_XXH3, seed=DEFAULT_SEED, table_ratio=0.0) -> JoinPar
     return p
 
 
-class Context:
-    """One HIP device + stream + workspace (phj_ctx)."""
+def shard_range(n: int, rank: int, world: int):
+    """Rows [lo, hi) of an n-row relation held by `rank` of `world` ranks: the
+    range sharding of every multi-device context (phj_shard_range; host only)."""
+    L = _capi.load()
+    lo, hi = C.c_uint64(), C.c_uint64()
+    L.phj_shard_range(n, rank, world, C.byref(lo), C.byref(hi))
+    return lo.value, hi.value
 
-    def __init__(self, device: int = 0):
+
+def comm_unique_id() -> bytes:
+    """A fresh RCCL unique id (rank 0 makes it; every rank passes it to
+    Context.rank)."""
+    L = _capi.load()
+    buf = C.create_string_buffer(_capi.UNIQUE_ID_BYTES)
+    rc = L.phj_comm_unique_id(buf)
+    if rc != 0:
+        raise PhjError(rc, "phj_comm_unique_id failed (RCCL unavailable?)")
+    return buf.raw
+
+
+class Context:
+    """A phj_ctx: one HIP device (Context(device)), several devices driven by
+    this process (Context(devices=[...]), the multi-GPU join; flags
+    CTX_EXCHANGE / CTX_LOCAL), or one rank of a multi-process job
+    (Context.rank)."""
+
+    def __init__(self, device: int = 0, devices=None, flags: int = 0, _handle=None):
         self._L = _capi.load()
+        self._keep = {}
+        if _handle is not None:
+            self._h = _handle
+            self.device = device
+            return
         h = C.c_void_p()
-        rc = self._L.phj_ctx_create(device, C.byref(h))
+        if devices is None:
+            rc = self._L.phj_ctx_create_device(device, C.byref(h))
+            what = f"phj_ctx_create_device({device})"
+        else:
+            arr = (C.c_int * len(devices))(*devices)
+            rc = self._L.phj_ctx_create_ex(len(devices), arr, flags, C.byref(h))
+            what = f"phj_ctx_create_ex({list(devices)}, flags={flags})"
+            device = devices[0]
         if rc != 0:
-            raise PhjError(rc, f"phj_ctx_create(device={device}) failed")
+            raise PhjError(rc, f"{what} failed")
         self._h = h
         self.device = device
-        self._keep = {}
+
+    @classmethod
+    def rank(cls, device: int, nranks: int, rank: int, unique_id: bytes) -> "Context":
+        """One device of a multi-process job (phj_ctx_create_rank): every call
+        on it is collective over the ranks."""
+        L = _capi.load()
+        h = C.c_void_p()
+        rc = L.phj_ctx_create_rank(device, nranks, rank, unique_id, C.byref(h))
+        if rc != 0:
+            raise PhjError(rc, f"phj_ctx_create_rank(device={device}, {rank}/{nranks}) failed")
+        return cls(device, _handle=h)
+
+    def info(self):
+        """(world, rank of the first local device, local devices)"""
+        w, r, n = C.c_int(), C.c_int(), C.c_int()
+        self._check(self._L.phj_ctx_info(self._h, C.byref(w), C.byref(r), C.byref(n)))
+        return w.value, r.value, n.value
 
     # -- lifecycle --
     def close(self):

@@ -37,7 +37,13 @@ EXPORTED = [
     "phj_relation_count_in_range", "phj_join", "phj_partition", "phj_join_partitioned",
     "phj_partitioned_download", "phj_hash_keys", "phj_timers_report", "phj_join_partitioned_async",
     "phj_prepare", "phj_join_materialize", "phj_joined_rows", "phj_joined_download",
+    "phj_ctx_create_ex", "phj_ctx_create_device", "phj_comm_unique_id", "phj_ctx_create_rank",
+    "phj_ctx_info", "phj_shard_range",
 ]
+ABI_VERSION = 2
+CTX_EXCHANGE = 0x1   # phj_ctx_create_ex: the multi-GPU path on one device (RCCL world of one)
+CTX_LOCAL = 0x2      # ... exchange by device copies; devices may repeat (rehearsal on one GPU)
+UNIQUE_ID_BYTES = 128
 
 
 class Tuple(C.Structure):
@@ -54,7 +60,7 @@ class JoinParams(C.Structure):
 
 class JoinResult(C.Structure):
     _fields_ = [("matches", C.c_uint64), ("partition_ms", C.c_double), ("build_ms", C.c_double),
-                ("probe_ms", C.c_double), ("total_ms", C.c_double),
+                ("probe_ms", C.c_double), ("total_ms", C.c_double), ("exchange_ms", C.c_double),
                 ("algorithmic_bytes", C.c_uint64), ("num_partitions", C.c_uint32),
                 ("num_timers", C.c_uint32), ("timer_ms", C.c_double * MAX_TIMERS),
                 ("timer_bytes", C.c_uint64 * MAX_TIMERS),
@@ -67,6 +73,7 @@ class JoinResult(C.Structure):
     def as_dict(self):
         return {"matches": self.matches, "partition_ms": self.partition_ms,
                 "build_ms": self.build_ms, "probe_ms": self.probe_ms, "total_ms": self.total_ms,
+                "exchange_ms": self.exchange_ms,
                 "algorithmic_bytes": self.algorithmic_bytes,
                 "num_partitions": self.num_partitions, "timers": self.timers()}
 
@@ -98,7 +105,13 @@ def load():
     u64, i64, i, d = C.c_uint64, C.c_int64, C.c_int, C.c_double
     sig = {
         "phj_abi_version": (i, []),
-        "phj_ctx_create": (i, [i, C.POINTER(P)]),
+        "phj_ctx_create": (i, [i, C.POINTER(i), C.POINTER(P)]),
+        "phj_ctx_create_ex": (i, [i, C.POINTER(i), C.c_uint32, C.POINTER(P)]),
+        "phj_ctx_create_device": (i, [i, C.POINTER(P)]),
+        "phj_comm_unique_id": (i, [C.c_char_p]),
+        "phj_ctx_create_rank": (i, [i, i, i, C.c_char_p, C.POINTER(P)]),
+        "phj_ctx_info": (i, [P, C.POINTER(i), C.POINTER(i), C.POINTER(i)]),
+        "phj_shard_range": (None, [u64, i, i, C.POINTER(u64), C.POINTER(u64)]),
         "phj_ctx_destroy": (None, [P]),
         "phj_last_error": (C.c_char_p, [P]),
         "phj_ctx_set_stream": (i, [P, P]),

@@ -126,9 +126,12 @@ uint32_t next_pow2_u32(uint32_t x) {
     return p;
 }
 
+struct Group;   // phj_group.h: the members of a multi-device context
+
 }  // namespace
 
 struct phj_ctx {
+    Group* group = nullptr;        // multi-device context (phj_group.h); null for one device
     int device = 0;
     hipStream_t stream = nullptr;  // the ctx stream (own or borrowed)
     hipStream_t aux = nullptr;     // ctx-owned: R-side partitioning runs here beside S
@@ -1309,13 +1312,7 @@ int join_radix_mark(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
     return fill_timers(c, r);
 }
 
-}  // namespace
-
-extern "C" {
-
-int phj_abi_version(void) { return PHJ_ABI_VERSION; }
-
-int phj_ctx_create(int device, phj_ctx** out) {
+int ctx_create_device(int device, phj_ctx** out) {
     if (!out) return PHJ_ERR_INVALID;
     *out = nullptr;
     int ndev = 0;
@@ -1384,8 +1381,86 @@ int phj_ctx_create(int device, phj_ctx** out) {
     return PHJ_OK;
 }
 
+}  // namespace
+
+#include "phj_group.h"
+
+namespace {
+
+// A multi-device context with one local member forwards the single-device
+// calls (building blocks) to it; with several members they are not defined.
+template <class F>
+int on_solo(phj_ctx* c, const char* what, F f) {
+    phj_ctx* m = c->group->nlocal() == 1 ? c->group->mem[0] : nullptr;
+    if (!m) return set_err(c, PHJ_ERR_STATE, std::string(what) + ": not available on a multi-device context");
+    const int rc = f(m);
+    if (rc != PHJ_OK) c->err = m->err;
+    return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int phj_abi_version(void) { return PHJ_ABI_VERSION; }
+
+int phj_ctx_create_device(int device, phj_ctx** out) { return ctx_create_device(device, out); }
+
+int phj_ctx_create_ex(int ngpus, const int* devs, uint32_t flags, phj_ctx** out) {
+    if (!out) return PHJ_ERR_INVALID;
+    *out = nullptr;
+    if (ngpus < 1 || ngpus > kMaxSegs) return PHJ_ERR_INVALID;
+    std::vector<int> d(ngpus);
+    for (int i = 0; i < ngpus; i++) d[i] = devs ? devs[i] : i;
+    if (ngpus == 1 && !(flags & (PHJ_CTX_EXCHANGE | PHJ_CTX_LOCAL))) return ctx_create_device(d[0], out);
+    return group_create(ngpus, d.data(), flags, ngpus, 0, nullptr, out);
+}
+
+int phj_ctx_create(int ngpus, const int* devs, phj_ctx** out) { return phj_ctx_create_ex(ngpus, devs, 0, out); }
+
+int phj_comm_unique_id(uint8_t* id) {
+    if (!id) return PHJ_ERR_INVALID;
+    RcclApi& api = rccl();
+    if (!api.loaded) {
+        std::fprintf(stderr, "phj_comm_unique_id: %s\n", api.err.c_str());
+        return PHJ_ERR_HIP;
+    }
+    static_assert(sizeof(ncclUniqueId) == PHJ_UNIQUE_ID_BYTES, "unique id size");
+    ncclUniqueId u;
+    if (api.GetUniqueId(&u) != ncclSuccess) return PHJ_ERR_HIP;
+    std::memcpy(id, &u, sizeof(u));
+    return PHJ_OK;
+}
+
+int phj_ctx_create_rank(int device, int nranks, int rank, const uint8_t* id, phj_ctx** out) {
+    if (!out) return PHJ_ERR_INVALID;
+    *out = nullptr;
+    if (!id || nranks < 1 || nranks > kMaxSegs || rank < 0 || rank >= nranks) return PHJ_ERR_INVALID;
+    return group_create(1, &device, 0, nranks, rank, id, out);
+}
+
+int phj_ctx_info(const phj_ctx* c, int* world, int* rank0, int* nlocal) {
+    if (!c) return PHJ_ERR_INVALID;
+    if (world) *world = c->group ? c->group->world : 1;
+    if (rank0) *rank0 = c->group ? c->group->rank0 : 0;
+    if (nlocal) *nlocal = c->group ? c->group->nlocal() : 1;
+    return PHJ_OK;
+}
+
+void phj_shard_range(uint64_t n, int rank, int world, uint64_t* lo, uint64_t* hi) {
+    uint64_t a = 0, b = 0;
+    if (world >= 1 && rank >= 0 && rank < world) shard_range(n, rank, world, &a, &b);
+    if (lo) *lo = a;
+    if (hi) *hi = b;
+}
+
 void phj_ctx_destroy(phj_ctx* c) {
     if (!c) return;
+    if (c->group) {
+        group_destroy(c->group);
+        delete c;
+        return;
+    }
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     (void)hipStreamSynchronize(c->aux);
@@ -1407,6 +1482,7 @@ const char* phj_last_error(const phj_ctx* c) { return c ? c->err.c_str() : "null
 
 int phj_ctx_set_stream(phj_ctx* c, void* stream) {
     if (!c) return PHJ_ERR_INVALID;
+    if (c->group) return on_solo(c, "phj_ctx_set_stream", [&](phj_ctx* m) { return phj_ctx_set_stream(m, stream); });
     PHJ_HIP(c, hipSetDevice(c->device));
     PHJ_HIP(c, hipStreamSynchronize(c->stream));
     PHJ_HIP(c, hipStreamSynchronize(c->aux));
@@ -1426,6 +1502,13 @@ int phj_ctx_set_stream(phj_ctx* c, void* stream) {
 
 int phj_ctx_synchronize(phj_ctx* c) {
     if (!c) return PHJ_ERR_INVALID;
+    if (c->group) {
+        for (phj_ctx* m : c->group->mem) {
+            const int rc = phj_ctx_synchronize(m);
+            if (rc != PHJ_OK) return set_err(c, rc, m->err);
+        }
+        return PHJ_OK;
+    }
     PHJ_HIP(c, hipStreamSynchronize(c->aux));
     PHJ_HIP(c, hipStreamSynchronize(c->stream));
     return PHJ_OK;
@@ -1434,6 +1517,7 @@ int phj_ctx_synchronize(phj_ctx* c) {
 int phj_relation_upload(phj_ctx* c, int side, const phj_tuple* host, uint64_t n) {
     PHJ_TRY(check_side(c, side));
     if (n && !host) return set_err(c, PHJ_ERR_INVALID, "null host relation");
+    if (c->group) return group_upload(c, side, host, n);
     PHJ_HIP(c, hipSetDevice(c->device));
     SideState& S = c->side[side];
     drop_relation(c, side);
@@ -1451,6 +1535,10 @@ int phj_relation_bind_device(phj_ctx* c, int side, const phj_tuple* dev, uint64_
     PHJ_TRY(check_side(c, side));
     if (n && !dev) return set_err(c, PHJ_ERR_INVALID, "null device relation");
     if (reinterpret_cast<uintptr_t>(dev) % 16) return set_err(c, PHJ_ERR_INVALID, "relation must be 16-byte aligned");
+    if (c->group) {
+        PHJ_TRY(on_solo(c, "phj_relation_bind_device", [&](phj_ctx* m) { return phj_relation_bind_device(m, side, dev, n); }));
+        return exchange_sizes(c, *c->group, side);
+    }
     drop_relation(c, side);
     c->side[side].rel = dev;
     c->side[side].n = n;
@@ -1459,12 +1547,21 @@ int phj_relation_bind_device(phj_ctx* c, int side, const phj_tuple* dev, uint64_
 
 const phj_tuple* phj_relation_device_ptr(phj_ctx* c, int side, uint64_t* n) {
     if (!c || (side != 0 && side != 1)) return nullptr;
+    if (c->group) {   // several local devices: rows of all of them, no single pointer
+        if (c->group->nlocal() == 1) return phj_relation_device_ptr(c->group->mem[0], side, n);
+        if (n) {
+            *n = 0;
+            for (phj_ctx* m : c->group->mem) *n += m->side[side].n;
+        }
+        return nullptr;
+    }
     if (n) *n = c->side[side].n;
     return c->side[side].rel;
 }
 
 int phj_relation_download(phj_ctx* c, int side, phj_tuple* host, uint64_t n) {
     PHJ_TRY(check_side(c, side));
+    if (c->group) return group_download(c, side, host, n);
     SideState& S = c->side[side];
     if (n > S.n) return set_err(c, PHJ_ERR_INVALID, "download larger than the relation");
     PHJ_HIP(c, hipSetDevice(c->device));
@@ -1477,6 +1574,10 @@ int phj_relation_download(phj_ctx* c, int side, phj_tuple* host, uint64_t n) {
 
 int phj_relation_generate_sequential(phj_ctx* c, int side, uint64_t n, int64_t start, uint64_t first_index) {
     PHJ_TRY(check_side(c, side));
+    if (c->group)
+        return group_generate(c, side, n, first_index, [&](phj_ctx* m, uint64_t k, uint64_t first) {
+            return phj_relation_generate_sequential(m, side, k, start, first);
+        });
     PHJ_HIP(c, hipSetDevice(c->device));
     SideState& S = c->side[side];
     drop_relation(c, side);
@@ -1498,6 +1599,10 @@ int phj_relation_generate_zipf(phj_ctx* c, int side, uint64_t n, double alpha, i
     PHJ_TRY(check_side(c, side));
     if (lo >= hi) return set_err(c, PHJ_ERR_INVALID, "Range for Zipf generation is incorrectly specified");
     if (alpha < 0.01) return set_err(c, PHJ_ERR_INVALID, "Skew parameter must be greater than 0.01.");
+    if (c->group)
+        return group_generate(c, side, n, first_index, [&](phj_ctx* m, uint64_t k, uint64_t first) {
+            return phj_relation_generate_zipf(m, side, k, alpha, lo, hi, seed, first);
+        });
     PHJ_HIP(c, hipSetDevice(c->device));
     SideState& S = c->side[side];
     drop_relation(c, side);
@@ -1518,6 +1623,17 @@ int phj_relation_generate_zipf(phj_ctx* c, int side, uint64_t n, double alpha, i
 int phj_relation_count_in_range(phj_ctx* c, int side, int64_t lo, int64_t hi, uint64_t* count) {
     PHJ_TRY(check_side(c, side));
     if (!count) return set_err(c, PHJ_ERR_INVALID, "null count");
+    if (c->group) {   // over this process's shards
+        uint64_t t = 0;
+        for (phj_ctx* m : c->group->mem) {
+            uint64_t k = 0;
+            const int rc = phj_relation_count_in_range(m, side, lo, hi, &k);
+            if (rc != PHJ_OK) return set_err(c, rc, m->err);
+            t += k;
+        }
+        *count = t;
+        return PHJ_OK;
+    }
     PHJ_HIP(c, hipSetDevice(c->device));
     SideState& S = c->side[side];
     PHJ_TRY(ensure(c, c->count, 8));
@@ -1533,6 +1649,7 @@ int phj_relation_count_in_range(phj_ctx* c, int side, int64_t lo, int64_t hi, ui
 
 int phj_partition(phj_ctx* c, int side, const phj_join_params* p, phj_partitioned* out) {
     PHJ_TRY(check_side(c, side));
+    if (c->group) return on_solo(c, "phj_partition", [&](phj_ctx* m) { return phj_partition(m, side, p, out); });
     (void)hipGetLastError();
     if (p && p->algo != PHJ_ALGO_RADIX) return set_err(c, PHJ_ERR_INVALID, "phj_partition needs PHJ_ALGO_RADIX");
     Plan pl;
@@ -1549,6 +1666,8 @@ int phj_partition(phj_ctx* c, int side, const phj_join_params* p, phj_partitione
 int phj_join_partitioned(phj_ctx* c, const phj_join_params* p, int nbuild, const phj_partitioned* build,
                          phj_join_result* r) {
     if (!c || !r) return PHJ_ERR_INVALID;
+    if (c->group)
+        return on_solo(c, "phj_join_partitioned", [&](phj_ctx* m) { return phj_join_partitioned(m, p, nbuild, build, r); });
     if (!build) return set_err(c, PHJ_ERR_INVALID, "null build segments");
     if (p && p->algo != PHJ_ALGO_RADIX) return set_err(c, PHJ_ERR_INVALID, "phj_join_partitioned needs PHJ_ALGO_RADIX");
     (void)hipGetLastError();
@@ -1581,6 +1700,9 @@ int phj_join_partitioned(phj_ctx* c, const phj_join_params* p, int nbuild, const
 int phj_join_partitioned_async(phj_ctx* c, const phj_join_params* p, int nbuild, const phj_partitioned* build,
                                uint64_t* dev_count) {
     if (!c) return PHJ_ERR_INVALID;
+    if (c->group)
+        return on_solo(c, "phj_join_partitioned_async",
+                       [&](phj_ctx* m) { return phj_join_partitioned_async(m, p, nbuild, build, dev_count); });
     if (!build || !dev_count) return set_err(c, PHJ_ERR_INVALID, "null build segments or count address");
     if (p && p->algo != PHJ_ALGO_RADIX)
         return set_err(c, PHJ_ERR_INVALID, "phj_join_partitioned_async needs PHJ_ALGO_RADIX");
@@ -1598,6 +1720,10 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
     if (!c || !r) return PHJ_ERR_INVALID;
     (void)hipGetLastError();
     if (!p) return set_err(c, PHJ_ERR_INVALID, "null params");
+    if (c->group) {
+        std::memset(r, 0, sizeof(*r));
+        return group_join(c, p, r, false);
+    }
     PHJ_HIP(c, hipSetDevice(c->device));
     std::memset(r, 0, sizeof(*r));
     reset_timers(c);
@@ -1643,6 +1769,10 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
 int phj_prepare(phj_ctx* c, const phj_join_params* p) {
     if (!c) return PHJ_ERR_INVALID;
     if (!p) return set_err(c, PHJ_ERR_INVALID, "null params");
+    if (c->group) {
+        phj_join_result r{};
+        return group_join(c, p, &r, true);
+    }
     (void)hipGetLastError();
     PHJ_HIP(c, hipSetDevice(c->device));
     struct DryScope {
@@ -1671,6 +1801,7 @@ int phj_prepare(phj_ctx* c, const phj_join_params* p) {
 
 int phj_timers_report(phj_ctx* c, phj_join_result* r) {
     if (!c || !r) return PHJ_ERR_INVALID;
+    if (c->group) return on_solo(c, "phj_timers_report", [&](phj_ctx* m) { return phj_timers_report(m, r); });
     PHJ_HIP(c, hipSetDevice(c->device));
     PHJ_HIP(c, hipStreamSynchronize(c->ks));
     std::memset(r, 0, sizeof(*r));
@@ -1682,6 +1813,9 @@ int phj_timers_report(phj_ctx* c, phj_join_result* r) {
 int phj_partitioned_download(phj_ctx* c, const phj_partitioned* v, int64_t* keys, int64_t* payloads,
                              uint32_t* bounds) {
     if (!c || !v) return PHJ_ERR_INVALID;
+    if (c->group)
+        return on_solo(c, "phj_partitioned_download",
+                       [&](phj_ctx* m) { return phj_partitioned_download(m, v, keys, payloads, bounds); });
     PHJ_HIP(c, hipSetDevice(c->device));
     if (v->n && keys) PHJ_HIP(c, hipMemcpyAsync(keys, v->keys, v->n * 8, hipMemcpyDefault, c->ks));
     if (v->n && payloads) PHJ_HIP(c, hipMemcpyAsync(payloads, v->payloads, v->n * 8, hipMemcpyDefault, c->ks));
@@ -1706,6 +1840,7 @@ static_assert(sizeof(phj_joined) == 24 && sizeof(JoinedRow) == sizeof(phj_joined
 
 int phj_join_materialize(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
     if (!c || !r) return PHJ_ERR_INVALID;
+    if (c->group) return set_err(c, PHJ_ERR_STATE, "phj_join_materialize: single-device contexts only");
     (void)hipGetLastError();
     if (!p) return set_err(c, PHJ_ERR_INVALID, "null params");
     PHJ_HIP(c, hipSetDevice(c->device));
@@ -1737,13 +1872,14 @@ int phj_join_materialize(phj_ctx* c, const phj_join_params* p, phj_join_result* 
 }
 
 const phj_joined* phj_joined_rows(phj_ctx* c, uint64_t* n) {
-    if (!c) return nullptr;
+    if (!c || c->group) return nullptr;
     if (n) *n = c->mat_n;
     return static_cast<const phj_joined*>(c->mat_rows.p);
 }
 
 int phj_joined_download(phj_ctx* c, phj_joined* host, uint64_t n) {
     if (!c) return PHJ_ERR_INVALID;
+    if (c->group) return set_err(c, PHJ_ERR_STATE, "phj_joined_download: single-device contexts only");
     if (n > c->mat_n) return set_err(c, PHJ_ERR_RANGE, "more rows requested than the last materialised join made");
     if (n == 0) return PHJ_OK;
     if (!host) return set_err(c, PHJ_ERR_INVALID, "null destination");
@@ -1755,6 +1891,8 @@ int phj_joined_download(phj_ctx* c, phj_joined* host, uint64_t n) {
 
 int phj_hash_keys(phj_ctx* c, int hash, uint64_t seed, const int64_t* keys, uint64_t n, uint64_t* out) {
     if (!c) return PHJ_ERR_INVALID;
+    if (c->group)
+        return on_solo(c, "phj_hash_keys", [&](phj_ctx* m) { return phj_hash_keys(m, hash, seed, keys, n, out); });
     if (hash != PHJ_HASH_XXH3 && hash != PHJ_HASH_MURMUR3) return set_err(c, PHJ_ERR_INVALID, "unknown hash function");
     if (n == 0) return PHJ_OK;
     (void)hipGetLastError();

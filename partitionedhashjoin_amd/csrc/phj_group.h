@@ -1,0 +1,704 @@
+// phj_group.h — several devices behind one phj_ctx: the multi-GPU join
+// (SURVEY.md §8(b) "phj_ctx_create(ngpus, devs)", §8(e)).
+//
+// The reference injects its parallelism into the joiner as a thread pool of
+// hardware_concurrency() - 1 workers (src/main.cpp:235-241) and dispatches
+// Run() from main (:260-276). Here the joiner's context spans G devices (one
+// process, `phj_ctx_create(ngpus, devs)`), or is one device of a G-process
+// job (one process per GPU, `phj_ctx_create_rank`). Either way every device
+// ("member", global rank r) runs the same step on its range shards
+// R_r = rows [r|R|/G, (r+1)|R|/G) and S_r:
+//
+//   aux stream:   partition R_r (2-pass radix) -> pack keys | bounds -> all-gather
+//   main stream:  partition S_r (beside it) -> wait -> fused build + probe of
+//                 S_r against the G gathered build segments -> all-reduce(count)
+//
+// S (95% of the bytes) never leaves its device and stays balanced under any
+// key skew; only the build keys travel (the join tests key equality and never
+// reads a build payload: RadixCluster/HashJoin.hpp:295-301). NoPartitioning
+// replicates R instead (grouped broadcasts = an all-gather-v into one
+// contiguous relation), builds the global table on every device and probes
+// the local S shard (§8(e) "NoPartitioning multi-GPU").
+//
+// The exchange is RCCL over xGMI (librccl, resolved at run time so the
+// library loads where RCCL is absent). PHJ_CTX_LOCAL replaces the
+// collectives by device copies between the members of one process, so the
+// multi-member orchestration runs with repeated devices (rehearsal on one GPU,
+// where RCCL refuses two ranks per device). A process drives its local members
+// from one worker thread each: issuing one member's ~30 launches costs
+// ~0.15 ms of host time, which one thread would serialise across 8 devices.
+#pragma once
+
+#include <dlfcn.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <type_traits>
+
+#include <rccl/rccl.h>
+
+namespace {
+
+// ---- RCCL, resolved with dlopen on first use ----
+struct RcclApi {
+    bool loaded = false;
+    std::string err;
+    decltype(&ncclGetUniqueId) GetUniqueId = nullptr;
+    decltype(&ncclCommInitRank) CommInitRank = nullptr;
+    decltype(&ncclCommInitAll) CommInitAll = nullptr;
+    decltype(&ncclCommDestroy) CommDestroy = nullptr;
+    decltype(&ncclAllGather) AllGather = nullptr;
+    decltype(&ncclAllReduce) AllReduce = nullptr;
+    decltype(&ncclBroadcast) Broadcast = nullptr;
+    decltype(&ncclGroupStart) GroupStart = nullptr;
+    decltype(&ncclGroupEnd) GroupEnd = nullptr;
+    decltype(&ncclGetErrorString) GetErrorString = nullptr;
+};
+
+RcclApi& rccl() {
+    static RcclApi api = [] {
+        RcclApi a;
+        // an RCCL already in the process (e.g. torch's) is reused by its soname
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) {
+            const char* e = dlerror();
+            a.err = std::string("dlopen(librccl.so.1): ") + (e ? e : "not found");
+            return a;
+        }
+        bool ok = true;
+        auto sym = [&](auto& fp, const char* name) {
+            fp = reinterpret_cast<std::remove_reference_t<decltype(fp)>>(dlsym(h, name));
+            if (!fp) {
+                ok = false;
+                a.err = std::string("librccl: missing ") + name;
+            }
+        };
+        sym(a.GetUniqueId, "ncclGetUniqueId");
+        sym(a.CommInitRank, "ncclCommInitRank");
+        sym(a.CommInitAll, "ncclCommInitAll");
+        sym(a.CommDestroy, "ncclCommDestroy");
+        sym(a.AllGather, "ncclAllGather");
+        sym(a.AllReduce, "ncclAllReduce");
+        sym(a.Broadcast, "ncclBroadcast");
+        sym(a.GroupStart, "ncclGroupStart");
+        sym(a.GroupEnd, "ncclGroupEnd");
+        sym(a.GetErrorString, "ncclGetErrorString");
+        a.loaded = ok;
+        return a;
+    }();
+    return api;
+}
+
+#define PHJ_NCCL(ctx, expr)                                                                   \
+    do {                                                                                      \
+        ncclResult_t r_ = (expr);                                                             \
+        if (r_ != ncclSuccess)                                                                \
+            return set_err(ctx, PHJ_ERR_HIP, std::string(#expr) + ": " + rccl().GetErrorString(r_)); \
+    } while (0)
+
+// ---- member threads: f(i) on thread i, the caller waits for all ----
+class MemberThreads {
+   public:
+    explicit MemberThreads(int n) : n_(n), rc_(n, PHJ_OK) {
+        for (int i = 0; i < n; i++) th_.emplace_back([this, i] { loop(i); });
+    }
+    ~MemberThreads() {
+        {
+            std::lock_guard<std::mutex> l(m_);
+            stop_ = true;
+            gen_++;
+        }
+        cv_.notify_all();
+        for (std::thread& t : th_) t.join();
+    }
+    int run(const std::function<int(int)>& f) {
+        {
+            std::lock_guard<std::mutex> l(m_);
+            f_ = &f;
+            pending_ = n_;
+            gen_++;
+        }
+        cv_.notify_all();
+        std::unique_lock<std::mutex> l(m_);
+        done_.wait(l, [&] { return pending_ == 0; });
+        f_ = nullptr;
+        for (int rc : rc_)
+            if (rc != PHJ_OK) return rc;
+        return PHJ_OK;
+    }
+
+   private:
+    void loop(int i) {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<int(int)>* f = nullptr;
+            {
+                std::unique_lock<std::mutex> l(m_);
+                cv_.wait(l, [&] { return gen_ != seen; });
+                seen = gen_;
+                if (stop_) return;
+                f = f_;
+            }
+            const int rc = (*f)(i);
+            {
+                std::lock_guard<std::mutex> l(m_);
+                rc_[i] = rc;
+                if (--pending_ == 0) done_.notify_one();
+            }
+        }
+    }
+    int n_;
+    std::vector<int> rc_;
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    const std::function<int(int)>* f_ = nullptr;
+    uint64_t gen_ = 0;
+    int pending_ = 0;
+    bool stop_ = false;
+};
+
+// Reusable barrier of the member threads (PHJ_CTX_LOCAL exchange).
+class Barrier {
+   public:
+    explicit Barrier(int n) : n_(n) {}
+    void wait() {
+        std::unique_lock<std::mutex> l(m_);
+        const uint64_t g = gen_;
+        if (++count_ == n_) {
+            count_ = 0;
+            gen_++;
+            cv_.notify_all();
+            return;
+        }
+        cv_.wait(l, [&] { return gen_ != g; });
+    }
+
+   private:
+    int n_, count_ = 0;
+    uint64_t gen_ = 0;
+    std::mutex m_;
+    std::condition_variable cv_;
+};
+
+void shard_range(uint64_t n, int rank, int world, uint64_t* lo, uint64_t* hi) {
+    // rows [n*r/G, n*(r+1)/G): 128-bit products keep any n exact
+    *lo = static_cast<uint64_t>((static_cast<unsigned __int128>(n) * rank) / world);
+    *hi = static_cast<uint64_t>((static_cast<unsigned __int128>(n) * (rank + 1)) / world);
+}
+
+// Radix exchange block of one rank: build keys[maxn] | bounds[P + 1] (uint32,
+// two per int64 element); maxn is padded to 64 elements so both columns stay
+// 16-B aligned inside the gathered buffer.
+struct PackLayout {
+    uint64_t maxn, elems;
+};
+
+PackLayout pack_layout(uint64_t maxn, uint32_t P) {
+    PackLayout l;
+    l.maxn = (maxn + 63) / 64 * 64;
+    l.elems = l.maxn + (static_cast<uint64_t>(P) + 2) / 2;
+    return l;
+}
+
+enum class Xchg { kRccl, kLocal };
+
+struct MemberBufs {
+    DevBuf send, recv, cnt, full;
+    hipEvent_t packed = nullptr;
+};
+
+struct Group {
+    int world = 1;     // global ranks
+    int rank0 = 0;     // global rank of local member 0
+    Xchg kind = Xchg::kRccl;
+    std::vector<phj_ctx*> mem;
+    std::vector<ncclComm_t> comm;
+    std::vector<MemberBufs> buf;
+    std::vector<uint64_t> n[2];   // shard sizes per global rank, per side
+    std::unique_ptr<MemberThreads> threads;
+    std::unique_ptr<Barrier> barrier;
+    std::vector<phj_join_result> res;   // per member, the last join
+    std::atomic<int> failed{0};          // local exchange: a member failed before the barrier
+    int nlocal() const { return static_cast<int>(mem.size()); }
+};
+
+// f(i) for every local member: on the member threads, or inline for one.
+int for_members(phj_ctx* shell, Group& G, const std::function<int(int)>& f) {
+    int rc;
+    if (G.nlocal() == 1) {
+        rc = f(0);
+    } else {
+        rc = G.threads->run(f);
+    }
+    if (rc != PHJ_OK) {
+        for (int i = 0; i < G.nlocal(); i++)
+            if (!G.mem[i]->err.empty()) {
+                shell->err = "device " + std::to_string(G.rank0 + i) + ": " + G.mem[i]->err;
+                break;
+            }
+    }
+    return rc;
+}
+
+void group_destroy(Group* G) {
+    if (!G) return;
+    G->threads.reset();
+    for (size_t i = 0; i < G->mem.size(); i++) {
+        phj_ctx* c = G->mem[i];
+        (void)hipSetDevice(c->device);
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipStreamSynchronize(c->aux);
+        if (i < G->comm.size() && G->comm[i]) (void)rccl().CommDestroy(G->comm[i]);
+        MemberBufs& B = G->buf[i];
+        for (DevBuf* b : {&B.send, &B.recv, &B.cnt, &B.full}) free_buf(*b);
+        if (B.packed) (void)hipEventDestroy(B.packed);
+    }
+    for (phj_ctx* c : G->mem) phj_ctx_destroy(c);
+    delete G;
+}
+
+// Sizes of every rank's shard after a local relation change: known on the
+// host when the whole world is local, else one all-gather (the relation calls
+// of a multi-process context are collective).
+int exchange_sizes(phj_ctx* shell, Group& G, int side) {
+    std::vector<uint64_t>& v = G.n[side];
+    v.assign(G.world, 0);
+    if (G.nlocal() == G.world) {
+        for (int i = 0; i < G.nlocal(); i++) v[i] = G.mem[i]->side[side].n;
+        return PHJ_OK;
+    }
+    phj_ctx* c = G.mem[0];
+    MemberBufs& B = G.buf[0];
+    PHJ_HIP(shell, hipSetDevice(c->device));
+    PHJ_TRY(ensure(c, B.cnt, 16 + static_cast<size_t>(G.world) * 8));
+    auto* d = static_cast<uint64_t*>(B.cnt.p);
+    const uint64_t mine = c->side[side].n;
+    PHJ_HIP(shell, hipMemcpyAsync(d, &mine, 8, hipMemcpyHostToDevice, c->stream));
+    PHJ_NCCL(shell, rccl().AllGather(d, d + 2, 1, ncclUint64, G.comm[0], c->stream));
+    PHJ_HIP(shell, hipMemcpyAsync(v.data(), d + 2, static_cast<size_t>(G.world) * 8, hipMemcpyDeviceToHost, c->stream));
+    PHJ_HIP(shell, hipStreamSynchronize(c->stream));
+    return PHJ_OK;
+}
+
+uint64_t total(const std::vector<uint64_t>& v) {
+    uint64_t t = 0;
+    for (uint64_t x : v) t += x;
+    return t;
+}
+
+// ---- the radix join step of one member ----
+
+// All-gather of `elems` int64 per rank from B.send into B.recv, on the member's
+// current launch stream (aux). `ok` = this member packed its block; with the
+// local exchange every member reaches the barrier even after an error, and
+// nobody copies when any member failed (its block may not exist).
+int allgather_blocks(Group& G, int i, uint64_t elems, bool ok) {
+    phj_ctx* c = G.mem[i];
+    MemberBufs& B = G.buf[i];
+    if (G.kind == Xchg::kRccl) {
+        if (!ok) return PHJ_ERR_STATE;
+        PHJ_NCCL(c, rccl().AllGather(B.send.p, B.recv.p, elems, ncclInt64, G.comm[i], c->ks));
+        c->since_ev++;
+        return PHJ_OK;
+    }
+    if (ok && hipEventRecord(B.packed, c->ks) != hipSuccess) ok = false;
+    if (!ok) G.failed.store(1);
+    G.barrier->wait();
+    if (G.failed.load()) return ok ? set_err(c, PHJ_ERR_STATE, "another member failed") : PHJ_ERR_STATE;
+    for (int h = 0; h < G.nlocal(); h++) {
+        phj_ctx* ch = G.mem[h];
+        char* dst = static_cast<char*>(B.recv.p) + static_cast<size_t>(h) * elems * 8;
+        PHJ_HIP(c, hipStreamWaitEvent(c->ks, G.buf[h].packed, 0));
+        if (ch->device == c->device)
+            PHJ_HIP(c, hipMemcpyAsync(dst, G.buf[h].send.p, elems * 8, hipMemcpyDeviceToDevice, c->ks));
+        else
+            PHJ_HIP(c, hipMemcpyPeerAsync(dst, c->device, G.buf[h].send.p, ch->device, elems * 8, c->ks));
+    }
+    c->since_ev++;
+    return PHJ_OK;
+}
+
+// Sum of the members' device counts: RCCL all-reduce on the main stream into
+// B.cnt, or (local) the host adds the members' counts afterwards.
+int allreduce_count(Group& G, int i, const void* local_count) {
+    phj_ctx* c = G.mem[i];
+    MemberBufs& B = G.buf[i];
+    if (G.kind == Xchg::kRccl) {
+        PHJ_NCCL(c, rccl().AllReduce(local_count, B.cnt.p, 1, ncclUint64, ncclSum, G.comm[i], c->stream));
+    } else {
+        PHJ_HIP(c, hipMemcpyAsync(B.cnt.p, local_count, 8, hipMemcpyDeviceToDevice, c->stream));
+    }
+    c->since_ev++;
+    return PHJ_OK;
+}
+
+int read_count(phj_ctx* c, const DevBuf& b, uint64_t* out) {
+    unsigned long long h = 0;
+    PHJ_HIP(c, hipMemcpyAsync(&h, b.p, 8, hipMemcpyDeviceToHost, c->stream));
+    PHJ_HIP(c, hipStreamSynchronize(c->stream));
+    *out = h;
+    return PHJ_OK;
+}
+
+int member_alloc_radix(Group& G, int i, const Plan& pl) {
+    phj_ctx* c = G.mem[i];
+    MemberBufs& B = G.buf[i];
+    uint64_t maxn = 0;
+    for (uint64_t x : G.n[PHJ_SIDE_BUILD]) maxn = std::max(maxn, x);
+    const PackLayout L = pack_layout(maxn, pl.Ppad);
+    PHJ_TRY(ensure(c, B.send, L.elems * 8));
+    PHJ_TRY(ensure(c, B.recv, static_cast<size_t>(G.world) * L.elems * 8));
+    PHJ_TRY(ensure(c, B.cnt, 16 + static_cast<size_t>(G.world) * 8));
+    if (!B.packed) PHJ_HIP(c, hipEventCreateWithFlags(&B.packed, hipEventDisableTiming));
+    return PHJ_OK;
+}
+
+// Build segments of the gathered blocks (keys only, bounds).
+void gathered_segments(const Group& G, int i, const PackLayout& L, uint32_t P, phj_partitioned* segs) {
+    const int64_t* base = static_cast<const int64_t*>(G.buf[i].recv.p);
+    for (int g = 0; g < G.world; g++) {
+        segs[g] = phj_partitioned{};
+        segs[g].keys = base + static_cast<size_t>(g) * L.elems;
+        segs[g].payloads = nullptr;
+        segs[g].bounds = reinterpret_cast<const uint32_t*>(base + static_cast<size_t>(g) * L.elems + L.maxn);
+        segs[g].n = G.n[PHJ_SIDE_BUILD][g];
+        segs[g].num_partitions = P;
+    }
+}
+
+int member_prepare_radix(Group& G, int i, const Plan& pl) {
+    phj_ctx* c = G.mem[i];
+    PHJ_HIP(c, hipSetDevice(c->device));
+    PHJ_TRY(member_alloc_radix(G, i, pl));
+    struct DryScope {
+        phj_ctx* c;
+        ~DryScope() { c->dry = false; }
+    } scope{c};
+    c->dry = true;
+    PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, pl));
+    PHJ_TRY(partition_side(c, PHJ_SIDE_BUILD, pl));
+    uint64_t maxn = 0;
+    for (uint64_t x : G.n[PHJ_SIDE_BUILD]) maxn = std::max(maxn, x);
+    const PackLayout L = pack_layout(maxn, pl.Ppad);
+    std::vector<phj_partitioned> segs(G.world);
+    gathered_segments(G, i, L, pl.Ppad, segs.data());
+    hipEvent_t b0, b1, p1;
+    PHJ_TRY(build_and_probe(c, pl, G.world, segs.data(), &b0, &b1, &p1));
+    PHJ_HIP(c, hipStreamSynchronize(c->stream));
+    return PHJ_OK;
+}
+
+int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
+    phj_ctx* c = G.mem[i];
+    MemberBufs& B = G.buf[i];
+    std::memset(r, 0, sizeof(*r));
+    uint64_t maxn = 0;
+    for (uint64_t x : G.n[PHJ_SIDE_BUILD]) maxn = std::max(maxn, x);
+    const PackLayout L = pack_layout(maxn, pl.Ppad);
+    const uint32_t P = pl.Ppad;
+    SideState& R = c->side[PHJ_SIDE_BUILD];
+    hipEvent_t t0 = nullptr, x0 = nullptr, x1 = nullptr, t1, b0, b1, p1, te;
+    // up to the exchange every step runs even after an error (no early
+    // return): the local exchange's barrier must see every member
+    int rc = hipSetDevice(c->device) == hipSuccess ? PHJ_OK : set_err(c, PHJ_ERR_HIP, "hipSetDevice");
+    if (rc == PHJ_OK) {
+        reset_timers(c);
+        rc = member_alloc_radix(G, i, pl);
+    }
+    if (rc == PHJ_OK) rc = mark(c, &t0);
+    if (rc == PHJ_OK && hipStreamWaitEvent(c->aux, t0, 0) != hipSuccess) rc = set_err(c, PHJ_ERR_HIP, "wait t0");
+    // R shard, pack and all-gather on the aux stream (S goes beside them)
+    c->ks = c->aux;
+    if (rc == PHJ_OK) rc = partition_side(c, PHJ_SIDE_BUILD, pl);
+    if (rc == PHJ_OK && R.n &&
+        hipMemcpyAsync(B.send.p, R.view.keys, R.n * 8, hipMemcpyDeviceToDevice, c->ks) != hipSuccess)
+        rc = set_err(c, PHJ_ERR_HIP, "pack keys");
+    if (rc == PHJ_OK &&
+        hipMemcpyAsync(static_cast<int64_t*>(B.send.p) + L.maxn, R.view.bounds, (static_cast<size_t>(P) + 1) * 4,
+                       hipMemcpyDeviceToDevice, c->ks) != hipSuccess)
+        rc = set_err(c, PHJ_ERR_HIP, "pack bounds");
+    c->since_ev += 2;
+    if (rc == PHJ_OK) rc = mark(c, &x0);
+    if (rc == PHJ_OK) rc = timer_begin(c, "exchange", static_cast<uint64_t>(G.world - 1) * L.elems * 8);
+    const int rx = allgather_blocks(G, i, L.elems, rc == PHJ_OK);
+    if (rc == PHJ_OK) rc = rx;
+    if (rc == PHJ_OK) rc = timer_end(c);
+    if (rc == PHJ_OK) rc = mark(c, &x1);
+    c->ks = c->stream;
+    PHJ_TRY(rc);
+    // S shard on the main stream, concurrently with R and the exchange
+    PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, pl));
+    PHJ_HIP(c, hipStreamWaitEvent(c->stream, x1, 0));
+    PHJ_TRY(mark(c, &t1));
+    std::vector<phj_partitioned> segs(G.world);
+    gathered_segments(G, i, L, P, segs.data());
+    PHJ_TRY(build_and_probe(c, pl, G.world, segs.data(), &b0, &b1, &p1));
+    PHJ_TRY(allreduce_count(G, i, c->count.p));
+    PHJ_TRY(mark(c, &te));
+    uint64_t m = 0;
+    PHJ_TRY(read_count(c, B.cnt, &m));
+    r->matches = m;
+    r->partition_ms = elapsed(c, t0, t1);
+    r->build_ms = elapsed(c, b0, b1);
+    r->probe_ms = elapsed(c, b1, p1);
+    if (c->last_fused) {
+        const double t = elapsed(c, b0, p1), fb = fused_build_fraction(c);
+        r->build_ms = t * fb;
+        r->probe_ms = t * (1.0 - fb);
+    }
+    r->exchange_ms = elapsed(c, x0, x1);
+    r->total_ms = elapsed(c, t0, te);
+    r->num_partitions = P;
+    const uint64_t nRall = total(G.n[PHJ_SIDE_BUILD]);
+    r->algorithmic_bytes = partition_bytes(pl, R.n) + partition_bytes(pl, c->side[PHJ_SIDE_PROBE].n) + nRall * 8 +
+                           c->side[PHJ_SIDE_PROBE].n * 8;
+    return fill_timers(c, r);
+}
+
+// ---- the NoPartitioning step of one member: replicate R, build, probe ----
+
+int member_nopart(Group& G, int i, const phj_join_params* p, phj_join_result* r, bool dry) {
+    phj_ctx* c = G.mem[i];
+    MemberBufs& B = G.buf[i];
+    std::memset(r, 0, sizeof(*r));
+    const std::vector<uint64_t>& nr = G.n[PHJ_SIDE_BUILD];
+    const uint64_t nRall = total(nr);
+    SideState& R = c->side[PHJ_SIDE_BUILD];
+    const phj_tuple* shard = R.rel;
+    const uint64_t shard_n = R.n;
+    struct Restore {   // the member keeps its R shard as its build relation
+        SideState& R;
+        const phj_tuple* rel;
+        uint64_t n;
+        ~Restore() {
+            R.rel = rel;
+            R.n = n;
+            R.partitioned = false;
+        }
+    } restore{R, shard, shard_n};
+    // no early return before the local exchange's barrier (see member_radix)
+    int rc = hipSetDevice(c->device) == hipSuccess ? PHJ_OK : set_err(c, PHJ_ERR_HIP, "hipSetDevice");
+    if (rc == PHJ_OK) {
+        reset_timers(c);
+        rc = ensure(c, B.full, std::max<uint64_t>(1, nRall) * sizeof(phj_tuple));
+    }
+    if (rc == PHJ_OK) rc = ensure(c, B.cnt, 16 + static_cast<size_t>(G.world) * 8);
+    if (rc == PHJ_OK && !B.packed && hipEventCreateWithFlags(&B.packed, hipEventDisableTiming) != hipSuccess)
+        rc = set_err(c, PHJ_ERR_HIP, "hipEventCreate");
+    auto* full = static_cast<phj_tuple*>(B.full.p);
+    if (dry) {
+        PHJ_TRY(rc);
+        R.rel = full;
+        R.n = nRall;
+        c->dry = true;
+        rc = join_nopart(c, p, r);
+        c->dry = false;
+        if (rc == PHJ_OK) PHJ_HIP(c, hipStreamSynchronize(c->stream));
+        return rc;
+    }
+    hipEvent_t t0 = nullptr, t1, te;
+    if (rc == PHJ_OK) rc = mark(c, &t0);
+    if (rc == PHJ_OK) rc = timer_begin(c, "exchange", (nRall - shard_n) * sizeof(phj_tuple));
+    if (G.kind == Xchg::kRccl) {
+        PHJ_TRY(rc);
+        // all-gather-v: one broadcast per root, grouped, straight into the
+        // contiguous relation (no padding, no compaction)
+        uint64_t off = 0;
+        PHJ_NCCL(c, rccl().GroupStart());
+        for (int g = 0; g < G.world; g++) {
+            if (nr[g]) {
+                const ncclResult_t e = rccl().Broadcast(g == G.rank0 + i ? static_cast<const void*>(shard) : nullptr,
+                                                        full + off, nr[g] * 2, ncclInt64, g, G.comm[i], c->stream);
+                if (e != ncclSuccess && rc == PHJ_OK)
+                    rc = set_err(c, PHJ_ERR_HIP, std::string("ncclBroadcast: ") + rccl().GetErrorString(e));
+            }
+            off += nr[g];
+        }
+        PHJ_NCCL(c, rccl().GroupEnd());
+        c->since_ev++;
+    } else {
+        // the shards are resident and read-only: after the barrier every member
+        // copies them all (their relations were bound before the join)
+        if (rc != PHJ_OK) G.failed.store(1);
+        G.barrier->wait();
+        if (G.failed.load()) return rc != PHJ_OK ? rc : set_err(c, PHJ_ERR_STATE, "another member failed");
+        uint64_t off = 0;
+        for (int h = 0; h < G.nlocal(); h++) {
+            phj_ctx* ch = G.mem[h];
+            const void* src = h == i ? static_cast<const void*>(shard)
+                                     : static_cast<const void*>(G.mem[h]->side[PHJ_SIDE_BUILD].rel);
+            if (nr[h]) {
+                if (ch->device == c->device)
+                    PHJ_HIP(c, hipMemcpyAsync(full + off, src, nr[h] * sizeof(phj_tuple), hipMemcpyDeviceToDevice,
+                                              c->stream));
+                else
+                    PHJ_HIP(c, hipMemcpyPeerAsync(full + off, c->device, src, ch->device, nr[h] * sizeof(phj_tuple),
+                                                  c->stream));
+            }
+            off += nr[h];
+        }
+        c->since_ev++;
+    }
+    PHJ_TRY(rc);
+    PHJ_TRY(timer_end(c));
+    PHJ_TRY(mark(c, &t1));
+    R.rel = full;
+    R.n = nRall;
+    R.partitioned = false;
+    // join_nopart resets nothing: its timers follow the exchange timer
+    phj_join_result jr{};
+    PHJ_TRY(join_nopart(c, p, &jr));
+    PHJ_TRY(allreduce_count(G, i, c->count.p));
+    PHJ_TRY(mark(c, &te));
+    uint64_t m = 0;
+    PHJ_TRY(read_count(c, B.cnt, &m));
+    *r = jr;
+    r->matches = m;
+    r->exchange_ms = elapsed(c, t0, t1);
+    r->total_ms = elapsed(c, t0, te);
+    return PHJ_OK;
+}
+
+// The member whose step took longest reports the phases (as the reference
+// reports the slowest worker, RadixCluster/HashJoin.hpp:63-87); the count is
+// the all-reduced (or, local, summed) total.
+void merge_results(Group& G, phj_join_result* r) {
+    int slow = 0;
+    for (int i = 1; i < G.nlocal(); i++)
+        if (G.res[i].total_ms > G.res[slow].total_ms) slow = i;
+    *r = G.res[slow];
+    if (G.kind == Xchg::kLocal) {
+        uint64_t m = 0;
+        for (const phj_join_result& x : G.res) m += x.matches;
+        r->matches = m;
+    }
+}
+
+int group_join(phj_ctx* shell, const phj_join_params* p, phj_join_result* r, bool dry) {
+    Group& G = *shell->group;
+    G.res.assign(G.nlocal(), phj_join_result{});
+    G.failed.store(0);
+    if (p->algo == PHJ_ALGO_NO_PARTITIONING) {
+        if (total(G.n[PHJ_SIDE_BUILD]) == 0)   // LinearProbing.hpp:295-299
+            return set_err(shell, PHJ_ERR_INVALID,
+                           "LinearProbingHashTable::LinearProbingHashTable: numberOfObjects must be greater than zero.");
+        PHJ_TRY(for_members(shell, G, [&](int i) { return member_nopart(G, i, p, &G.res[i], dry); }));
+        if (!dry) merge_results(G, r);
+        return PHJ_OK;
+    }
+    if (p->algo != PHJ_ALGO_RADIX) return set_err(shell, PHJ_ERR_INVALID, "Unrecognized join algorithm");
+    if (G.world > kMaxSegs) return set_err(shell, PHJ_ERR_RANGE, "at most 16 ranks");
+    Plan pl;
+    PHJ_TRY(make_plan(shell, p, pl));
+    const uint32_t requested = pl.Ppad;
+    // every rank plans for the GLOBAL build side (the gathered segments), so all
+    // ranks partition by the same function
+    refine_plan(G.mem[0], pl, total(G.n[PHJ_SIDE_BUILD]));
+    if (dry) return for_members(shell, G, [&](int i) { return member_prepare_radix(G, i, pl); });
+    PHJ_TRY(for_members(shell, G, [&](int i) { return member_radix(G, i, pl, &G.res[i]); }));
+    merge_results(G, r);
+    r->num_partitions = requested;
+    return PHJ_OK;
+}
+
+int group_create(int ngpus, const int* devs, uint32_t flags, int world, int rank0, const uint8_t* unique_id,
+                 phj_ctx** out) {
+    *out = nullptr;
+    auto* G = new Group();
+    G->world = world;
+    G->rank0 = rank0;
+    G->kind = (flags & PHJ_CTX_LOCAL) ? Xchg::kLocal : Xchg::kRccl;
+    phj_ctx* shell = new phj_ctx();
+    shell->group = G;
+    shell->device = devs[0];
+    auto fail = [&](int code, const std::string& msg) {
+        std::fprintf(stderr, "phj_ctx_create: %s\n", msg.c_str());
+        group_destroy(G);
+        shell->group = nullptr;
+        delete shell;
+        return code;
+    };
+    for (int i = 0; i < ngpus; i++) {
+        phj_ctx* c = nullptr;
+        const int rc = ctx_create_device(devs[i], &c);
+        if (rc != PHJ_OK) return fail(rc, "device " + std::to_string(devs[i]) + " unavailable");
+        G->mem.push_back(c);
+        G->buf.emplace_back();
+    }
+    if (G->kind == Xchg::kLocal) {
+        if (world != ngpus) return fail(PHJ_ERR_INVALID, "the local exchange needs every rank in this process");
+    } else {
+        for (int i = 0; i < ngpus; i++)
+            for (int j = 0; j < i; j++)
+                if (devs[i] == devs[j])
+                    return fail(PHJ_ERR_INVALID, "RCCL needs distinct devices (PHJ_CTX_LOCAL rehearses repeated ones)");
+        RcclApi& api = rccl();
+        if (!api.loaded) return fail(PHJ_ERR_HIP, api.err);
+        G->comm.assign(ngpus, nullptr);
+        ncclResult_t e;
+        if (world == ngpus) {
+            e = api.CommInitAll(G->comm.data(), ngpus, devs);
+        } else {
+            ncclUniqueId id;
+            std::memcpy(&id, unique_id, sizeof(id));
+            if (hipSetDevice(devs[0]) != hipSuccess) return fail(PHJ_ERR_HIP, "hipSetDevice");
+            e = api.CommInitRank(&G->comm[0], world, id, rank0);
+        }
+        if (e != ncclSuccess) return fail(PHJ_ERR_HIP, std::string("RCCL communicator: ") + api.GetErrorString(e));
+    }
+    if (ngpus > 1) {
+        G->threads.reset(new MemberThreads(ngpus));
+        G->barrier.reset(new Barrier(ngpus));
+    }
+    for (int s = 0; s < 2; s++) G->n[s].assign(world, 0);
+    *out = shell;
+    return PHJ_OK;
+}
+
+// ---- relation calls on a group: the process's rows, split over its members ----
+
+int group_upload(phj_ctx* shell, int side, const phj_tuple* host, uint64_t n) {
+    Group& G = *shell->group;
+    PHJ_TRY(for_members(shell, G, [&](int i) {
+        uint64_t lo, hi;
+        shard_range(n, i, G.nlocal(), &lo, &hi);
+        return phj_relation_upload(G.mem[i], side, host ? host + lo : nullptr, hi - lo);
+    }));
+    return exchange_sizes(shell, G, side);
+}
+
+int group_generate(phj_ctx* shell, int side, uint64_t n, uint64_t first_index,
+                   const std::function<int(phj_ctx*, uint64_t, uint64_t)>& gen) {
+    Group& G = *shell->group;
+    PHJ_TRY(for_members(shell, G, [&](int i) {
+        uint64_t lo, hi;
+        shard_range(n, i, G.nlocal(), &lo, &hi);
+        return gen(G.mem[i], hi - lo, first_index + lo);
+    }));
+    return exchange_sizes(shell, G, side);
+}
+
+int group_download(phj_ctx* shell, int side, phj_tuple* host, uint64_t n) {
+    Group& G = *shell->group;
+    uint64_t have = 0;
+    for (phj_ctx* c : G.mem) have += c->side[side].n;
+    if (n > have) return set_err(shell, PHJ_ERR_INVALID, "download larger than the relation");
+    uint64_t off = 0;
+    for (phj_ctx* c : G.mem) {
+        const uint64_t k = std::min<uint64_t>(n - off, c->side[side].n);
+        if (k) {
+            const int rc = phj_relation_download(c, side, host + off, k);
+            if (rc != PHJ_OK) return set_err(shell, rc, c->err);
+        }
+        off += k;
+    }
+    return PHJ_OK;
+}
+
+}  // namespace

@@ -71,6 +71,8 @@ struct GpuConfiguration {
     bool GenerateOnDevice = false;
     double TableRatio = 0.0;         // NoPartitioning slots per tuple (0: default)
     bool Materialize = false;        // --materialize on: Run() returns the joined rows (phj_join_materialize)
+    std::vector<int> Devices;        // --gpus N / --devices a,b,..: the context's devices (empty: {Device})
+    uint32_t ContextFlags = 0;       // --exchange rccl|local: PHJ_CTX_EXCHANGE / PHJ_CTX_LOCAL
 };
 
 struct Configuration {

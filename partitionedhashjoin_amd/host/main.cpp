@@ -14,6 +14,8 @@
 //   --hash-seed S         hasher seed (default: random, as the reference)
 //   --generate host|device  where the relations are generated (default host)
 //   --table-ratio X       no-partitioning: table slots per build tuple
+//   --gpus N | --devices a,b,..  several devices (multi-GPU join over RCCL)
+//   --exchange rccl|local  force the multi-GPU path (RCCL world of one / device copies)
 #include <cstdlib>
 #include <cstring>
 #include <iostream>
@@ -61,7 +63,12 @@ const char* kHelp =
     "  --hash-seed arg                     Hasher seed (default: random).\n"
     "  --generate arg (=host)              host | device.\n"
     "  --table-ratio arg                   No-partitioning table slots per build tuple.\n"
-    "  --materialize arg (=off)            on | off: return the joined rows (Table<JoinedTuple>).\n";
+    "  --materialize arg (=off)            on | off: return the joined rows (Table<JoinedTuple>).\n"
+    "  --gpus arg (=1)                     Devices --device .. --device+N-1: range-sharded relations,\n"
+    "                                      RCCL exchange of the partitioned build side.\n"
+    "  --devices arg                       Explicit device list a,b,... (instead of --gpus).\n"
+    "  --exchange arg                      rccl | local: force the multi-GPU path (rccl on one device is\n"
+    "                                      an RCCL world of one; local = device copies, devices may repeat).\n";
 
 // --materialize on: the rows Run() returned (count, and a checksum of their
 // columns so a caller can compare runs without the rows themselves)
@@ -89,7 +96,7 @@ Common::Configuration parseArguments(int argc, char** argv) {
     static const std::map<std::string, std::string> shortNames = {
         {"-u", "unit"}, {"-o", "output"}, {"-f", "filename"}, {"-p", "partitions"}, {"-h", "help"}};
     static const std::set<std::string> known = {"help", "primary", "secondary", "skew", "log", "join", "format",
-                                                "unit", "output", "filename", "partitions", "device", "hash",
+                                                "unit", "output", "filename", "partitions", "device", "gpus", "devices", "exchange", "hash",
                                                 "radix-bits", "seed", "hash-seed", "generate", "table-ratio",
                                                 "materialize"};
     Common::Configuration c{};
@@ -169,6 +176,33 @@ Common::Configuration parseArguments(int argc, char** argv) {
                 throw std::invalid_argument("the argument ('" + vm["generate"] + "') for option '--generate' is invalid");
         }
         if (vm.count("table-ratio")) c.GpuConfig.TableRatio = parse_number<double>("table-ratio", vm["table-ratio"]);
+        if (vm.count("gpus") && vm.count("devices"))
+            throw std::invalid_argument("--gpus and --devices are mutually exclusive");
+        if (vm.count("gpus")) {
+            const int n = parse_number<int>("gpus", vm["gpus"]);
+            if (n < 1 || n > 16) throw std::invalid_argument("--gpus takes 1..16");
+            for (int i = 0; i < n; i++) c.GpuConfig.Devices.push_back(c.GpuConfig.Device + i);
+        }
+        if (vm.count("devices")) {
+            std::string v = vm["devices"];
+            size_t pos = 0;
+            while (pos <= v.size()) {
+                const size_t comma = v.find(',', pos);
+                const std::string item = v.substr(pos, comma == std::string::npos ? std::string::npos : comma - pos);
+                c.GpuConfig.Devices.push_back(parse_number<int>("devices", item));
+                if (comma == std::string::npos) break;
+                pos = comma + 1;
+            }
+            if (c.GpuConfig.Devices.empty() || c.GpuConfig.Devices.size() > 16)
+                throw std::invalid_argument("--devices takes 1..16 device ids");
+        }
+        if (vm.count("exchange")) {
+            if (vm["exchange"] == "rccl") c.GpuConfig.ContextFlags = PHJ_CTX_EXCHANGE;
+            else if (vm["exchange"] == "local") c.GpuConfig.ContextFlags = PHJ_CTX_LOCAL;
+            else throw std::invalid_argument("the argument ('" + vm["exchange"] + "') for option '--exchange' is invalid");
+        }
+        if (c.GpuConfig.Materialize && (c.GpuConfig.Devices.size() > 1 || c.GpuConfig.ContextFlags))
+            throw std::invalid_argument("--materialize on runs on one device");
         // validateParsedConfiguration (src/Arguments.hpp:7-18)
         c.OutputConfig.Validate();
         c.OutputFormatConfig.Validate();
@@ -213,7 +247,12 @@ int main(int argc, char** argv) {
     LOG(logger, Common::info) << "Starting running tests.";
     std::shared_ptr<Gpu::Device> device;
     try {
-        device = std::make_shared<Gpu::Device>(configuration.GpuConfig.Device);
+        const auto& g = configuration.GpuConfig;
+        if (g.Devices.size() > 1 || g.ContextFlags)
+            device = std::make_shared<Gpu::Device>(g.Devices.empty() ? std::vector<int>{g.Device} : g.Devices,
+                                                   g.ContextFlags);
+        else
+            device = std::make_shared<Gpu::Device>(g.Devices.empty() ? g.Device : g.Devices[0]);
     } catch (std::exception& e) {
         LOG(logger, Common::error) << "No usable HIP device: " << e.what();
         return 1;

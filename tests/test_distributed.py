@@ -129,6 +129,15 @@ def _free_port():
         return s.getsockname()[1]
 
 
+def test_library_shard_range_is_the_documented_split():
+    # phj_shard_range (host-only C ABI) = rows [n*r/G, (n*(r+1))/G), exact for any n
+    for n in (0, 1, 7, 10_000_000, 2**40 + 3, 2**63):
+        for w in (1, 2, 3, 7, 8, 16):
+            for r in range(w):
+                assert phj.shard_range(n, r, w) == ((n * r) // w, (n * (r + 1)) // w)
+    assert phj.shard_range(10, 3, 2) == (0, 0)   # out of range rank: empty
+
+
 def test_shard_ranges_cover_exactly():
     for n in (0, 1, 7, 10_000_000):
         for w in (1, 2, 3, 8):

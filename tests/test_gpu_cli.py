@@ -72,3 +72,23 @@ def test_cli_materialize_rows(tmp_path, join):
                 + S[:, 1].astype(np.uint64) * np.uint64(7)).sum(dtype=np.uint64))
     assert int(res["device"]["rows"]) == int(res["device"]["matches"]) == nS
     assert int(res["device"]["rows_checksum"]) == want
+
+
+@pytest.mark.parametrize("devs,join", [
+    (("--exchange", "rccl"), "radix-partitioning"),            # RCCL world of one (phj_ctx_create_ex)
+    (("--exchange", "rccl"), "no-partitioning"),
+    (("--exchange", "local", "--devices", "0,0,0"), "radix-partitioning"),   # 3 ranks on one GPU
+    (("--exchange", "local", "--devices", "0,0"), "no-partitioning"),
+])
+def test_cli_multi_device_context(tmp_path, devs, join):
+    # the multi-GPU join through the reference's own entry point (phjoin ->
+    # Gpu::HashJoiner::Run -> multi-device phj_ctx): same count, reference
+    # JSON, plus the device object's gpus / exchange_us
+    nR, nS, skew, seed = 200_000, 3_000_000, 1.05, 99
+    res, log = run_cli(tmp_path, "--primary", str(nR), "--secondary", str(nS), "--skew", str(skew),
+                       "--seed", str(seed), "--join", join, *devs)
+    assert int(res["device"]["matches"]) == nS
+    ndev = len(devs[3].split(",")) if len(devs) > 2 else 1
+    assert int(res["device"]["gpus"]) == ndev
+    assert "exchange_us" in res["device"]
+    assert list(res["results"]) == ["partition", "build", "probe"]

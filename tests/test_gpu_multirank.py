@@ -1,148 +1,110 @@
-"""Multi-rank HIP path on one GPU: two ranks share cuda:0 over gloo (RCCL
-refuses two ranks on one device), so the real HipShardEngine pack /
-all-gather / multi-segment join / count all-reduce run end to end."""
-import os
-import socket
+"""The multi-GPU join behind the C ABI (csrc/phj_group.h) on one GPU.
 
+* PHJ_CTX_LOCAL: 2-3 members on device 0 driven by their own threads, the
+  exchange done by device copies (RCCL refuses two ranks per device): the
+  whole multi-member step (range shards, R partition + pack, gather,
+  multi-segment join, count sum; replicated NoPartitioning build) runs.
+* PHJ_CTX_EXCHANGE: the same step with the RCCL collectives on a world of one
+  (ncclCommInitAll), and phj_ctx_create_rank with a unique id (ncclCommInitRank,
+  the size all-gather of the multi-process path).
+The 8-GPU bench runs exactly this code with more ranks.
+
+Workloads have a real miss fraction: R holds keys [1 + off, |R| + off], S is
+Zipf over [1, |R|], so the S keys below 1 + off miss (the hottest keys).
+"""
+import numpy as np
 import pytest
-import torch
-import torch.distributed as dist
-import torch.multiprocessing as mp
+
+import partitionedhashjoin_amd as phj
+from partitionedhashjoin_amd.distributed import generate_shards, shard_range
+from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
 
+SEED = 0x1234_5678_9ABC_DEF1
+PARAMS = [("radix-8+8-murmur3", phj.radix_params((8, 8), hash=phj.HASH_MURMUR3, seed=SEED)),
+          ("radix-mod1024-xxh3", phj.radix_params(num_partitions=1024, hash=phj.HASH_XXH3, seed=SEED)),
+          ("nopart-xxh3", phj.nopart_params(hash=phj.HASH_XXH3, seed=SEED))]
 
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
 
-
-def _worker(rank, world, port, nR, nS, alpha, out):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    try:
-        import partitionedhashjoin_amd as phj
-        from partitionedhashjoin_amd.distributed import HipShardEngine, distributed_join
-        from partitionedhashjoin_amd.distributed import shard_range
-        eng = HipShardEngine(0)
-        # R holds keys [1 + off, |R| + off], S draws from [1, |R|]: S keys below
-        # 1 + off miss, so the expected count is the S keys in [1 + off, |R|]
-        off = nR // 3
-        rlo, rhi = shard_range(nR, rank, world)
-        slo, shi = shard_range(nS, rank, world)
-        eng.ctx_r.generate_sequential(0, rhi - rlo, 1 + off, rlo)
-        eng.ctx.generate_zipf(1, shi - slo, alpha, 1, nR, 77, slo)
-        eng.share_build()
-        expect_local = eng.ctx.count_in_range(1, 1 + off, nR)
-        for _ in range(2):   # a second step reuses every buffer
-            res = distributed_join(eng, phj.radix_params((8, 8)), nR, nS, rank, world, dist)
-        out[rank] = (res.matches, expect_local, res.local_matches)
-    finally:
-        dist.destroy_process_group()
+def _generate(ctx, nR, nS, alpha, off, rank=0, world=1):
+    generate_shards(ctx, nR, nS, alpha, 77, rank, world, start=1 + off)
+    return ctx.count_in_range(phj.SIDE_PROBE, 1 + off, nR)
 
 
 @pytest.mark.parametrize("world", [2, 3])
-def test_hip_engine_multirank_on_one_gpu(world):
-    nR, nS = 300_001, 4_000_003
-    mgr = mp.Manager()
-    out = mgr.dict()
-    mp.spawn(_worker, args=(world, _free_port(), nR, nS, 1.25, out), nprocs=world)
-    expect = sum(out[r][1] for r in range(world))
-    assert 0 < expect < nS
-    assert {out[r][0] for r in range(world)} == {expect}
-    # each rank's local count is exactly its own S shard's matches
-    assert all(out[r][2] == out[r][1] for r in range(world))
+def test_local_group_on_one_gpu(world):
+    nR, nS, off = 300_001, 4_000_003, 100_000
+    with phj.Context(devices=[0] * world, flags=phj.CTX_LOCAL) as g:
+        assert g.info() == (world, 0, world)
+        expect = _generate(g, nR, nS, 1.25, off)
+        assert 0 < expect < nS
+        for name, p in PARAMS:
+            for _ in range(2):   # a second step reuses every buffer
+                r = g.join(p)
+                assert r.matches == expect, name
+            assert r.total_ms > 0 and r.exchange_ms >= 0
+            assert "exchange" in {t for t, _, _ in r.timers()}, name
 
 
-def test_single_rank_generation_matches_sharded_generation():
-    import partitionedhashjoin_amd as phj
-    from partitionedhashjoin_amd.distributed import shard_range
+def test_local_group_matches_oracle_on_host_relations():
+    # host relations range-sharded on upload; adversarial keys
+    rng = np.random.default_rng(5)
+    R = np.stack([rng.integers(-50_000, 50_000, 70_001, dtype=np.int64), np.arange(70_001)], axis=1)
+    S = np.stack([rng.integers(-100_000, 100_000, 900_007, dtype=np.int64), np.arange(900_007)], axis=1)
+    expect = O.semijoin_count(R, S)
+    with phj.Context(devices=[0, 0, 0], flags=phj.CTX_LOCAL) as g:
+        g.upload(phj.SIDE_BUILD, R)
+        g.upload(phj.SIDE_PROBE, S)
+        assert np.array_equal(g.download(phj.SIDE_PROBE), S)
+        for name, p in PARAMS:
+            g.prepare(p)
+            assert g.join(p).matches == expect, name
+
+
+def test_group_shards_concatenate_to_the_single_device_relation():
     n = 4096 * 5 + 123
-    with phj.Context(0) as full:
-        full.generate_zipf(1, n, 1.05, 1, 10_000, 9)
-        whole = full.download(1)
-        parts = []
-        for r in range(3):
-            lo, hi = shard_range(n, r, 3)
-            full.generate_zipf(1, hi - lo, 1.05, 1, 10_000, 9, lo)
-            parts.append(full.download(1))
-    import numpy as np
-    assert np.array_equal(whole, np.concatenate(parts))
+    with phj.Context(0) as one, phj.Context(devices=[0, 0, 0], flags=phj.CTX_LOCAL) as g:
+        one.generate_zipf(1, n, 1.05, 1, 10_000, 9)
+        g.generate_zipf(1, n, 1.05, 1, 10_000, 9)
+        assert np.array_equal(one.download(1), g.download(1))
+        # and a shard generated on its own is the same rows
+        lo, hi = shard_range(n, 1, 3)
+        one.generate_zipf(1, hi - lo, 1.05, 1, 10_000, 9, lo)
+        assert np.array_equal(one.download(1), g.download(1)[lo:hi])
 
 
-def _nccl_worker(rank, port, nR, nS, out):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    torch.cuda.set_device(0)
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
-    try:
-        import partitionedhashjoin_amd as phj
-        from partitionedhashjoin_amd.distributed import HipShardEngine, distributed_join
-        eng = HipShardEngine(0)
-        off = nR // 4
-        eng.ctx_r.generate_sequential(0, nR, 1 + off, 0)
-        eng.ctx.generate_zipf(1, nS, 1.05, 1, nR, 5, 0)
-        eng.share_build()
-        expect = eng.ctx.count_in_range(1, 1 + off, nR)
-        got = [distributed_join(eng, phj.radix_params((8, 8)), nR, nS, 0, 1, dist,
-                                force_exchange=True).matches for _ in range(3)]
-        out[0] = (got, expect)
-    finally:
-        dist.destroy_process_group()
+def test_building_blocks_refused_on_several_local_devices():
+    with phj.Context(devices=[0, 0], flags=phj.CTX_LOCAL) as g:
+        g.upload(phj.SIDE_PROBE, np.zeros((10, 2), dtype=np.int64))
+        with pytest.raises(phj.PhjError, match="multi-device"):
+            g.partition(phj.SIDE_PROBE, phj.radix_params((4, 0)))
+        with pytest.raises(phj.PhjError, match="single-device"):
+            g.join_materialize(phj.radix_params((4, 0)))
 
 
-def test_rccl_exchange_branch_world_one():
-    """The N>1 step (pack, asynchronous RCCL all-gather issued from the R
-    stream, S issued from the second host thread, work.wait, multi-segment
-    join, RCCL all-reduce) over the real nccl backend on a world of one: the
-    8-GPU bench runs exactly this code with more ranks."""
-    nR, nS = 1_000_003, 20_000_001
-    mgr = mp.Manager()
-    out = mgr.dict()
-    mp.spawn(_nccl_worker, args=(_free_port(), nR, nS, out), nprocs=1)
-    got, expect = out[0]
-    assert 0 < expect < nS
-    assert got == [expect] * 3
+def test_rccl_world_of_one_group():
+    nR, nS, off = 1_000_003, 20_000_001, 250_000
+    with phj.Context(devices=[0], flags=phj.CTX_EXCHANGE) as g:
+        expect = _generate(g, nR, nS, 1.05, off)
+        assert 0 < expect < nS
+        for name, p in PARAMS:
+            got = [g.join(p).matches for _ in range(3)]
+            assert got == [expect] * 3, name
 
 
-def _np_worker(rank, world, port, backend, nR, nS, out):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    if backend == "nccl":
-        torch.cuda.set_device(0)
-        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
-    else:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-    try:
-        import partitionedhashjoin_amd as phj
-        from partitionedhashjoin_amd.distributed import HipShardEngine, distributed_join_nopart, shard_range
-        eng = HipShardEngine(0)
-        off = nR // 3
-        rlo, rhi = shard_range(nR, rank, world)
-        slo, shi = shard_range(nS, rank, world)
-        eng.ctx_r.generate_sequential(0, rhi - rlo, 1 + off, rlo)
-        eng.ctx.generate_zipf(1, shi - slo, 1.25, 1, nR, 31, slo)
-        eng.share_build()
-        expect_local = eng.ctx.count_in_range(1, 1 + off, nR)
-        for _ in range(2):
-            res = distributed_join_nopart(eng, phj.nopart_params(), nR, nS, rank, world, dist,
-                                          force_exchange=True)
-        out[rank] = (res.matches, expect_local, res.local_matches)
-    finally:
-        dist.destroy_process_group()
-
-
-@pytest.mark.parametrize("backend,world", [("gloo", 2), ("gloo", 3), ("nccl", 1)])
-def test_nopart_replicated_build_multirank(backend, world):
-    """NoPartitioning over range shards: all-gather of the R shards, global
-    table per rank, local S probe, count all-reduce."""
-    nR, nS = 300_001, 4_000_003
-    mgr = mp.Manager()
-    out = mgr.dict()
-    mp.spawn(_np_worker, args=(world, _free_port(), backend, nR, nS, out), nprocs=world)
-    expect = sum(out[r][1] for r in range(world))
-    assert 0 < expect < nS
-    assert {out[r][0] for r in range(world)} == {expect}
-    assert all(out[r][2] == out[r][1] for r in range(world))
+def test_rccl_rank_context_world_of_one():
+    # phj_ctx_create_rank: ncclCommInitRank from a unique id, the collective
+    # size exchange on every relation call, then the member step
+    nR, nS, off = 500_009, 6_000_011, 3
+    uid = phj.comm_unique_id()
+    assert len(uid) == 128
+    with phj.Context.rank(0, 1, 0, uid) as ctx:
+        assert ctx.info() == (1, 0, 1)
+        expect = _generate(ctx, nR, nS, 1.25, off, rank=0, world=1)
+        assert 0 < expect < nS
+        for name, p in PARAMS:
+            assert ctx.join(p).matches == expect, name
+        # a one-device rank context also takes the building blocks
+        v = ctx.partition(phj.SIDE_PROBE, phj.radix_params((8, 8)))
+        assert v.n == nS

@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(lib, s), s
     from partitionedhashjoin_amd import _capi
     assert sorted(_capi.EXPORTED) == syms
-    assert lib.phj_abi_version() == 1
+    assert lib.phj_abi_version() == _capi.ABI_VERSION == 2
 
 
 def test_no_device_fails_loudly():
