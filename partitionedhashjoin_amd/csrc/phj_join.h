@@ -30,6 +30,7 @@
 #include <stdint.h>
 
 #include "phj_hash.h"
+#include "phj_pow.h"
 #include "phj_partition.h"
 
 namespace phj {
@@ -1190,10 +1191,15 @@ __device__ __forceinline__ double lcg_next(int64_t& st) {
 }
 
 // Thread per 4096-tuple batch; Zipf::generate (Zipf.cpp:14-56) per sample.
-// Writes global rows [first, first + n) to out[0, n).
+// Writes global rows [first, first + n) to out[0, n). Bit-exact with the host
+// generator: glibc's pow (phj_pow.h) and no contracted arithmetic (the
+// reference's x86-64 build has no FMA), so every sample and every batch's LCG
+// stream equal the host's.
 __global__ __launch_bounds__(kBlock) void k_gen_zipf(longlong2* out, uint64_t n, double alpha,
                                                      uint64_t card, int64_t correction,
                                                      uint64_t seed, uint64_t first) {
+#pragma clang fp contract(off)
+    using glibc_pow::pow;
     const uint64_t b = first / kGenBatch + static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
     const uint64_t lo = b * kGenBatch;
     const uint64_t end = first + n;
