@@ -67,6 +67,11 @@ struct Tuning {
     int np_nt = 1;        // NoPartitioning probe: 1 nontemporal S loads, 2 also the bucket loads
     int np_items = 4;     // NoPartitioning probe: S keys per thread per round (4 or 8)
     bool np_region = true;   // NoPartitioning build: partition R into table regions, build each in LDS
+    int np_hot = 1;          // NoPartitioning probe: hot-key LDS cache (0 off, 1 from np_hot_min probes)
+    uint64_t np_hot_min = 1u << 20;
+    uint32_t np_hot_samples = 65536;
+    int np_diag = 0;         // PHJ_NP_DIAG: diagnostic probe floors (timing only, wrong counts)
+    int np_coop = 0;         // NoPartitioning probe: four lanes per bucket (k_np_probe_coop; measured slower)
 };
 
 int env_int(const char* name, int dflt) {
@@ -143,6 +148,7 @@ struct phj_ctx {
     DevBuf scan_partials, prep, tkeys, tpays, toffs, gcursor, items, count, biglist;
     DevBuf np_tab, np_pays;
     DevBuf np_ovf, np_ovfb, np_ovfn;   // region build: overflow tuples, their start buckets, count
+    DevBuf np_hot, np_img;             // hot-key cache: sampled keys + count, LDS image (keys, states)
     DevBuf fitems, split;
     DevBuf mat_mark, mat_cnt, mat_rows;   // materialised join: per-probe match, block offsets, rows
     uint64_t mat_n = 0;   // fused join: item slots; wave clocks {build, probe} since the last timer reset
@@ -1104,6 +1110,12 @@ int join_nopart(phj_ctx* c, const phj_join_params* p, phj_join_result* r, uint32
     PHJ_TRY(ensure(c, c->np_tab, static_cast<size_t>(nb) * sizeof(NPBucket)));
     PHJ_TRY(ensure(c, c->np_pays, static_cast<size_t>(nb) * kNPSlots * 8));
     PHJ_TRY(ensure(c, c->count, 8));
+    // hot-key cache for the count probe (not the materialising one)
+    const bool hot = !marks && c->tune.np_hot > 0 && S.n >= c->tune.np_hot_min;
+    if (hot) {
+        PHJ_TRY(ensure(c, c->np_hot, static_cast<size_t>(c->tune.np_hot_samples) * 8 + kHotCand * 16 + 16));
+        PHJ_TRY(ensure(c, c->np_img, kHotSlots * 9));
+    }
     Plan rp;
     if (g.rbits) {
         PHJ_TRY(ensure(c, c->np_ovf, R.n * 16));
@@ -1119,9 +1131,31 @@ int join_nopart(phj_ctx* c, const phj_join_params* p, phj_join_result* r, uint32
         if (c->dry) return partition_side(c, PHJ_SIDE_BUILD, rp);
     }
     if (c->dry) return PHJ_OK;
-    hipEvent_t e0, e1, e2;
+    hipEvent_t e0, e1, e2, es = nullptr;
     const uint32_t nR = static_cast<uint32_t>(R.n);
     PHJ_TRY(mark(c, &e0));
+    const uint32_t nsamp = c->tune.np_hot_samples;
+    auto* samp = static_cast<int64_t*>(c->np_hot.p);
+    auto* cand = reinterpret_cast<longlong2*>(samp + nsamp);
+    auto* cand_n = reinterpret_cast<uint32_t*>(cand + kHotCand);
+    if (hot) {
+        // the sample reads only S: it runs on the aux stream beside the build
+        PHJ_HIP(c, hipStreamWaitEvent(c->aux, e0, 0));
+        PHJ_HIP(c, hipMemsetAsync(cand_n, 0, 4, c->aux));
+        const auto* S_rel = reinterpret_cast<const longlong2*>(S.rel);
+        hipLaunchKernelGGL(k_np_hot_gather, dim3((nsamp + kBlock - 1) / kBlock), dim3(kBlock), 0, c->aux, S_rel, S.n,
+                           nsamp, samp);
+        if (p->hash == PHJ_HASH_MURMUR3)
+            hipLaunchKernelGGL(k_np_hot_count<kMurmur3>, dim3(kHotClasses), dim3(kBlock), 0, c->aux, samp, nsamp,
+                               p->hash_seed, cand, cand_n);
+        else
+            hipLaunchKernelGGL(k_np_hot_count<kXXH3>, dim3(kHotClasses), dim3(kBlock), 0, c->aux, samp, nsamp,
+                               p->hash_seed, cand, cand_n);
+        PHJ_LAUNCHED(c, "k_np_hot_count");
+        es = next_event(c);
+        if (!es) return set_err(c, PHJ_ERR_HIP, "hipEventCreate failed");
+        PHJ_HIP(c, hipEventRecord(es, c->aux));
+    }
     if (g.rbits) {
         // the partition is part of the build (its R.* timers show it)
         PHJ_TRY(partition_side(c, PHJ_SIDE_BUILD, rp));
@@ -1179,7 +1213,59 @@ int join_nopart(phj_ctx* c, const phj_join_params* p, phj_join_result* r, uint32
             if (c->tune.np_nt == 2) PHJ_NP_PROBE(HKV, 4, 2); else if (c->tune.np_nt) PHJ_NP_PROBE(HKV, 4, 1); else PHJ_NP_PROBE(HKV, 4, 0); \
         }                                                                        \
     } while (0)
-        if (marks) {
+        if (c->tune.np_diag == 4 && !marks) {
+            const uint32_t dg = static_cast<uint32_t>(std::min<uint64_t>((S.n + 256ull * kBlock - 1) / (256ull * kBlock), 8192));
+            hipLaunchKernelGGL((k_np_probe_coop<kXXH3, 4, 1, 4>), dim3(dg), dim3(kBlock), 0, c->ks, S_rel, S.n, tab, g, p->hash_seed, cnt);
+        } else if (c->tune.np_coop && !marks) {
+            // one round = 4 keys per lane; a workgroup of 4 waves takes 1024 keys
+            const uint64_t per = 4ull * kBlock;
+            const uint32_t cg = static_cast<uint32_t>(std::min<uint64_t>((S.n + per - 1) / per, 8192));
+            if (p->hash == PHJ_HASH_MURMUR3) {
+                if (c->tune.np_items == 8) hipLaunchKernelGGL((k_np_probe_coop<kMurmur3, 8, 1>), dim3(cg), dim3(kBlock), 0, c->ks, S_rel, S.n, tab, g, p->hash_seed, cnt);
+                else hipLaunchKernelGGL((k_np_probe_coop<kMurmur3, 4, 1>), dim3(cg), dim3(kBlock), 0, c->ks, S_rel, S.n, tab, g, p->hash_seed, cnt);
+            } else {
+                if (c->tune.np_items == 8) hipLaunchKernelGGL((k_np_probe_coop<kXXH3, 8, 1>), dim3(cg), dim3(kBlock), 0, c->ks, S_rel, S.n, tab, g, p->hash_seed, cnt);
+                else hipLaunchKernelGGL((k_np_probe_coop<kXXH3, 4, 1>), dim3(cg), dim3(kBlock), 0, c->ks, S_rel, S.n, tab, g, p->hash_seed, cnt);
+            }
+            if (hot) PHJ_HIP(c, hipStreamWaitEvent(c->ks, es, 0));
+        } else if (c->tune.np_diag >= 1 && c->tune.np_diag <= 3 && !marks) {
+            const uint32_t dg = static_cast<uint32_t>(std::min<uint64_t>((S.n + 4ull * kBlock - 1) / (4ull * kBlock), 8192));
+            if (c->tune.np_diag == 1)
+                hipLaunchKernelGGL((k_np_probe_diag<kXXH3, 1>), dim3(dg), dim3(kBlock), 0, c->ks, S_rel, S.n, tab, g, p->hash_seed, cnt);
+            else if (c->tune.np_diag == 2)
+                hipLaunchKernelGGL((k_np_probe_diag<kXXH3, 2>), dim3(dg), dim3(kBlock), 0, c->ks, S_rel, S.n, tab, g, p->hash_seed, cnt);
+            else
+                hipLaunchKernelGGL((k_np_probe_diag<kXXH3, 3>), dim3(dg), dim3(kBlock), 0, c->ks, S_rel, S.n, tab, g, p->hash_seed, cnt);
+            if (hot) PHJ_HIP(c, hipStreamWaitEvent(c->ks, es, 0));
+        } else if (hot) {
+            PHJ_HIP(c, hipStreamWaitEvent(c->ks, es, 0));
+            auto* img_keys = static_cast<int64_t*>(c->np_img.p);
+            auto* img_st = reinterpret_cast<uint8_t*>(img_keys + kHotSlots);
+            const void* kfn;
+            if (p->hash == PHJ_HASH_MURMUR3) {
+                hipLaunchKernelGGL(k_np_hot_resolve<kMurmur3>, dim3(1), dim3(kBlock), 0, c->ks, cand, cand_n, tab, g,
+                                   p->hash_seed, img_keys, img_st);
+                kfn = reinterpret_cast<const void*>(&k_np_probe_hot<kMurmur3, 4, 1>);
+            } else {
+                hipLaunchKernelGGL(k_np_hot_resolve<kXXH3>, dim3(1), dim3(kBlock), 0, c->ks, cand, cand_n, tab, g,
+                                   p->hash_seed, img_keys, img_st);
+                kfn = reinterpret_cast<const void*>(&k_np_probe_hot<kXXH3, 4, 1>);
+            }
+            PHJ_LAUNCHED(c, "k_np_hot_resolve");
+            int per_cu = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, kBlock, 0) != hipSuccess || per_cu < 1)
+                per_cu = 4;
+            const uint64_t want = (S.n + 4ull * kBlock - 1) / (4ull * kBlock);
+            const uint32_t hg = static_cast<uint32_t>(std::max<uint64_t>(
+                1, std::min<uint64_t>(want, static_cast<uint64_t>(per_cu) * c->num_cus)));
+            const auto* img_k = img_keys;
+            const auto* img_s = img_st;
+            uint64_t nS64 = S.n;
+            uint64_t seed = p->hash_seed;
+            void* kargs[] = {const_cast<longlong2**>(&S_rel), &nS64, const_cast<NPBucket**>(&tab), &g, &seed,
+                             const_cast<int64_t**>(&img_k), const_cast<uint8_t**>(&img_s), &cnt};
+            PHJ_HIP(c, hipLaunchKernel(kfn, dim3(hg), dim3(kBlock), kargs, 0, c->ks));
+        } else if (marks) {
             const uint32_t mg = static_cast<uint32_t>(std::min<uint64_t>((S.n + 4 * kBlock - 1) / (4 * kBlock), 8192));
             if (p->hash == PHJ_HASH_MURMUR3)
                 hipLaunchKernelGGL((k_np_probe_mark<kMurmur3>), dim3(mg), dim3(kBlock), 0, c->ks, S_rel, S.n, tab, g,
@@ -1359,6 +1445,11 @@ int ctx_create_device(int device, phj_ctx** out) {
     c->tune.np_nt = std::min(2, std::max(0, env_int("PHJ_NP_NT", 1)));
     c->tune.np_items = env_int("PHJ_NP_ITEMS", 4) == 8 ? 8 : 4;
     c->tune.np_region = env_int("PHJ_NP_REGION", 1) != 0;
+    c->tune.np_hot = env_int("PHJ_NP_HOT", 1);
+    c->tune.np_hot_min = static_cast<uint64_t>(std::max(0, env_int("PHJ_NP_HOT_MIN", 1 << 20)));
+    c->tune.np_hot_samples = static_cast<uint32_t>(std::max(256, env_int("PHJ_NP_HOT_SAMPLES", 65536)));
+    c->tune.np_diag = env_int("PHJ_NP_DIAG", 0);
+    c->tune.np_coop = env_int("PHJ_NP_COOP", 0);
     c->tune.p1_slots = env_int("PHJ_P1_SLOTS", 0);
     c->tune.p1_tps = std::max(1, env_int("PHJ_P1_TPS", static_cast<int>(kTilesPerShard)));
     c->tune.p1_min_tiles = std::max(0, env_int("PHJ_P1_MIN_TILES", 32768));
@@ -1470,7 +1561,7 @@ void phj_ctx_destroy(phj_ctx* c) {
             free_buf(*b);
     }
     for (DevBuf* b : {&c->scan_partials, &c->prep, &c->tkeys, &c->tpays, &c->toffs, &c->gcursor, &c->items, &c->biglist,
-                      &c->count, &c->np_tab, &c->np_pays, &c->np_ovf, &c->np_ovfb, &c->np_ovfn, &c->fitems, &c->split, &c->mat_mark, &c->mat_cnt, &c->mat_rows})
+                      &c->count, &c->np_tab, &c->np_pays, &c->np_ovf, &c->np_ovfb, &c->np_ovfn, &c->np_hot, &c->np_img, &c->fitems, &c->split, &c->mat_mark, &c->mat_cnt, &c->mat_rows})
         free_buf(*b);
     for (hipEvent_t e : c->evpool) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->stream);

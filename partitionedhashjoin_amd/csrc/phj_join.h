@@ -1070,6 +1070,311 @@ __global__ __launch_bounds__(kBlock) void k_np_probe(const longlong2* S, uint64_
 }
 
 // ---------------------------------------------------------------------------
+// NoPartitioning hot-key cache. Under Zipf a few keys
+// take most probes (s = 1.05 over 10M keys: the top key 8.7 %, the top ~1000
+// about half); their buckets are L2 hits, but every probe of one key lands on
+// the same cache line and L2 channel, which serialises. The probe therefore
+// answers the hottest keys from a small LDS table first: a strided sample of S
+// is counted (k_np_hot_sample), keys seen >= kHotMinCount times are looked up
+// once in the global table after the build (k_np_hot_resolve) and every probe
+// workgroup copies the resulting image (keys + {empty, absent, present}) into
+// LDS (k_np_probe_hot). The sample only chooses WHICH keys are cached; each
+// cached answer is the global table's own lookup, so the count is unchanged.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kHotSlots = 4096;     // direct-mapped LDS table slots
+constexpr uint32_t kHotCand = 4096;      // sampled candidates (key, count)
+constexpr uint32_t kHotClasses = 64;     // sampler workgroups (a hash class each)
+constexpr uint32_t kHotSampleSlots = 2048;
+constexpr uint32_t kHotMinCount = 3;
+
+__device__ __forceinline__ uint32_t hot_slot(uint64_t h) { return static_cast<uint32_t>(h >> 20) & (kHotSlots - 1); }
+
+// A strided sample of the probe keys, gathered contiguously (one load per lane).
+__global__ __launch_bounds__(kBlock) void k_np_hot_gather(const longlong2* S, uint64_t nS, uint32_t nsamp,
+                                                          int64_t* samp) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= nsamp) return;
+    const uint64_t stride = nS / nsamp > 0 ? nS / nsamp : 1;
+    const uint64_t idx = static_cast<uint64_t>(i) * stride;
+    samp[i] = idx < nS ? S[idx].x : S[0].x;
+}
+
+// Count the sampled keys per hash class (workgroup c takes the keys with
+// (h >> 58) == c); append (key, count) for those seen >= kHotMinCount times.
+template <int HK>
+__global__ __launch_bounds__(kBlock) void k_np_hot_count(const int64_t* samp, uint32_t nsamp, uint64_t seed,
+                                                         longlong2* cand, uint32_t* cand_n) {
+    constexpr unsigned long long kEmpty = 0x8000000000000000ull;   // a sampled INT64_MIN is skipped
+    __shared__ unsigned long long lkey[kHotSampleSlots];
+    __shared__ uint32_t lcnt[kHotSampleSlots];
+    for (uint32_t i = threadIdx.x; i < kHotSampleSlots; i += kBlock) {
+        lkey[i] = kEmpty;
+        lcnt[i] = 0;
+    }
+    __syncthreads();
+    const uint32_t c = blockIdx.x;
+    for (uint32_t i = threadIdx.x; i < nsamp; i += kBlock) {
+        const unsigned long long key = static_cast<unsigned long long>(samp[i]);
+        const uint64_t h = hash64<HK>(key, seed);
+        if (static_cast<uint32_t>(h >> 58) != c || key == kEmpty) continue;
+        uint32_t sl = static_cast<uint32_t>(h >> 32) & (kHotSampleSlots - 1);
+        for (uint32_t t = 0; t < kHotSampleSlots; t++) {
+            const unsigned long long prev = atomicCAS(&lkey[sl], kEmpty, key);
+            if (prev == kEmpty || prev == key) {
+                atomicAdd(&lcnt[sl], 1u);
+                break;
+            }
+            sl = (sl + 1) & (kHotSampleSlots - 1);
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < kHotSampleSlots; i += kBlock) {
+        if (lcnt[i] >= kHotMinCount) {
+            const uint32_t o = atomicAdd(cand_n, 1u);
+            if (o < kHotCand) cand[o] = make_longlong2(static_cast<int64_t>(lkey[i]), lcnt[i]);
+        }
+    }
+}
+
+// One workgroup: a direct-mapped table of the candidates (a slot keeps its
+// most-sampled key), each kept key looked up once in the built table. The
+// image the probe copies: keys[kHotSlots] then state[kHotSlots] (u8: 0 empty,
+// 1 absent from R, 2 present).
+template <int HK>
+__global__ __launch_bounds__(kBlock) void k_np_hot_resolve(const longlong2* cand, const uint32_t* cand_n,
+                                                           const NPBucket* tab, NPHome g, uint64_t seed,
+                                                           int64_t* img_keys, uint8_t* img_state) {
+    __shared__ uint32_t lwin[kHotSlots];
+    for (uint32_t i = threadIdx.x; i < kHotSlots; i += kBlock) lwin[i] = 0;
+    __syncthreads();
+    const uint32_t n = min(*cand_n, kHotCand);
+    for (uint32_t i = threadIdx.x; i < n; i += kBlock) {
+        const longlong2 kc = cand[i];
+        const uint64_t h = hash64<HK>(static_cast<uint64_t>(kc.x), seed);
+        const uint32_t cnt = static_cast<uint32_t>(min<int64_t>(kc.y, 0xffff));
+        atomicMax(&lwin[hot_slot(h)], (cnt << 16) | (i + 1));
+    }
+    __syncthreads();
+    for (uint32_t sl = threadIdx.x; sl < kHotSlots; sl += kBlock) {
+        const uint32_t w = lwin[sl];
+        int64_t key = 0;
+        uint8_t st = 0;
+        if (w) {
+            key = cand[(w & 0xffff) - 1].x;
+            const uint64_t h = hash64<HK>(static_cast<uint64_t>(key), seed);
+            st = np_lookup(tab, g.nb, np_home_r(h, g), key) ? 2 : 1;
+        }
+        img_keys[sl] = key;
+        img_state[sl] = st;
+    }
+}
+
+// k_np_probe with the direct-mapped hot-key LDS table in front: a probe key
+// equal to its slot's key is answered from the slot; the others read their
+// home bucket as before (ITEMS random reads in flight per thread, issued only
+// for the lanes that need them). Persistent grid: each workgroup copies the
+// image once.
+template <int HK, int ITEMS, int NT>
+__global__ __launch_bounds__(kBlock) void k_np_probe_hot(const longlong2* S, uint64_t nS, const NPBucket* tab,
+                                                         NPHome g, uint64_t seed, const int64_t* img_keys,
+                                                         const uint8_t* img_state, unsigned long long* count) {
+    __shared__ int64_t hkey[kHotSlots];
+    __shared__ uint8_t hst[kHotSlots];
+    __shared__ uint32_t red[kWaves];
+    {
+        const longlong2* src = reinterpret_cast<const longlong2*>(img_keys);
+        longlong2* dst = reinterpret_cast<longlong2*>(hkey);
+        for (uint32_t i = threadIdx.x; i < kHotSlots / 2; i += kBlock) dst[i] = src[i];
+        const uint4* s8 = reinterpret_cast<const uint4*>(img_state);
+        uint4* d8 = reinterpret_cast<uint4*>(hst);
+        for (uint32_t i = threadIdx.x; i < kHotSlots / 16; i += kBlock) d8[i] = s8[i];
+    }
+    __syncthreads();
+    const uint32_t nb = g.nb;
+    uint32_t hits = 0;
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kBlock * ITEMS;
+    for (uint64_t base = static_cast<uint64_t>(blockIdx.x) * kBlock * ITEMS; base < nS; base += stride) {
+        int64_t k[ITEMS];
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const uint64_t idx = base + static_cast<uint64_t>(j) * kBlock + threadIdx.x;
+            if constexpr (NT > 0)
+                k[j] = idx < nS ? __builtin_nontemporal_load(&S[idx].x) : 0;
+            else
+                k[j] = idx < nS ? S[idx].x : 0;
+        }
+        uint32_t b[ITEMS];
+        bool cold[ITEMS];
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const uint64_t idx = base + static_cast<uint64_t>(j) * kBlock + threadIdx.x;
+            const uint64_t h = hash64<HK>(static_cast<uint64_t>(k[j]), seed);
+            b[j] = np_home_r(h, g);
+            const uint32_t sl = hot_slot(h);
+            const uint32_t st = hst[sl];
+            const bool hot = st != 0 && hkey[sl] == k[j];
+            cold[j] = idx < nS && !hot;
+            hits += (idx < nS && hot && st == 2) ? 1u : 0u;
+        }
+        // the cold keys' home buckets, all requested before any is compared
+        longlong2 q[ITEMS][4];
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            if (cold[j]) {
+                const longlong2* bp = reinterpret_cast<const longlong2*>(tab + b[j]);
+#pragma unroll
+                for (int w = 0; w < 4; w++) q[j][w] = bp[w];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            if (cold[j]) {
+                const int64_t key = k[j];
+                const uint32_t fill = static_cast<uint32_t>(q[j][3].y);
+                const uint32_t c = fill < kNPSlots ? fill : kNPSlots;
+                const bool hit = (c > 0 && q[j][0].x == key) || (c > 1 && q[j][0].y == key) ||
+                                 (c > 2 && q[j][1].x == key) || (c > 3 && q[j][1].y == key) ||
+                                 (c > 4 && q[j][2].x == key) || (c > 5 && q[j][2].y == key) ||
+                                 (c > 6 && q[j][3].x == key);
+                if (hit)
+                    hits++;
+                else if (fill >= kNPSlots)
+                    hits += np_lookup(tab, nb, b[j] + 1 == nb ? 0 : b[j] + 1, key) ? 1u : 0u;
+            }
+        }
+    }
+    uint32_t x = hits;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_down(x, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (int w = 0; w < kWaves; w++) t += red[w];
+        if (t) atomicAdd(count, t);
+    }
+}
+
+// Cooperative NoPartitioning probe: four lanes read one 64-B bucket (one
+// 16-B part each), so a wave's bucket load instruction touches 16 cache lines
+// instead of 64. Measured on the probe's own access pattern: with one lane per
+// bucket a wave's 4 x ITEMS load instructions each touch 64 lines and the
+// vector L1 (one tag lookup per line per clock) caps the probe at ~1.3 ms for
+// 200M probes even when every bucket is an L2 hit (PHJ_NP_DIAG=2), against
+// 0.46 ms for streaming and hashing S alone (PHJ_NP_DIAG=1). Each wave stages
+// its ITEMS x 64 keys and home buckets in LDS; in load step t the quad g of
+// lanes serves key t * 16 + g; a quad's hit is OR-reduced and counted once.
+// DIAG = 4: every bucket index is replaced by one of 4096 (the L2-hit floor).
+template <int HK, int ITEMS, int NT, int DIAG = 0>
+__global__ __launch_bounds__(kBlock) void k_np_probe_coop(const longlong2* S, uint64_t nS, const NPBucket* tab,
+                                                          NPHome g, uint64_t seed, unsigned long long* count) {
+    constexpr int NK = ITEMS * 64;   // keys per wave per round
+    __shared__ int64_t wkey[kWaves][NK];
+    __shared__ uint32_t wbkt[kWaves][NK];
+    __shared__ uint32_t red[kWaves];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t quad = lane >> 2, part = lane & 3;
+    const uint32_t nb = g.nb;
+    uint32_t hits = 0;
+    const uint64_t wstride = static_cast<uint64_t>(gridDim.x) * kWaves * NK;
+    for (uint64_t base = (static_cast<uint64_t>(blockIdx.x) * kWaves + wv) * NK; base < nS; base += wstride) {
+        // stage: ITEMS coalesced keys per lane, their home buckets (~0u: past the end)
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const uint64_t idx = base + static_cast<uint64_t>(j) * 64 + lane;
+            int64_t k = 0;
+            if (idx < nS) {
+                if constexpr (NT > 0) k = __builtin_nontemporal_load(&S[idx].x);
+                else k = S[idx].x;
+            }
+            const uint64_t h = hash64<HK>(static_cast<uint64_t>(k), seed);
+            uint32_t b = np_home_r(h, g);
+            if constexpr (DIAG == 4) b = static_cast<uint32_t>(h) & 4095u;
+            wkey[wv][j * 64 + lane] = k;
+            wbkt[wv][j * 64 + lane] = idx < nS ? b : ~0u;
+        }
+        __builtin_amdgcn_wave_barrier();
+        // every part of every bucket of the round requested before any compare
+        longlong2 q[4 * ITEMS];
+        int64_t key[4 * ITEMS];
+        uint32_t bk[4 * ITEMS];
+#pragma unroll
+        for (int t = 0; t < 4 * ITEMS; t++) {
+            const uint32_t slot = t * 16 + quad;
+            key[t] = wkey[wv][slot];
+            bk[t] = wbkt[wv][slot];
+            if (bk[t] != ~0u) q[t] = reinterpret_cast<const longlong2*>(tab + bk[t])[part];
+            else q[t] = make_longlong2(0, 0);
+        }
+#pragma unroll
+        for (int t = 0; t < 4 * ITEMS; t++) {
+            // the fill count sits in part 3's second half
+            const uint32_t fill = static_cast<uint32_t>(__shfl(q[t].y, (lane & ~3u) | 3u, 64));
+            const uint32_t c = fill < kNPSlots ? fill : kNPSlots;
+            const uint32_t s0 = 2 * part;
+            bool m = (s0 < c && q[t].x == key[t]) || (part < 3 && s0 + 1 < c && q[t].y == key[t]);
+            uint32_t any = m ? 1u : 0u;
+            any |= static_cast<uint32_t>(__shfl_xor(static_cast<int>(any), 1, 64));
+            any |= static_cast<uint32_t>(__shfl_xor(static_cast<int>(any), 2, 64));
+            if (part == 0 && bk[t] != ~0u) {
+                if (any) hits++;
+                else if (fill >= kNPSlots)   // full home bucket: continue in the next ones (rare)
+                    hits += np_lookup(tab, nb, bk[t] + 1 == nb ? 0 : bk[t] + 1, key[t]) ? 1u : 0u;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    uint32_t x = hits;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_down(x, o, 64);
+    if (lane == 0) red[wv] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (int w = 0; w < kWaves; w++) t += red[w];
+        if (t) atomicAdd(count, t);
+    }
+}
+
+// Diagnostic floors of the probe (PHJ_NP_DIAG, timing only; the count is not
+// the join's): 1 = stream and hash S without any bucket read; 2 = every probe
+// reads one of 4096 buckets (L2 hits spread over the channels); 3 = every
+// probe reads bucket 0 (one L2 line).
+template <int HK, int MODE>
+__global__ __launch_bounds__(kBlock) void k_np_probe_diag(const longlong2* S, uint64_t nS, const NPBucket* tab,
+                                                          NPHome g, uint64_t seed, unsigned long long* count) {
+    constexpr int ITEMS = 4;
+    uint32_t hits = 0;
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kBlock * ITEMS;
+    for (uint64_t base = static_cast<uint64_t>(blockIdx.x) * kBlock * ITEMS; base < nS; base += stride) {
+        int64_t k[ITEMS];
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const uint64_t idx = base + static_cast<uint64_t>(j) * kBlock + threadIdx.x;
+            k[j] = idx < nS ? __builtin_nontemporal_load(&S[idx].x) : 0;
+        }
+        longlong2 q[ITEMS][4];
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const uint64_t h = hash64<HK>(static_cast<uint64_t>(k[j]), seed);
+            const uint32_t b = MODE == 2 ? static_cast<uint32_t>(h) & 4095u : 0u;
+            if constexpr (MODE == 1) {
+                hits += (h & 1023) == 7;
+            } else {
+                const longlong2* bp = reinterpret_cast<const longlong2*>(tab + b);
+#pragma unroll
+                for (int w = 0; w < 4; w++) q[j][w] = bp[w];
+            }
+        }
+        if constexpr (MODE != 1) {
+#pragma unroll
+            for (int j = 0; j < ITEMS; j++) hits += q[j][0].x == k[j] || q[j][2].y == k[j];
+        }
+    }
+    if (hits == 0xffffffffu) atomicAdd(count, 1ull);
+}
+
+// ---------------------------------------------------------------------------
 // Partitioned bucket tables in HBM, for partitions too large for the fused
 // LDS join (the reference's small-P configurations, e.g. -p 32: 312K build
 // tuples per partition). Partition p owns buckets [tob[p], tob[p+1]) of

@@ -63,6 +63,9 @@ SCHEDULES = [
     {"PHJ_NP_NT": "2"},                                         # ... nontemporal bucket loads too
     {"PHJ_NP_ITEMS": "8"},                                      # ... 8 S keys per thread per round
     {"PHJ_NP_REGION": "0"},                                     # ... device-atomic build
+    {"PHJ_NP_HOT": "0"},                                        # ... no hot-key LDS cache
+    {"PHJ_NP_HOT_MIN": "0", "PHJ_NP_HOT_SAMPLES": "4096"},      # ... hot-key cache at every size
+    {"PHJ_NP_COOP": "1"},                                       # ... four lanes per bucket
 ]
 
 CASES = [((8, 8), 0, phj.HASH_MURMUR3), ((11, 0), 0, phj.HASH_XXH3), ((1, 0), 1000, phj.HASH_XXH3),
