@@ -72,6 +72,7 @@ struct Tuning {
     uint32_t np_hot_samples = 65536;
     int np_diag = 0;         // PHJ_NP_DIAG: diagnostic probe floors (timing only, wrong counts)
     int np_coop = 0;         // NoPartitioning probe: four lanes per bucket (k_np_probe_coop; measured slower)
+    int p2probe = 0;         // radix join, 2 passes: the probe side's pass 2 on-chip (k_probe_p1)
 };
 
 int env_int(const char* name, int dflt) {
@@ -114,6 +115,8 @@ struct SideState {
     DevBuf ccur, ctab, tstart;   // chunked pass 1: digit cursors + pool counter, chunk table, pass-2 tile starts
     uint32_t gen = 0;            // chunked pass 1: tag of the current chunk-table entries
     phj_partitioned view{};
+    PassArgs p2{};               // p1_only: the pass-2 tile mapping over the pass-1 output
+    uint32_t nt2 = 0;            // ... and its tile bound
     bool partitioned = false;
     Plan plan;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -636,7 +639,7 @@ uint32_t pass_tile(const phj_ctx* c, uint32_t n, uint32_t nb, bool* wc) {
     return static_cast<uint32_t>(sub * k);
 }
 
-int partition_side(phj_ctx* c, int s, const Plan& pl) {
+int partition_side(phj_ctx* c, int s, const Plan& pl, bool p1_only = false) {
     SideState& S = c->side[s];
     c->scan_scratch = &S.partials;
     if (!S.rel && S.n > 0) return set_err(c, PHJ_ERR_STATE, "relation not bound");
@@ -796,6 +799,14 @@ int partition_side(phj_ctx* c, int s, const Plan& pl) {
             b.dig_wide = dbytes == 2 ? 1u : 0u;
         }
         const uint32_t grid2 = n ? nt2 : 0;
+        if (p1_only) {   // the caller consumes the pass-2 tiles itself (k_probe_p1)
+            S.p2 = b;
+            S.nt2 = grid2;
+            S.view = phj_partitioned{};
+            S.partitioned = false;
+            S.plan = pl;
+            return PHJ_OK;
+        }
         if (wc2)
             PHJ_TRY(launch_pass_wc(c, pl.hk, false, b, grid2, tile2, std::string(tag) + ".p2", n, grid2 * pl.nb2));
         else
@@ -1066,6 +1077,98 @@ int build_and_probe(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned*
     PHJ_LAUNCHED(c, "k_probe");
     PHJ_TRY(timer_end(c));
     PHJ_TRY(mark(c, e_probe1));
+    return PHJ_OK;
+}
+
+// CSR bucket tables (k_build_small / k_build_big) over `nseg` partitioned
+// build segments, keys only, plus the per-partition descriptors of k_probe_p1.
+int build_csr(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned* segs) {
+    const uint32_t P = pl.Ppad;
+    SegList L{};
+    L.nseg = static_cast<uint32_t>(nseg);
+    L.P = P;
+    uint64_t nR = 0;
+    for (int g = 0; g < nseg; g++) {
+        if (segs[g].num_partitions != P) return set_err(c, PHJ_ERR_INVALID, "build segment partition count mismatch");
+        L.seg[g].keys = segs[g].keys;
+        L.seg[g].pays = nullptr;   // the count join tests keys only
+        L.seg[g].bounds = segs[g].bounds;
+        nR += segs[g].n;
+    }
+    if (nR >= (1ull << 32) - 1) return set_err(c, PHJ_ERR_RANGE, "build side above 2^32 tuples");
+    const size_t stride = static_cast<size_t>(P) + 1;
+    PHJ_TRY(ensure(c, c->prep, stride * 2 * 4));
+    PHJ_TRY(ensure(c, c->tkeys, std::max<uint64_t>(1, nR) * 8));
+    const size_t noffs = nR + 2 * static_cast<size_t>(P) + 1;
+    PHJ_TRY(ensure(c, c->toffs, noffs * 4));
+    PHJ_TRY(ensure(c, c->gcursor, noffs * 4));
+    PHJ_TRY(ensure(c, c->biglist, static_cast<size_t>(P) * 4));
+    PHJ_TRY(ensure(c, c->count, 16));
+    PHJ_TRY(ensure(c, c->items, static_cast<size_t>(P) * 16));   // desc[P]
+    if (c->dry) return scan_u32(c, nullptr, P + 1, 2, static_cast<uint32_t>(stride));
+    uint32_t* prep = static_cast<uint32_t*>(c->prep.p);
+    hipLaunchKernelGGL(k_csr_prep, dim3((P + 1 + kBlock - 1) / kBlock), dim3(kBlock), 0, c->ks, L, prep);
+    PHJ_LAUNCHED(c, "k_csr_prep");
+    PHJ_TRY(scan_u32(c, prep, P + 1, 2, static_cast<uint32_t>(stride)));
+    const uint32_t* tkb = prep;
+    const uint32_t* tob = prep + stride;
+    hipLaunchKernelGGL(k_csr_desc, dim3((P + kBlock - 1) / kBlock), dim3(kBlock), 0, c->ks, tkb, tob, P,
+                       static_cast<uint4*>(c->items.p));
+    PHJ_LAUNCHED(c, "k_csr_desc");
+    BuildArgs ba{};
+    ba.L = L;
+    ba.tkb = tkb;
+    ba.tob = tob;
+    ba.tkeys = static_cast<int64_t*>(c->tkeys.p);
+    ba.tpays = nullptr;
+    ba.toffs = static_cast<uint32_t*>(c->toffs.p);
+    ba.gcursor = static_cast<uint32_t*>(c->gcursor.p);
+    ba.seed = pl.seed;
+    ba.biglist = static_cast<uint32_t*>(c->biglist.p);
+    ba.bigcount = static_cast<uint32_t*>(c->count.p) + 2;
+    PHJ_HIP(c, hipMemsetAsync(ba.bigcount, 0, 4, c->ks));
+    const uint64_t expect = (nR + P - 1) / P;
+    const uint32_t kcap = expect * 2 > 8192 ? 256u : std::max<uint32_t>(256, next_pow2_u32(static_cast<uint32_t>(expect * 2)));
+    ba.ocap = std::min<uint32_t>(2048, std::max<uint32_t>(64, kcap));
+    const uint32_t sgrid = (P + kWaves - 1) / kWaves;
+    const size_t slds = static_cast<size_t>(ba.ocap) * 4 * kWaves;
+    if (pl.hk == kMurmur3)
+        hipLaunchKernelGGL((k_build_small<kMurmur3, kBuildKPL>), dim3(sgrid), dim3(kBlock), slds, c->ks, ba);
+    else
+        hipLaunchKernelGGL((k_build_small<kXXH3, kBuildKPL>), dim3(sgrid), dim3(kBlock), slds, c->ks, ba);
+    PHJ_LAUNCHED(c, "k_build_small");
+    ba.ocap = 16384;
+    const size_t blds = 64 + static_cast<size_t>(ba.ocap) * 4;
+    if (pl.hk == kMurmur3)
+        hipLaunchKernelGGL((k_build_big<kMurmur3>), dim3(256), dim3(kBlock), blds, c->ks, ba);
+    else
+        hipLaunchKernelGGL((k_build_big<kXXH3>), dim3(256), dim3(kBlock), blds, c->ks, ba);
+    PHJ_LAUNCHED(c, "k_build_big");
+    return PHJ_OK;
+}
+
+// Probe the partitioned-by-pass-1 probe side (partition_side p1_only) against
+// the CSR tables of build_csr; the count lands in c->count.
+int probe_p1(phj_ctx* c, const Plan& pl) {
+    SideState& PS = c->side[PHJ_SIDE_PROBE];
+    PHJ_HIP(c, hipMemsetAsync(c->count.p, 0, 8, c->ks));
+    if (PS.nt2 == 0) return PHJ_OK;
+    P1ProbeArgs pa{};
+    pa.a = PS.p2;
+    pa.a.xcd_remap = c->tune.xcd_remap ? 1u : 0u;
+    const uint32_t grid = pa.a.xcd_remap ? (PS.nt2 + 7) & ~7u : PS.nt2;
+    pa.desc = static_cast<const uint4*>(c->items.p);
+    pa.toffs = static_cast<const uint32_t*>(c->toffs.p);
+    pa.tkeys = static_cast<const int64_t*>(c->tkeys.p);
+    pa.count = static_cast<unsigned long long*>(c->count.p);
+    pa.seed = pl.seed;
+    pa.nb2 = pl.nb2;
+    const size_t lds = probe_p1_lds_bytes(4096, pl.nb2, 8);
+    if (pl.hk == kMurmur3)
+        hipLaunchKernelGGL((k_probe_p1<512, 8, kMurmur3>), dim3(grid), dim3(512), lds, c->ks, pa);
+    else
+        hipLaunchKernelGGL((k_probe_p1<512, 8, kXXH3>), dim3(grid), dim3(512), lds, c->ks, pa);
+    PHJ_LAUNCHED(c, "k_probe_p1");
     return PHJ_OK;
 }
 
@@ -1450,6 +1553,7 @@ int ctx_create_device(int device, phj_ctx** out) {
     c->tune.np_hot_samples = static_cast<uint32_t>(std::max(256, env_int("PHJ_NP_HOT_SAMPLES", 65536)));
     c->tune.np_diag = env_int("PHJ_NP_DIAG", 0);
     c->tune.np_coop = env_int("PHJ_NP_COOP", 0);
+    c->tune.p2probe = env_int("PHJ_P2PROBE", 0);
     c->tune.p1_slots = env_int("PHJ_P1_SLOTS", 0);
     c->tune.p1_tps = std::max(1, env_int("PHJ_P1_TPS", static_cast<int>(kTilesPerShard)));
     c->tune.p1_min_tiles = std::max(0, env_int("PHJ_P1_MIN_TILES", 32768));
@@ -1826,7 +1930,41 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
     SideState& S = c->side[PHJ_SIDE_PROBE];
     const uint32_t requested = pl.Ppad;   // reported; the join may sub-partition
     refine_plan(c, pl, R.n);
+    bool wc_dummy = false;
     hipEvent_t t0, t1, tr, b0, b1, p1;
+    if (c->tune.p2probe && pl.npass == 2 && tile_shape(c, pl.nb2).tile == 4096 && tile_shape(c, pl.nb2).block == 512 &&
+        pass_tile(c, static_cast<uint32_t>(std::min<uint64_t>(S.n, 0xffffffffu)), pl.nb1, &wc_dummy) == 4096) {
+        // S: pass 1 only (its pass 2 runs inside the probe); R: both passes and
+        // its bucket tables on the aux stream, beside S
+        PHJ_TRY(mark(c, &t0));
+        PHJ_HIP(c, hipStreamWaitEvent(c->aux, t0, 0));
+        PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, pl, true));
+        c->ks = c->aux;
+        int rc = partition_side(c, PHJ_SIDE_BUILD, pl);
+        if (rc == PHJ_OK) rc = mark(c, &b0);
+        if (rc == PHJ_OK) rc = timer_begin(c, "build", R.n * 8 * 2);
+        if (rc == PHJ_OK) rc = build_csr(c, pl, 1, &R.view);
+        if (rc == PHJ_OK) rc = timer_end(c);
+        if (rc == PHJ_OK) rc = mark(c, &tr);
+        c->ks = c->stream;
+        PHJ_TRY(rc);
+        PHJ_HIP(c, hipStreamWaitEvent(c->stream, tr, 0));
+        PHJ_TRY(mark(c, &t1));
+        PHJ_TRY(timer_begin(c, "probe", S.n * (16 + 8)));
+        PHJ_TRY(probe_p1(c, pl));
+        PHJ_TRY(timer_end(c));
+        PHJ_TRY(mark(c, &p1));
+        uint64_t m = 0;
+        PHJ_TRY(get_count(c, &m));
+        r->matches = m;
+        r->partition_ms = elapsed(c, t0, t1);
+        r->build_ms = elapsed(c, b0, tr);
+        r->probe_ms = elapsed(c, t1, p1);
+        r->total_ms = elapsed(c, t0, p1);
+        r->num_partitions = requested;
+        r->algorithmic_bytes = partition_bytes(pl, R.n) + S.n * (16 + 32) + R.n * 16 + S.n * 16;
+        return fill_timers(c, r);
+    }
     // Partition(R) || Partition(S) (HashJoin.hpp:210-216): S (the long one) is
     // issued first on the ctx stream, R beside it on the aux stream
     PHJ_TRY(mark(c, &t0));
