@@ -72,7 +72,7 @@ struct Tuning {
     uint32_t np_hot_samples = 65536;
     int np_diag = 0;         // PHJ_NP_DIAG: diagnostic probe floors (timing only, wrong counts)
     int np_coop = 0;         // NoPartitioning probe: four lanes per bucket (k_np_probe_coop; measured slower)
-    int p2probe = 0;         // radix join, 2 passes: the probe side's pass 2 on-chip (k_probe_p1)
+    int p2probe = 1;         // radix join, 2 passes: the probe side's pass 2 on-chip (k_probe_p1)
 };
 
 int env_int(const char* name, int dflt) {
@@ -1147,6 +1147,15 @@ int build_csr(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned* segs)
     return PHJ_OK;
 }
 
+// phj_join takes the on-chip pass 2 (k_probe_p1, 512 x 4096 tiles) for a
+// 2-pass plan unless PHJ_P2PROBE=0 or a tuning knob changed the tile shape.
+bool use_p2probe(const phj_ctx* c, const Plan& pl, uint64_t nS) {
+    bool wc = false;
+    return c->tune.p2probe && pl.npass == 2 && tile_shape(c, pl.nb2).tile == 4096 && tile_shape(c, pl.nb2).block == 512 &&
+           pass_tile(c, static_cast<uint32_t>(std::min<uint64_t>(nS, 0xffffffffu)), pl.nb1, &wc) == 4096 && !wc &&
+           probe_p1_lds_bytes(4096, pl.nb2, 8) <= 160 * 1024;
+}
+
 // Probe the partitioned-by-pass-1 probe side (partition_side p1_only) against
 // the CSR tables of build_csr; the count lands in c->count.
 int probe_p1(phj_ctx* c, const Plan& pl) {
@@ -1155,8 +1164,6 @@ int probe_p1(phj_ctx* c, const Plan& pl) {
     if (PS.nt2 == 0) return PHJ_OK;
     P1ProbeArgs pa{};
     pa.a = PS.p2;
-    pa.a.xcd_remap = c->tune.xcd_remap ? 1u : 0u;
-    const uint32_t grid = pa.a.xcd_remap ? (PS.nt2 + 7) & ~7u : PS.nt2;
     pa.desc = static_cast<const uint4*>(c->items.p);
     pa.toffs = static_cast<const uint32_t*>(c->toffs.p);
     pa.tkeys = static_cast<const int64_t*>(c->tkeys.p);
@@ -1164,10 +1171,23 @@ int probe_p1(phj_ctx* c, const Plan& pl) {
     pa.seed = pl.seed;
     pa.nb2 = pl.nb2;
     const size_t lds = probe_p1_lds_bytes(4096, pl.nb2, 8);
-    if (pl.hk == kMurmur3)
-        hipLaunchKernelGGL((k_probe_p1<512, 8, kMurmur3>), dim3(grid), dim3(512), lds, c->ks, pa);
+    const int diag = env_int("PHJ_P1_DIAG", 0);
+    const void* kfn;
+    if (diag == 1)
+        kfn = pl.hk == kMurmur3 ? reinterpret_cast<const void*>(&k_probe_p1<512, 8, kMurmur3, 1>)
+                                : reinterpret_cast<const void*>(&k_probe_p1<512, 8, kXXH3, 1>);
     else
-        hipLaunchKernelGGL((k_probe_p1<512, 8, kXXH3>), dim3(grid), dim3(512), lds, c->ks, pa);
+        kfn = pl.hk == kMurmur3 ? reinterpret_cast<const void*>(&k_probe_p1<512, 8, kMurmur3>)
+                                : reinterpret_cast<const void*>(&k_probe_p1<512, 8, kXXH3>);
+    // persistent: as many workgroups as fit the chip at once (a multiple of 8:
+    // XCD x owns tiles [x, x + 1) * ntiles / 8), never many more than tiles
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, 512, lds) != hipSuccess || per_cu < 1) per_cu = 2;
+    per_cu = std::min<int>(per_cu, static_cast<int>(160 * 1024 / lds));
+    const uint32_t want = (PS.nt2 + 7) & ~7u;
+    const uint32_t grid = std::max<uint32_t>(8, std::min<uint32_t>(want, static_cast<uint32_t>(per_cu) * c->num_cus) & ~7u);
+    void* kargs[] = {&pa};
+    PHJ_HIP(c, hipLaunchKernel(kfn, dim3(grid), dim3(512), kargs, lds, c->ks));
     PHJ_LAUNCHED(c, "k_probe_p1");
     return PHJ_OK;
 }
@@ -1553,7 +1573,7 @@ int ctx_create_device(int device, phj_ctx** out) {
     c->tune.np_hot_samples = static_cast<uint32_t>(std::max(256, env_int("PHJ_NP_HOT_SAMPLES", 65536)));
     c->tune.np_diag = env_int("PHJ_NP_DIAG", 0);
     c->tune.np_coop = env_int("PHJ_NP_COOP", 0);
-    c->tune.p2probe = env_int("PHJ_P2PROBE", 0);
+    c->tune.p2probe = env_int("PHJ_P2PROBE", 1);
     c->tune.p1_slots = env_int("PHJ_P1_SLOTS", 0);
     c->tune.p1_tps = std::max(1, env_int("PHJ_P1_TPS", static_cast<int>(kTilesPerShard)));
     c->tune.p1_min_tiles = std::max(0, env_int("PHJ_P1_MIN_TILES", 32768));
@@ -1930,10 +1950,8 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
     SideState& S = c->side[PHJ_SIDE_PROBE];
     const uint32_t requested = pl.Ppad;   // reported; the join may sub-partition
     refine_plan(c, pl, R.n);
-    bool wc_dummy = false;
     hipEvent_t t0, t1, tr, b0, b1, p1;
-    if (c->tune.p2probe && pl.npass == 2 && tile_shape(c, pl.nb2).tile == 4096 && tile_shape(c, pl.nb2).block == 512 &&
-        pass_tile(c, static_cast<uint32_t>(std::min<uint64_t>(S.n, 0xffffffffu)), pl.nb1, &wc_dummy) == 4096) {
+    if (use_p2probe(c, pl, S.n)) {
         // S: pass 1 only (its pass 2 runs inside the probe); R: both passes and
         // its bucket tables on the aux stream, beside S
         PHJ_TRY(mark(c, &t0));
@@ -2017,6 +2035,16 @@ int phj_prepare(phj_ctx* c, const phj_join_params* p) {
     Plan pl;
     PHJ_TRY(make_plan(c, p, pl));
     refine_plan(c, pl, c->side[PHJ_SIDE_BUILD].n);
+    if (use_p2probe(c, pl, c->side[PHJ_SIDE_PROBE].n)) {
+        PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, pl, true));
+        PHJ_TRY(partition_side(c, PHJ_SIDE_BUILD, pl));
+        phj_partitioned rv{};
+        rv.n = c->side[PHJ_SIDE_BUILD].n;
+        rv.num_partitions = pl.Ppad;
+        PHJ_TRY(build_csr(c, pl, 1, &rv));
+        PHJ_HIP(c, hipStreamSynchronize(c->stream));
+        return PHJ_OK;
+    }
     PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, pl));
     PHJ_TRY(partition_side(c, PHJ_SIDE_BUILD, pl));
     phj_partitioned seg{};

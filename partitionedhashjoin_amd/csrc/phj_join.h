@@ -840,193 +840,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KPL <= 2
 }
 
 // ---------------------------------------------------------------------------
-// Probe straight from the pass-1 partitions (PHJ_P2PROBE): the probe side's
-// second partitioning pass runs on-chip instead of through HBM. A pass-2 tile
-// (<= T tuples of one pass-1 partition d1, from the chunked or the stable
-// pass-1 layout) is loaded, sorted by its second digit d2 in LDS exactly as
-// k_scatter sorts it, and then every key probes the prebuilt bucket table of
-// its final partition p = d1 * nb2 + d2 (CSR in HBM, k_build_small over the
-// fully partitioned R) instead of being written out and read back. The
-// per-partition semantics are the reference's (HashJoin.hpp:267-303: build a
-// table per partition, probe it with the partition's S tuples); sorting by d2
-// makes consecutive lanes probe the same small table, so its lines are L1/L2
-// hits. Saved per S tuple: the pass-2 histogram (1 B), the pass-2 write
-// (16 B) and the probe's re-read of the key (8 B).
-// ---------------------------------------------------------------------------
-struct P1ProbeArgs {
-    PassArgs a;               // the pass-2 tile mapping over the pass-1 output (in_keys = AoS tuples)
-    const uint4* desc;        // per final partition: {kb, ob, nbk, m}
-    const uint32_t* toffs;    // bucket offsets (relative to kb), nbk + 1 per partition
-    const int64_t* tkeys;     // keys in bucket order
-    unsigned long long* count;
-    uint64_t seed;
-    uint32_t nb2;             // digits of pass 2 (final partition = d1 * nb2 + d2)
-    uint32_t pad;
-};
-
-// arr: 2 arrays of P+1 entries: m_p and NB_p + 1 (last entries 0), for the
-// CSR tables of k_build_small when no probe work list is needed.
-__global__ __launch_bounds__(kBlock) void k_csr_prep(SegList L, uint32_t* arr) {
-    const uint32_t P = L.P;
-    const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
-    if (p > P) return;
-    const size_t stride = static_cast<size_t>(P) + 1;
-    if (p == P) {
-        arr[P] = 0;
-        arr[stride + P] = 0;
-        return;
-    }
-    uint32_t m = 0;
-    for (uint32_t g = 0; g < L.nseg; g++) m += L.seg[g].bounds[p + 1] - L.seg[g].bounds[p];
-    arr[p] = m;
-    arr[stride + p] = table_buckets(m) + 1;
-}
-
-// desc[p] = {kb, ob, nbk, m} from the scanned table bases.
-__global__ __launch_bounds__(kBlock) void k_csr_desc(const uint32_t* tkb, const uint32_t* tob, uint32_t P,
-                                                     uint4* desc) {
-    const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
-    if (p >= P) return;
-    const uint32_t kb = tkb[p], ob = tob[p];
-    desc[p] = make_uint4(kb, ob, tob[p + 1] - ob - 1, tkb[p + 1] - kb);
-}
-
-template <int BLOCK, int ITEMS, int HK>
-__global__ __launch_bounds__(BLOCK) void k_probe_p1(P1ProbeArgs pa) {
-    constexpr int NW = BLOCK / 64;
-    constexpr int T = BLOCK * ITEMS;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const PassArgs& a = pa.a;
-    const uint32_t nb = a.nbins;
-    int64_t* skey = reinterpret_cast<int64_t*>(smem);
-    uint32_t* shash = reinterpret_cast<uint32_t*>(skey + T);    // high hash word (bucket bits)
-    uint32_t* wcnt = shash + T;                                   // [NW][nb]
-    uint32_t* tmp = wcnt + NW * nb;                               // 16 words
-    const SortedDigits sdig{tmp + 16, nb <= 256};                 // [T]
-    __shared__ uint32_t red[NW];
-
-    const uint32_t tile = tile_id(a);
-    TileLoc L;
-    if (!locate_tile<T>(a, tile, L)) return;
-    const uint32_t d1 = a.tile_seg[tile];
-    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const uint32_t cnt = L.hi - L.lo;
-    for (uint32_t i = tid; i < NW * nb; i += BLOCK) wcnt[i] = 0;
-    int64_t key[ITEMS];
-    const uint32_t wbase = wave * 64 * ITEMS;
-    const longlong2* rel = reinterpret_cast<const longlong2*>(a.in_keys);
-#pragma unroll
-    for (int i = 0; i < ITEMS; i++) {
-        const uint32_t e = wbase + i * 64 + lane;
-        key[i] = e < cnt ? rel[L.lo + e].x : 0;
-    }
-    __syncthreads();
-    uint32_t dig[ITEMS], rank[ITEMS], hh[ITEMS];
-    uint32_t* my = wcnt + wave * nb;
-#pragma unroll
-    for (int i = 0; i < ITEMS; i++) {
-        const uint32_t e = wbase + i * 64 + lane;
-        const bool valid = e < cnt;
-        const uint64_t h = hash64<HK>(static_cast<uint64_t>(key[i]), pa.seed);
-        const uint32_t d = valid ? (static_cast<uint32_t>(q_from_hash(h, a.f) >> a.f.shift) & a.f.dmask) : 0u;
-        hh[i] = static_cast<uint32_t>(h >> 32);
-        const uint64_t peers = match_digit(d, valid, a.nbits);
-        dig[i] = d;
-        rank[i] = 0;
-        if (valid) {
-            const uint32_t before = my[d];
-            const uint64_t lt = peers & lanemask_lt();
-            rank[i] = before + __popcll(lt);
-            if (lt == 0) my[d] = before + __popcll(peers);
-        }
-    }
-    __syncthreads();
-    {
-        const uint32_t dpt = (nb + BLOCK - 1) / BLOCK;
-        const uint32_t d0 = tid * dpt;
-        uint32_t local = 0;
-        for (uint32_t j = 0; j < dpt; j++) {
-            const uint32_t d = d0 + j;
-            if (d < nb) {
-#pragma unroll
-                for (int w = 0; w < NW; w++) local += wcnt[w * nb + d];
-            }
-        }
-        uint32_t total;
-        uint32_t run = block_exclusive_scan_t<NW>(local, tmp, total);
-        for (uint32_t j = 0; j < dpt; j++) {
-            const uint32_t d = d0 + j;
-            if (d < nb) {
-#pragma unroll
-                for (int w = 0; w < NW; w++) {
-                    const uint32_t c = wcnt[w * nb + d];
-                    wcnt[w * nb + d] = run;
-                    run += c;
-                }
-            }
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < ITEMS; i++) {
-        const uint32_t e = wbase + i * 64 + lane;
-        if (e < cnt) {
-            const uint32_t pos = my[dig[i]] + rank[i];
-            skey[pos] = key[i];
-            shash[pos] = hh[i];
-            sdig.put(pos, dig[i]);
-        }
-    }
-    __syncthreads();
-    // probe in sorted order: consecutive lanes mostly share a partition
-    const uint32_t pbase = d1 * pa.nb2;
-    uint32_t hits = 0;
-    uint4 ds[ITEMS];
-    int64_t k2[ITEMS];
-    uint32_t b2[ITEMS];
-#pragma unroll
-    for (int i = 0; i < ITEMS; i++) {
-        const uint32_t k = i * BLOCK + tid;
-        ds[i] = make_uint4(0, 0, 0, 0);
-        if (k < cnt) {
-            k2[i] = skey[k];
-            b2[i] = shash[k];
-            ds[i] = pa.desc[pbase + sdig.get(k)];
-        }
-    }
-    uint32_t o0[ITEMS], o1[ITEMS];
-#pragma unroll
-    for (int i = 0; i < ITEMS; i++) {
-        o0[i] = o1[i] = 0;
-        if (ds[i].w) {   // m > 0
-            const uint32_t b = b2[i] & (ds[i].z - 1u);
-            o0[i] = pa.toffs[ds[i].y + b];
-            o1[i] = pa.toffs[ds[i].y + b + 1];
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < ITEMS; i++) {
-        bool hit = false;
-        for (uint32_t j = o0[i]; j < o1[i] && !hit; j++) hit = pa.tkeys[ds[i].x + j] == k2[i];
-        hits += hit ? 1u : 0u;
-    }
-    uint32_t x = hits;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x += __shfl_down(x, o, 64);
-    if (lane == 0) red[wave] = x;
-    __syncthreads();
-    if (tid == 0) {
-        unsigned long long t = 0;
-        for (int w = 0; w < NW; w++) t += red[w];
-        if (t) atomicAdd(pa.count, t);
-    }
-}
-
-__host__ __device__ constexpr size_t probe_p1_lds_bytes(int T, uint32_t nb, int NW) {
-    return static_cast<size_t>(T) * (8 + 4 + (nb <= 256 ? 1 : 2)) + static_cast<size_t>(nb) * 4 * NW + 64 + 16;
-}
-
-// ---------------------------------------------------------------------------
 // NoPartitioning: global bucketized linear probing.
 // ---------------------------------------------------------------------------
 constexpr int kNPSlots = 7;
@@ -1254,6 +1067,213 @@ __global__ __launch_bounds__(kBlock) void k_np_probe(const longlong2* S, uint64_
         for (int w = 0; w < kWaves; w++) t += red[w];
         if (t) atomicAdd(count, t);
     }
+}
+
+// ---------------------------------------------------------------------------
+// Probe straight from the pass-1 partitions (PHJ_P2PROBE): the probe side's
+// second partitioning pass runs on-chip instead of through HBM. A pass-2 tile
+// (<= T tuples of one pass-1 partition d1, from the chunked or the stable
+// pass-1 layout) is loaded, sorted by its second digit d2 in LDS exactly as
+// k_scatter sorts it, and then every key probes the prebuilt bucket table of
+// its final partition p = d1 * nb2 + d2 (CSR in HBM, k_build_small over the
+// fully partitioned R) instead of being written out and read back. The
+// per-partition semantics are the reference's (HashJoin.hpp:267-303: build a
+// table per partition, probe it with the partition's S tuples); sorting by d2
+// makes consecutive lanes probe the same small table, so its lines are L1/L2
+// hits. Saved per S tuple: the pass-2 histogram (1 B), the pass-2 write
+// (16 B) and the probe's re-read of the key (8 B).
+// ---------------------------------------------------------------------------
+struct P1ProbeArgs {
+    PassArgs a;               // the pass-2 tile mapping over the pass-1 output (in_keys = AoS tuples)
+    const uint4* desc;        // per final partition: {kb, ob, nbk, m}
+    const uint32_t* toffs;    // bucket offsets (relative to kb), nbk + 1 per partition
+    const int64_t* tkeys;     // keys in bucket order
+    unsigned long long* count;
+    uint64_t seed;
+    uint32_t nb2;             // digits of pass 2 (final partition = d1 * nb2 + d2)
+    uint32_t pad;
+};
+
+// arr: 2 arrays of P+1 entries: m_p and NB_p + 1 (last entries 0), for the
+// CSR tables of k_build_small when no probe work list is needed.
+__global__ __launch_bounds__(kBlock) void k_csr_prep(SegList L, uint32_t* arr) {
+    const uint32_t P = L.P;
+    const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+    if (p > P) return;
+    const size_t stride = static_cast<size_t>(P) + 1;
+    if (p == P) {
+        arr[P] = 0;
+        arr[stride + P] = 0;
+        return;
+    }
+    uint32_t m = 0;
+    for (uint32_t g = 0; g < L.nseg; g++) m += L.seg[g].bounds[p + 1] - L.seg[g].bounds[p];
+    arr[p] = m;
+    arr[stride + p] = table_buckets(m) + 1;
+}
+
+// desc[p] = {kb, ob, nbk, m} from the scanned table bases.
+__global__ __launch_bounds__(kBlock) void k_csr_desc(const uint32_t* tkb, const uint32_t* tob, uint32_t P,
+                                                     uint4* desc) {
+    const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+    if (p >= P) return;
+    const uint32_t kb = tkb[p], ob = tob[p];
+    desc[p] = make_uint4(kb, ob, tob[p + 1] - ob - 1, tkb[p + 1] - kb);
+}
+
+// Persistent: XCD x walks the contiguous tile range [x, x + 1) * ntiles / 8
+// (tiles of one pass-1 partition are contiguous, so an XCD's L2 holds the
+// few R tables it is probing), its workgroups round-robin over it, and the
+// next tile's keys load while the current one is probed. The tile is grouped
+// by d2 with one LDS atomic per key (an unstable counting sort: the probe only
+// needs neighbours to share a table); the tile's nb2 table descriptors are
+// staged in LDS. The bucket bits are re-hashed after the grouping. Measured
+// against a one-read table of 64-B buckets (7 keys + fill per bucket, wrapping
+// regions): 1.94 ms against 1.45 for these narrow CSR reads (two 4-B offsets,
+// ~1.2 8-B keys), as in the NoPartitioning probe a lane's four 16-B loads of
+// one bucket cost more than the extra dependent level. DIAG (timing only):
+// 1 = no table reads.
+template <int BLOCK, int ITEMS, int HK, int DIAG = 0>
+__global__ __launch_bounds__(BLOCK) void k_probe_p1(P1ProbeArgs pa) {
+    constexpr int T = BLOCK * ITEMS;
+    constexpr int PB = 4;   // probes in flight per lane per batch
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const PassArgs& a = pa.a;
+    const uint32_t nb = a.nbins;
+    int64_t* skey = reinterpret_cast<int64_t*>(smem);
+    uint4* sdesc = reinterpret_cast<uint4*>(skey + T);            // [nb]
+    uint32_t* cnt_d = reinterpret_cast<uint32_t*>(sdesc + nb);    // [nb] counts, then starts
+    uint32_t* tmp = cnt_d + nb;                                   // 16 words
+    const SortedDigits sdig{tmp + 16, nb <= 256};                 // [T]
+    __shared__ uint32_t red[BLOCK / 64];
+
+    const uint32_t total = a.tile_base[a.nseg];
+    const uint32_t xcd = blockIdx.x & 7u, g8 = gridDim.x >> 3;
+    const uint32_t t_lo = static_cast<uint32_t>(static_cast<uint64_t>(total) * xcd / 8);
+    const uint32_t t_hi = static_cast<uint32_t>(static_cast<uint64_t>(total) * (xcd + 1) / 8);
+    uint32_t tile = t_lo + (blockIdx.x >> 3);
+    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    uint32_t hits = 0;
+    if (tile < t_hi) {
+        const uint32_t wbase = wave * 64 * ITEMS;
+        const longlong2* rel = reinterpret_cast<const longlong2*>(a.in_keys);
+        int64_t key[ITEMS];
+        uint32_t cnt = 0, d1 = 0;
+        auto load = [&](uint32_t t, uint32_t& c, uint32_t& d) {
+            TileLoc L;
+            locate_tile<T>(a, t, L);
+            c = L.hi - L.lo;
+            d = a.tile_seg[t];
+#pragma unroll
+            for (int i = 0; i < ITEMS; i++) {
+                const uint32_t e = wbase + i * 64 + lane;
+                key[i] = e < c ? rel[L.lo + e].x : 0;
+            }
+        };
+        load(tile, cnt, d1);
+        for (;;) {
+            const uint32_t pbase = d1 * pa.nb2;
+            for (uint32_t d = tid; d < nb; d += BLOCK) {
+                cnt_d[d] = 0;
+                sdesc[d] = pa.desc[pbase + d];
+            }
+            __syncthreads();
+            uint32_t dig[ITEMS], rank[ITEMS];
+#pragma unroll
+            for (int i = 0; i < ITEMS; i++) {
+                const uint32_t e = wbase + i * 64 + lane;
+                const uint64_t h = hash64<HK>(static_cast<uint64_t>(key[i]), pa.seed);
+                dig[i] = static_cast<uint32_t>(q_from_hash(h, a.f) >> a.f.shift) & a.f.dmask;
+                if (e < cnt) rank[i] = atomicAdd(&cnt_d[dig[i]], 1u);
+            }
+            __syncthreads();
+            {
+                const uint32_t dpt = (nb + BLOCK - 1) / BLOCK;
+                const uint32_t d0 = tid * dpt;
+                uint32_t local = 0;
+                for (uint32_t j = 0; j < dpt; j++)
+                    if (d0 + j < nb) local += cnt_d[d0 + j];
+                uint32_t tot;
+                uint32_t run = block_exclusive_scan_t<BLOCK / 64>(local, tmp, tot);
+                for (uint32_t j = 0; j < dpt; j++) {
+                    const uint32_t d = d0 + j;
+                    if (d < nb) {
+                        const uint32_t c = cnt_d[d];
+                        cnt_d[d] = run;
+                        run += c;
+                    }
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < ITEMS; i++) {
+                const uint32_t e = wbase + i * 64 + lane;
+                if (e < cnt) {
+                    const uint32_t pos = cnt_d[dig[i]] + rank[i];
+                    skey[pos] = key[i];
+                    sdig.put(pos, dig[i]);
+                }
+            }
+            // the next tile's keys go out now, into the same registers
+            const uint32_t next = tile + g8;
+            uint32_t ncnt = 0, nd1 = 0;
+            load(next < t_hi ? next : tile, ncnt, nd1);
+            __syncthreads();
+            // probe in grouped order: consecutive lanes mostly share a table
+#pragma unroll
+            for (int i0 = 0; i0 < ITEMS; i0 += PB) {
+                uint4 ds[PB];
+                int64_t k2[PB];
+#pragma unroll
+                for (int i = 0; i < PB; i++) {
+                    const uint32_t k = (i0 + i) * BLOCK + tid;
+                    ds[i] = make_uint4(0, 0, 1, 0);
+                    k2[i] = 0;
+                    if (k < cnt) {
+                        k2[i] = skey[k];
+                        if constexpr (DIAG == 1) ds[i].w = (k2[i] & 1) ? 1u : 0u;
+                        else ds[i] = sdesc[sdig.get(k)];
+                    }
+                }
+                uint32_t o0[PB], o1[PB];
+#pragma unroll
+                for (int i = 0; i < PB; i++) {
+                    o0[i] = o1[i] = 0;
+                    if (DIAG != 1 && ds[i].w) {   // m > 0
+                        const uint32_t hb = static_cast<uint32_t>(hash64<HK>(static_cast<uint64_t>(k2[i]), pa.seed) >> 32);
+                        const uint32_t b = hb & (ds[i].z - 1u);
+                        o0[i] = pa.toffs[ds[i].y + b];
+                        o1[i] = pa.toffs[ds[i].y + b + 1];
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < PB; i++) {
+                    bool hit = DIAG == 1 && ds[i].w != 0;
+                    for (uint32_t j = o0[i]; j < o1[i] && !hit; j++) hit = pa.tkeys[ds[i].x + j] == k2[i];
+                    hits += hit ? 1u : 0u;
+                }
+            }
+            if (next >= t_hi) break;
+            tile = next;
+            cnt = ncnt;
+            d1 = nd1;
+            __syncthreads();   // LDS reads of this tile before the next tile's counts
+        }
+    }
+    uint32_t x = hits;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_down(x, o, 64);
+    if (lane == 0) red[wave] = x;
+    __syncthreads();
+    if (tid == 0) {
+        unsigned long long t = 0;
+        for (int w = 0; w < BLOCK / 64; w++) t += red[w];
+        if (t) atomicAdd(pa.count, t);
+    }
+}
+
+__host__ __device__ constexpr size_t probe_p1_lds_bytes(int T, uint32_t nb, int NW) {
+    return static_cast<size_t>(T) * (8 + (nb <= 256 ? 1 : 2)) + static_cast<size_t>(nb) * 20 + 64 + 16 + 0 * NW;
 }
 
 // ---------------------------------------------------------------------------

@@ -66,8 +66,8 @@ SCHEDULES = [
     {"PHJ_NP_HOT": "0"},                                        # ... no hot-key LDS cache
     {"PHJ_NP_HOT_MIN": "0", "PHJ_NP_HOT_SAMPLES": "4096"},      # ... hot-key cache at every size
     {"PHJ_NP_COOP": "1"},                                       # ... four lanes per bucket
-    {"PHJ_P2PROBE": "1"},                                       # radix: probe side's pass 2 on-chip
-    {"PHJ_P2PROBE": "1", "PHJ_P1_MIN_TILES": "0"},              # ... over the chunked pass 1
+    {"PHJ_P2PROBE": "0"},                                       # radix: probe side's pass 2 through HBM
+    {"PHJ_P2PROBE": "0", "PHJ_P1_MIN_TILES": "0"},              # ... after the chunked pass 1
 ]
 
 CASES = [((8, 8), 0, phj.HASH_MURMUR3), ((11, 0), 0, phj.HASH_XXH3), ((1, 0), 1000, phj.HASH_XXH3),
