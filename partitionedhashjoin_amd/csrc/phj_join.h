@@ -1164,10 +1164,12 @@ __global__ __launch_bounds__(BLOCK) void k_probe_p1(P1ProbeArgs pa) {
             locate_tile<T>(a, t, L);
             c = L.hi - L.lo;
             d = a.tile_seg[t];
+            // pass-1 output as AoS tuples (the default) or as a key column (PHJ_P1_AOS=0)
+            const bool soa = a.in_pays != nullptr;
 #pragma unroll
             for (int i = 0; i < ITEMS; i++) {
                 const uint32_t e = wbase + i * 64 + lane;
-                key[i] = e < c ? rel[L.lo + e].x : 0;
+                key[i] = e < c ? (soa ? a.in_keys[L.lo + e] : rel[L.lo + e].x) : 0;
             }
         };
         load(tile, cnt, d1);
