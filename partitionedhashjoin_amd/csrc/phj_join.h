@@ -1127,7 +1127,8 @@ __global__ __launch_bounds__(kBlock) void k_csr_desc(const uint32_t* tkb, const 
 // next tile's keys load while the current one is probed. The tile is grouped
 // by d2 with one LDS atomic per key (an unstable counting sort: the probe only
 // needs neighbours to share a table); the tile's nb2 table descriptors are
-// staged in LDS. The bucket bits are re-hashed after the grouping. Measured
+// staged in LDS. The digit and bucket bits are re-hashed after the grouping
+// (the LDS holds keys only: four workgroups per CU). Measured
 // against a one-read table of 64-B buckets (7 keys + fill per bucket, wrapping
 // regions): 1.94 ms against 1.45 for these narrow CSR reads (two 4-B offsets,
 // ~1.2 8-B keys), as in the NoPartitioning probe a lane's four 16-B loads of
@@ -1144,7 +1145,6 @@ __global__ __launch_bounds__(BLOCK) void k_probe_p1(P1ProbeArgs pa) {
     uint4* sdesc = reinterpret_cast<uint4*>(skey + T);            // [nb]
     uint32_t* cnt_d = reinterpret_cast<uint32_t*>(sdesc + nb);    // [nb] counts, then starts
     uint32_t* tmp = cnt_d + nb;                                   // 16 words
-    const SortedDigits sdig{tmp + 16, nb <= 256};                 // [T]
     __shared__ uint32_t red[BLOCK / 64];
 
     const uint32_t total = a.tile_base[a.nseg];
@@ -1210,11 +1210,7 @@ __global__ __launch_bounds__(BLOCK) void k_probe_p1(P1ProbeArgs pa) {
 #pragma unroll
             for (int i = 0; i < ITEMS; i++) {
                 const uint32_t e = wbase + i * 64 + lane;
-                if (e < cnt) {
-                    const uint32_t pos = cnt_d[dig[i]] + rank[i];
-                    skey[pos] = key[i];
-                    sdig.put(pos, dig[i]);
-                }
+                if (e < cnt) skey[cnt_d[dig[i]] + rank[i]] = key[i];
             }
             // the next tile's keys go out now, into the same registers
             const uint32_t next = tile + g8;
@@ -1226,15 +1222,19 @@ __global__ __launch_bounds__(BLOCK) void k_probe_p1(P1ProbeArgs pa) {
             for (int i0 = 0; i0 < ITEMS; i0 += PB) {
                 uint4 ds[PB];
                 int64_t k2[PB];
+                uint32_t hb[PB];
 #pragma unroll
                 for (int i = 0; i < PB; i++) {
                     const uint32_t k = (i0 + i) * BLOCK + tid;
                     ds[i] = make_uint4(0, 0, 1, 0);
                     k2[i] = 0;
+                    hb[i] = 0;
                     if (k < cnt) {
                         k2[i] = skey[k];
+                        const uint64_t h = hash64<HK>(static_cast<uint64_t>(k2[i]), pa.seed);
+                        hb[i] = static_cast<uint32_t>(h >> 32);
                         if constexpr (DIAG == 1) ds[i].w = (k2[i] & 1) ? 1u : 0u;
-                        else ds[i] = sdesc[sdig.get(k)];
+                        else ds[i] = sdesc[static_cast<uint32_t>(q_from_hash(h, a.f) >> a.f.shift) & a.f.dmask];
                     }
                 }
                 uint32_t o0[PB], o1[PB];
@@ -1242,8 +1242,7 @@ __global__ __launch_bounds__(BLOCK) void k_probe_p1(P1ProbeArgs pa) {
                 for (int i = 0; i < PB; i++) {
                     o0[i] = o1[i] = 0;
                     if (DIAG != 1 && ds[i].w) {   // m > 0
-                        const uint32_t hb = static_cast<uint32_t>(hash64<HK>(static_cast<uint64_t>(k2[i]), pa.seed) >> 32);
-                        const uint32_t b = hb & (ds[i].z - 1u);
+                        const uint32_t b = hb[i] & (ds[i].z - 1u);
                         o0[i] = pa.toffs[ds[i].y + b];
                         o1[i] = pa.toffs[ds[i].y + b + 1];
                     }
@@ -1275,7 +1274,7 @@ __global__ __launch_bounds__(BLOCK) void k_probe_p1(P1ProbeArgs pa) {
 }
 
 __host__ __device__ constexpr size_t probe_p1_lds_bytes(int T, uint32_t nb, int NW) {
-    return static_cast<size_t>(T) * (8 + (nb <= 256 ? 1 : 2)) + static_cast<size_t>(nb) * 20 + 64 + 16 + 0 * NW;
+    return static_cast<size_t>(T) * 8 + static_cast<size_t>(nb) * 20 + 64 + 16 + 0 * NW;
 }
 
 // ---------------------------------------------------------------------------
