@@ -652,7 +652,8 @@ int partition_side(phj_ctx* c, int s, const Plan& pl, bool p1_only = false) {
     const uint32_t nt1 = (n + tile - 1) / tile;
     const bool p1_aos = pl.npass == 2 && c->tune.p1_aos && !wc1;
     // pass 1 leaves the pass-2 digit in a column (tile kernels only)
-    const bool dcol = pl.npass == 2 && c->tune.dcol && !wc1 && !wc2;
+    // (p1_only: the probe re-hashes the keys itself, nothing reads the column)
+    const bool dcol = pl.npass == 2 && c->tune.dcol && !wc1 && !wc2 && !p1_only;
     const uint32_t dbytes = pl.bits2 > 8 ? 2 : 1;
     const char* tag = s == PHJ_SIDE_BUILD ? "R" : "S";
     // Chunked pass 1 (unordered partitions, tile kernels): pass-1 chunks are
@@ -662,7 +663,7 @@ int partition_side(phj_ctx* c, int s, const Plan& pl, bool p1_only = false) {
     // loses to the stable pass below ~100M, where fewer shards (more
     // workgroups per cursor line) or more partial chunks cost more than the
     // histogram read saves; so it starts at p1_min_tiles tiles.
-    const bool chunked = pl.npass == 2 && !pl.stable && c->tune.p1_chunk && dcol && p1_aos && n > 0 &&
+    const bool chunked = pl.npass == 2 && !pl.stable && c->tune.p1_chunk && (dcol || p1_only) && p1_aos && n > 0 &&
                          nt1 >= static_cast<uint32_t>(c->tune.p1_min_tiles) &&
                          tile == tile2 && pl.nb1 <= static_cast<uint32_t>(tile_shape(c, pl.nb1).block) &&
                          tile / tile_shape(c, pl.nb1).block <= 8 &&   // registers: the next tile is prefetched

@@ -721,7 +721,7 @@ void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
                 const uint32_t d = sdig.get(k);
                 const uint32_t o = (k < dsplit[d] ? gofs[d] : dstart[d]) + k;
                 store_tuple<true>(a, o, skey[k], spay[k]);
-                store_next_digit<HK>(a, o, skey[k]);
+                if (a.out_dig) store_next_digit<HK>(a, o, skey[k]);
             }
         }
         if (next >= t_end) break;
