@@ -1091,6 +1091,8 @@ int build_csr(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned* segs)
     uint64_t nR = 0;
     for (int g = 0; g < nseg; g++) {
         if (segs[g].num_partitions != P) return set_err(c, PHJ_ERR_INVALID, "build segment partition count mismatch");
+        if (!c->dry && (!segs[g].bounds || (segs[g].n && !segs[g].keys)))
+            return set_err(c, PHJ_ERR_INVALID, "null build segment");
         L.seg[g].keys = segs[g].keys;
         L.seg[g].pays = nullptr;   // the count join tests keys only
         L.seg[g].bounds = segs[g].bounds;
@@ -1969,7 +1971,9 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
         PHJ_TRY(rc);
         PHJ_HIP(c, hipStreamWaitEvent(c->stream, tr, 0));
         PHJ_TRY(mark(c, &t1));
-        PHJ_TRY(timer_begin(c, "probe", S.n * (16 + 8)));
+        // algorithmic bytes: the pass-1 tuples read once (16 B); the CSR tables
+        // are re-read from L2, not HBM
+        PHJ_TRY(timer_begin(c, "probe", S.n * 16));
         PHJ_TRY(probe_p1(c, pl));
         PHJ_TRY(timer_end(c));
         PHJ_TRY(mark(c, &p1));

@@ -211,6 +211,7 @@ enum class Xchg { kRccl, kLocal };
 struct MemberBufs {
     DevBuf send, recv, cnt, full;
     hipEvent_t packed = nullptr;
+    bool rehearsal_packed = false;   // PHJ_REHEARSE: this member's block is packed (members > 0 pack once)
 };
 
 struct Group {
@@ -225,6 +226,7 @@ struct Group {
     std::unique_ptr<Barrier> barrier;
     std::vector<phj_join_result> res;   // per member, the last join
     std::atomic<int> failed{0};          // local exchange: a member failed before the barrier
+    bool rehearse = false;               // PHJ_REHEARSE (local exchange): members > 0 only feed the exchange
     int nlocal() const { return static_cast<int>(mem.size()); }
 };
 
@@ -298,7 +300,7 @@ uint64_t total(const std::vector<uint64_t>& v) {
 // current launch stream (aux). `ok` = this member packed its block; with the
 // local exchange every member reaches the barrier even after an error, and
 // nobody copies when any member failed (its block may not exist).
-int allgather_blocks(Group& G, int i, uint64_t elems, bool ok) {
+int allgather_blocks(Group& G, int i, uint64_t elems, bool ok, bool receive = true) {
     phj_ctx* c = G.mem[i];
     MemberBufs& B = G.buf[i];
     if (G.kind == Xchg::kRccl) {
@@ -311,6 +313,7 @@ int allgather_blocks(Group& G, int i, uint64_t elems, bool ok) {
     if (!ok) G.failed.store(1);
     G.barrier->wait();
     if (G.failed.load()) return ok ? set_err(c, PHJ_ERR_STATE, "another member failed") : PHJ_ERR_STATE;
+    if (!receive) return PHJ_OK;
     for (int h = 0; h < G.nlocal(); h++) {
         phj_ctx* ch = G.mem[h];
         char* dst = static_cast<char*>(B.recv.p) + static_cast<size_t>(h) * elems * 8;
@@ -381,7 +384,8 @@ int member_prepare_radix(Group& G, int i, const Plan& pl) {
         ~DryScope() { c->dry = false; }
     } scope{c};
     c->dry = true;
-    PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, pl));
+    const bool p2 = use_p2probe(c, pl, c->side[PHJ_SIDE_PROBE].n);
+    PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, pl, p2));
     PHJ_TRY(partition_side(c, PHJ_SIDE_BUILD, pl));
     uint64_t maxn = 0;
     for (uint64_t x : G.n[PHJ_SIDE_BUILD]) maxn = std::max(maxn, x);
@@ -389,7 +393,8 @@ int member_prepare_radix(Group& G, int i, const Plan& pl) {
     std::vector<phj_partitioned> segs(G.world);
     gathered_segments(G, i, L, pl.Ppad, segs.data());
     hipEvent_t b0, b1, p1;
-    PHJ_TRY(build_and_probe(c, pl, G.world, segs.data(), &b0, &b1, &p1));
+    if (p2) PHJ_TRY(build_csr(c, pl, G.world, segs.data()));
+    else PHJ_TRY(build_and_probe(c, pl, G.world, segs.data(), &b0, &b1, &p1));
     PHJ_HIP(c, hipStreamSynchronize(c->stream));
     return PHJ_OK;
 }
@@ -403,7 +408,11 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
     const PackLayout L = pack_layout(maxn, pl.Ppad);
     const uint32_t P = pl.Ppad;
     SideState& R = c->side[PHJ_SIDE_BUILD];
-    hipEvent_t t0 = nullptr, x0 = nullptr, x1 = nullptr, t1, b0, b1, p1, te;
+    // the probe side's pass 2 on-chip (k_probe_p1) against CSR tables built
+    // over the gathered segments on the aux stream, beside the S pass 1
+    const bool p2 = use_p2probe(c, pl, c->side[PHJ_SIDE_PROBE].n);
+    std::vector<phj_partitioned> segs(G.world);   // filled once the exchange buffers exist
+    hipEvent_t t0 = nullptr, x0 = nullptr, x1 = nullptr, t1, b0 = nullptr, b1 = nullptr, p1, te;
     // up to the exchange every step runs even after an error (no early
     // return): the local exchange's barrier must see every member
     int rc = hipSetDevice(c->device) == hipSuccess ? PHJ_OK : set_err(c, PHJ_ERR_HIP, "hipSetDevice");
@@ -413,8 +422,19 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
     }
     if (rc == PHJ_OK) rc = mark(c, &t0);
     if (rc == PHJ_OK && hipStreamWaitEvent(c->aux, t0, 0) != hipSuccess) rc = set_err(c, PHJ_ERR_HIP, "wait t0");
-    // R shard, pack and all-gather on the aux stream (S goes beside them)
+    // R shard, pack and all-gather on the aux stream (S goes beside them);
+    // a rehearsal's members > 0 pack their (unchanging) block once and from
+    // then on only take part in the exchange, so member 0 has the GPU
     c->ks = c->aux;
+    const bool quiet = G.rehearse && i > 0 && B.rehearsal_packed;
+    if (quiet) {
+        c->ks = c->stream;
+        const int rx = allgather_blocks(G, i, L.elems, rc == PHJ_OK, false);
+        if (rc == PHJ_OK) rc = rx;
+        PHJ_TRY(rc);
+        r->total_ms = 0;
+        return PHJ_OK;
+    }
     if (rc == PHJ_OK) rc = partition_side(c, PHJ_SIDE_BUILD, pl);
     if (rc == PHJ_OK && R.n &&
         hipMemcpyAsync(B.send.p, R.view.keys, R.n * 8, hipMemcpyDeviceToDevice, c->ks) != hipSuccess)
@@ -430,15 +450,37 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
     if (rc == PHJ_OK) rc = rx;
     if (rc == PHJ_OK) rc = timer_end(c);
     if (rc == PHJ_OK) rc = mark(c, &x1);
+    if (rc == PHJ_OK) gathered_segments(G, i, L, P, segs.data());
+    if (p2) {
+        b0 = x1;
+        if (rc == PHJ_OK) rc = timer_begin(c, "build", total(G.n[PHJ_SIDE_BUILD]) * 16);
+        if (rc == PHJ_OK) rc = build_csr(c, pl, G.world, segs.data());
+        if (rc == PHJ_OK) rc = timer_end(c);
+        if (rc == PHJ_OK) rc = mark(c, &b1);
+    }
     c->ks = c->stream;
     PHJ_TRY(rc);
+    if (G.rehearse && i > 0) {   // rehearsal: only member 0 joins (its time = one rank's device work)
+        B.rehearsal_packed = true;
+        PHJ_HIP(c, hipStreamWaitEvent(c->stream, p2 ? b1 : x1, 0));
+        PHJ_HIP(c, hipMemsetAsync(B.cnt.p, 0, 8, c->stream));
+        PHJ_HIP(c, hipStreamSynchronize(c->stream));
+        r->total_ms = 0;
+        return PHJ_OK;
+    }
     // S shard on the main stream, concurrently with R and the exchange
-    PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, pl));
-    PHJ_HIP(c, hipStreamWaitEvent(c->stream, x1, 0));
+    PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, pl, p2));
+    PHJ_HIP(c, hipStreamWaitEvent(c->stream, p2 ? b1 : x1, 0));
     PHJ_TRY(mark(c, &t1));
-    std::vector<phj_partitioned> segs(G.world);
-    gathered_segments(G, i, L, P, segs.data());
-    PHJ_TRY(build_and_probe(c, pl, G.world, segs.data(), &b0, &b1, &p1));
+    if (p2) {
+        PHJ_TRY(timer_begin(c, "probe", c->side[PHJ_SIDE_PROBE].n * 16));
+        PHJ_TRY(probe_p1(c, pl));
+        PHJ_TRY(timer_end(c));
+        PHJ_TRY(mark(c, &p1));
+        c->last_fused = false;
+    } else {
+        PHJ_TRY(build_and_probe(c, pl, G.world, segs.data(), &b0, &b1, &p1));
+    }
     PHJ_TRY(allreduce_count(G, i, c->count.p));
     PHJ_TRY(mark(c, &te));
     uint64_t m = 0;
@@ -446,8 +488,8 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
     r->matches = m;
     r->partition_ms = elapsed(c, t0, t1);
     r->build_ms = elapsed(c, b0, b1);
-    r->probe_ms = elapsed(c, b1, p1);
-    if (c->last_fused) {
+    r->probe_ms = p2 ? elapsed(c, t1, p1) : elapsed(c, b1, p1);
+    if (!p2 && c->last_fused) {
         const double t = elapsed(c, b0, p1), fb = fused_build_fraction(c);
         r->build_ms = t * fb;
         r->probe_ms = t * (1.0 - fb);
@@ -652,10 +694,9 @@ int group_create(int ngpus, const int* devs, uint32_t flags, int world, int rank
         }
         if (e != ncclSuccess) return fail(PHJ_ERR_HIP, std::string("RCCL communicator: ") + api.GetErrorString(e));
     }
-    if (ngpus > 1) {
-        G->threads.reset(new MemberThreads(ngpus));
-        G->barrier.reset(new Barrier(ngpus));
-    }
+    G->rehearse = G->kind == Xchg::kLocal && env_int("PHJ_REHEARSE", 0) != 0;
+    G->barrier.reset(new Barrier(ngpus));   // the local exchange waits on it, even with one member
+    if (ngpus > 1) G->threads.reset(new MemberThreads(ngpus));
     for (int s = 0; s < 2; s++) G->n[s].assign(world, 0);
     *out = shell;
     return PHJ_OK;

@@ -32,7 +32,7 @@ def _generate(ctx, nR, nS, alpha, off, rank=0, world=1):
     return ctx.count_in_range(phj.SIDE_PROBE, 1 + off, nR)
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [1, 2, 3])
 def test_local_group_on_one_gpu(world):
     nR, nS, off = 300_001, 4_000_003, 100_000
     with phj.Context(devices=[0] * world, flags=phj.CTX_LOCAL) as g:
