@@ -46,3 +46,18 @@ def test_fused_join_is_one_dispatch_for_build_and_probe():
     assert got["build"] == got["probe"] == {"FETCH_SIZE": 7.0}
     assert got["S.p1.scatter"]["FETCH_SIZE"] == 5
     assert got["S.p1.hist"]["FETCH_SIZE"] == 4
+
+
+def test_sweep_writes_generate_sh_figure_layout(tmp_path):
+    # scripts/sweep.py writes the reference's figure.dat layout (generate.sh:66-82):
+    # one column per run, rows NumberOfPartitions / Partition / Build / Probe
+    import sweep
+    names = [n for n, _a, _p in sweep.columns()]
+    assert names[0] == "NoPartitioning" and names[1:] == [f"Radix{p}" for p in sweep.PARTITIONS]
+    table = {n: {"partition": i, "build": 2 * i, "probe": 3 * i} for i, n in enumerate(names)}
+    path = tmp_path / "fig.dat"
+    sweep.write_figure(str(path), table)
+    rows = [line.split() for line in path.read_text().splitlines()]
+    assert [r[0] for r in rows] == ["NumberOfPartitions", "Partition", "Build", "Probe"]
+    assert rows[0][1:] == names
+    assert rows[3][1:] == [str(3 * i) for i in range(len(names))]
