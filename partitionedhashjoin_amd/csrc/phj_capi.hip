@@ -1174,14 +1174,17 @@ int probe_p1(phj_ctx* c, const Plan& pl) {
     pa.seed = pl.seed;
     pa.nb2 = pl.nb2;
     const size_t lds = probe_p1_lds_bytes(4096, pl.nb2, 8);
-    const int diag = env_int("PHJ_P1_DIAG", 0);
+    const int diag = env_int("PHJ_P1_DIAG", 0), wpe = env_int("PHJ_P1_WPE", 6);
     const void* kfn;
     if (diag == 1)
         kfn = pl.hk == kMurmur3 ? reinterpret_cast<const void*>(&k_probe_p1<512, 8, kMurmur3, 1>)
                                 : reinterpret_cast<const void*>(&k_probe_p1<512, 8, kXXH3, 1>);
+    else if (wpe == 4)   // waves per SIMD the compiler budgets registers for (6: 3 workgroups per CU, measured best)
+        kfn = pl.hk == kMurmur3 ? reinterpret_cast<const void*>(&k_probe_p1<512, 8, kMurmur3, 0, 4>)
+                                : reinterpret_cast<const void*>(&k_probe_p1<512, 8, kXXH3, 0, 4>);
     else
-        kfn = pl.hk == kMurmur3 ? reinterpret_cast<const void*>(&k_probe_p1<512, 8, kMurmur3>)
-                                : reinterpret_cast<const void*>(&k_probe_p1<512, 8, kXXH3>);
+        kfn = pl.hk == kMurmur3 ? reinterpret_cast<const void*>(&k_probe_p1<512, 8, kMurmur3, 0, 6>)
+                                : reinterpret_cast<const void*>(&k_probe_p1<512, 8, kXXH3, 0, 6>);
     // persistent: as many workgroups as fit the chip at once (a multiple of 8:
     // XCD x owns tiles [x, x + 1) * ntiles / 8), never many more than tiles
     int per_cu = 0;

@@ -1134,8 +1134,8 @@ __global__ __launch_bounds__(kBlock) void k_csr_desc(const uint32_t* tkb, const 
 // ~1.2 8-B keys), as in the NoPartitioning probe a lane's four 16-B loads of
 // one bucket cost more than the extra dependent level. DIAG (timing only):
 // 1 = no table reads.
-template <int BLOCK, int ITEMS, int HK, int DIAG = 0>
-__global__ __launch_bounds__(BLOCK) void k_probe_p1(P1ProbeArgs pa) {
+template <int BLOCK, int ITEMS, int HK, int DIAG = 0, int WPE = 4>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void k_probe_p1(P1ProbeArgs pa) {
     constexpr int T = BLOCK * ITEMS;
     constexpr int PB = 4;   // probes in flight per lane per batch
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1243,8 +1243,11 @@ __global__ __launch_bounds__(BLOCK) void k_probe_p1(P1ProbeArgs pa) {
                     o0[i] = o1[i] = 0;
                     if (DIAG != 1 && ds[i].w) {   // m > 0
                         const uint32_t b = hb[i] & (ds[i].z - 1u);
-                        o0[i] = pa.toffs[ds[i].y + b];
-                        o1[i] = pa.toffs[ds[i].y + b + 1];
+                        // the bucket's [start, end) offsets in one 8-B load (4-B aligned)
+                        typedef uint32_t u32x2 __attribute__((ext_vector_type(2), aligned(4)));
+                        const u32x2 ob = *reinterpret_cast<const u32x2*>(pa.toffs + ds[i].y + b);
+                        o0[i] = ob.x;
+                        o1[i] = ob.y;
                     }
                 }
 #pragma unroll
