@@ -73,6 +73,10 @@ struct Tuning {
     int np_diag = 0;         // PHJ_NP_DIAG: diagnostic probe floors (timing only, wrong counts)
     int np_coop = 0;         // NoPartitioning probe: four lanes per bucket (k_np_probe_coop; measured slower)
     int p2probe = 1;         // radix join, 2 passes: the probe side's pass 2 on-chip (k_probe_p1)
+    int p1_priv = 0;
+    int p1_bits = 0;
+    double np_ratio = kNPDefaultRatio;   // NoPartitioning: slots per build tuple when the params leave it 0         // 2-pass join: pass-1 digit bits (0: the plan's split; rebalance_plan)         // pass 1 consumed on chip: workgroup-private chains (k_scatter_priv)
+    int p1_var = 3;          // chunked pass 1 variant (k_scatter_chunked VAR: 1 atomic rank, 2 tuple LDS)
 };
 
 int env_int(const char* name, int dflt) {
@@ -113,6 +117,9 @@ struct SideState {
     DevBuf hist1, hist2, bounds1, tbase2, tseg2, bounds, partials;
     DevBuf dig;           // pass-2 digit column written by pass 1
     DevBuf ccur, ctab, tstart;   // chunked pass 1: digit cursors + pool counter, chunk table, pass-2 tile starts
+    DevBuf priv;                 // private-chain pass 1: chunk logs, chain states, chunk lists (k_scatter_priv)
+    const uint32_t* p2_ent = nullptr;     // ... the probe's chunk list and its per-digit offsets
+    const uint32_t* p2_ebase = nullptr;
     uint32_t gen = 0;            // chunked pass 1: tag of the current chunk-table entries
     phj_partitioned view{};
     PassArgs p2{};               // p1_only: the pass-2 tile mapping over the pass-1 output
@@ -395,7 +402,7 @@ int make_plan(phj_ctx* c, const phj_join_params* p, Plan& pl) {
 // and partition on the refined q in two balanced passes. The count is the
 // same (a partition's hash table is simply organised by further hash bits);
 // phj_partition keeps the exact layout of the requested partitions.
-void refine_plan(const phj_ctx* c, Plan& pl, uint64_t nR) {
+void refine_plan_sub(const phj_ctx* c, Plan& pl, uint64_t nR) {
     if (!c->tune.subpart || !c->tune.fused || pl.P == 0) return;
     const double expect = static_cast<double>(nR) / static_cast<double>(pl.P);
     if (expect * 3 <= static_cast<double>(kFusedTcap) * 2) return;
@@ -418,6 +425,33 @@ void refine_plan(const phj_ctx* c, Plan& pl, uint64_t nR) {
     pl.shift1 = b2;
     pl.dmask1 = 0xffffffffu;
     pl.Ppad = pl.nb1 * pl.nb2;
+}
+
+// Pass split of a 2-pass join plan (PHJ_P1_BITS = b > 0): pass 1 on the top
+// b bits of q, pass 2 on the rest. The final partitions (q) are the same;
+// fewer pass-1 digits give the private-chain pass 1 longer runs per tile
+// (fewer partial 64-B segments) and the on-chip probe more digits to group.
+void rebalance_plan(const phj_ctx* c, Plan& pl) {
+    const int b1 = c->tune.p1_bits;
+    if (b1 <= 0 || pl.npass != 2) return;
+    const uint64_t range = pl.sub_bits == 0 && pl.mode == 0 ? (1ull << (pl.bits1 + pl.bits2))
+                           : (pl.mode == 0 ? (1ull << ceil_log2(pl.P)) : pl.P) << pl.sub_bits;
+    const uint32_t tot = ceil_log2(range);
+    if (static_cast<uint32_t>(b1) >= tot || tot - b1 > static_cast<uint32_t>(kMaxDigitBits)) return;
+    const uint32_t b2 = tot - b1;
+    pl.nb2 = 1u << b2;
+    pl.bits2 = b2;
+    pl.dmask2 = pl.nb2 - 1;
+    pl.shift1 = b2;
+    pl.nb1 = static_cast<uint32_t>((range + pl.nb2 - 1) / pl.nb2);
+    pl.bits1 = ceil_log2(pl.nb1);
+    pl.dmask1 = 0xffffffffu;
+    pl.Ppad = pl.nb1 * pl.nb2;
+}
+
+void refine_plan(const phj_ctx* c, Plan& pl, uint64_t nR) {
+    refine_plan_sub(c, pl, nR);
+    rebalance_plan(c, pl);
 }
 
 DigitFn digit_fn(const Plan& pl, int pass) {
@@ -481,12 +515,22 @@ int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const st
             uint32_t slots = std::max<uint32_t>(1, std::min<uint32_t>(per, fit * c->num_cus / a.nshards));
             if (c->tune.p1_slots > 0) slots = std::min<uint32_t>(per, c->tune.p1_slots);
             if (c->tune.p1_slots < 0) slots = per;   // one tile per workgroup
-            if (hk == kMurmur3)
-                hipLaunchKernelGGL((k_scatter_chunked<BLOCK, ITEMS, kMurmur3>), dim3(slots * a.nshards), dim3(BLOCK), sc_lds,
-                                   c->ks, a, ntiles, per);
-            else
-                hipLaunchKernelGGL((k_scatter_chunked<BLOCK, ITEMS, kXXH3>), dim3(slots * a.nshards), dim3(BLOCK), sc_lds,
-                                   c->ks, a, ntiles, per);
+            const void* kfn = nullptr;
+            switch (c->tune.p1_var & 3) {
+#define PHJ_P1_VARIANT(V)                                                                            \
+    case V:                                                                                          \
+        kfn = hk == kMurmur3 ? reinterpret_cast<const void*>(&k_scatter_chunked<BLOCK, ITEMS, kMurmur3, V>) \
+                             : reinterpret_cast<const void*>(&k_scatter_chunked<BLOCK, ITEMS, kXXH3, V>);    \
+        break;
+                PHJ_P1_VARIANT(0)
+                PHJ_P1_VARIANT(1)
+                PHJ_P1_VARIANT(2)
+                PHJ_P1_VARIANT(3)
+#undef PHJ_P1_VARIANT
+            }
+            PassArgs ak = a;
+            void* kargs[] = {&ak, const_cast<uint32_t*>(&ntiles), const_cast<uint32_t*>(&per)};
+            PHJ_HIP(c, hipLaunchKernel(kfn, dim3(slots * a.nshards), dim3(BLOCK), kargs, sc_lds, c->ks));
             PHJ_LAUNCHED(c, sname);
         } else {
             (void)grid;
@@ -656,6 +700,22 @@ int partition_side(phj_ctx* c, int s, const Plan& pl, bool p1_only = false) {
     const bool dcol = pl.npass == 2 && c->tune.dcol && !wc1 && !wc2 && !p1_only;
     const uint32_t dbytes = pl.bits2 > 8 ? 2 : 1;
     const char* tag = s == PHJ_SIDE_BUILD ? "R" : "S";
+    // Pass 1 into workgroup-private chains of 64-slot chunks when the on-chip
+    // probe consumes it (k_scatter_priv): no histogram pass and no claims that
+    // leave the CU; the probe reads a chunk list. Persistent workgroups (two
+    // per CU, what the LDS allows), each a contiguous run of `pper` tiles.
+    const uint32_t pblock = static_cast<uint32_t>(tile_shape(c, pl.nb1).block);
+    uint32_t pG = 0, pper = 0, prch = 0;
+    bool priv = p1_only && pl.npass == 2 && !pl.stable && c->tune.p1_priv && p1_aos && !wc1 && !wc2 && n > 0 &&
+                tile == 4096 && tile2 == 4096 && pblock == 512 && pl.nb1 <= pblock;
+    if (priv) {
+        const uint32_t fit = std::max<uint32_t>(1, static_cast<uint32_t>(160 * 1024 / scatter_priv_lds_bytes(4096, pl.nb1)));
+        pG = std::min<uint32_t>(nt1, fit * c->num_cus);
+        pper = (nt1 + pG - 1) / pG;
+        pG = (nt1 + pper - 1) / pper;   // no workgroup without tiles
+        prch = pper * (tile / kPrivCh) + pl.nb1;
+        priv = static_cast<uint64_t>(pG) * prch * kPrivCh < (1ull << 32) - 64;
+    }
     // Chunked pass 1 (unordered partitions, tile kernels): pass-1 chunks are
     // the pass-2 tiles, every digit's run of a tile fits one workgroup thread
     // (nb1 <= block) and spans at most two chunks (tile1 == tile2).
@@ -663,7 +723,7 @@ int partition_side(phj_ctx* c, int s, const Plan& pl, bool p1_only = false) {
     // loses to the stable pass below ~100M, where fewer shards (more
     // workgroups per cursor line) or more partial chunks cost more than the
     // histogram read saves; so it starts at p1_min_tiles tiles.
-    const bool chunked = pl.npass == 2 && !pl.stable && c->tune.p1_chunk && (dcol || p1_only) && p1_aos && n > 0 &&
+    const bool chunked = !priv && pl.npass == 2 && !pl.stable && c->tune.p1_chunk && (dcol || p1_only) && p1_aos && n > 0 &&
                          nt1 >= static_cast<uint32_t>(c->tune.p1_min_tiles) &&
                          tile == tile2 && pl.nb1 <= static_cast<uint32_t>(tile_shape(c, pl.nb1).block) &&
                          tile / tile_shape(c, pl.nb1).block <= 8 &&   // registers: the next tile is prefetched
@@ -678,14 +738,22 @@ int partition_side(phj_ctx* c, int s, const Plan& pl, bool p1_only = false) {
     const uint32_t per = (nt1 + nshards - 1) / nshards;
     const uint32_t pool_stride = 3 * per + pl.nb1;
     const uint32_t maxch = per + 1;   // chunks of one chain (every tuple of a shard in one digit)
-    const size_t slots1 = chunked ? static_cast<size_t>(nshards) * pool_stride * tile : n;
-    // pass-2 tiles (bound): one partial tile per segment, or per chain when chunked
-    const uint32_t nt2 = pl.npass == 2 ? (n + tile2 - 1) / tile2 + pl.nb1 * (chunked ? nshards : 1) : 0;
+    const size_t slots1 = priv ? static_cast<size_t>(pG) * prch * kPrivCh
+                               : chunked ? static_cast<size_t>(nshards) * pool_stride * tile : n;
+    // pass-2 tiles (bound): one partial tile per segment, or per chain when
+    // chunked; private chains: 64 chunks per tile, one partial tile per digit
+    const uint32_t nt2 = pl.npass != 2 ? 0
+                         : priv ? static_cast<uint32_t>((static_cast<uint64_t>(pG) * prch + 63) / 64) + pl.nb1
+                                : (n + tile2 - 1) / tile2 + pl.nb1 * (chunked ? nshards : 1);
     const uint32_t nt2max = nt2 + 8;
     // workspace (grow-only; allocation is outside the timed phases on reuse)
     PHJ_TRY(ensure(c, S.kA, slots1 * (p1_aos ? 16 : 8)));
     if (!p1_aos) PHJ_TRY(ensure(c, S.pA, static_cast<size_t>(n) * 8));
-    if (!chunked) PHJ_TRY(ensure(c, S.hist1, static_cast<size_t>(nt1) * pl.nb1 * 4));
+    if (!chunked && !priv) PHJ_TRY(ensure(c, S.hist1, static_cast<size_t>(nt1) * pl.nb1 * 4));
+    // private chains (u32 words): log, ent [pG * prch]; ccount, clast, cfill,
+    // offw [pG * nb1]; nused [pG]; nch, ntup [nb1]; ebase [nb1 + 1]
+    const size_t pw_ch = static_cast<size_t>(pG) * prch, pw_cw = static_cast<size_t>(pG) * pl.nb1;
+    if (priv) PHJ_TRY(ensure(c, S.priv, (2 * pw_ch + 4 * pw_cw + pG + 3 * static_cast<size_t>(pl.nb1) + 1) * 4));
     PHJ_TRY(ensure(c, S.bounds1, (static_cast<size_t>(pl.nb1) + 1) * 4));
     if (pl.npass == 2) {
         PHJ_TRY(ensure(c, S.kB, static_cast<size_t>(n) * 8));
@@ -709,7 +777,7 @@ int partition_side(phj_ctx* c, int s, const Plan& pl, bool p1_only = false) {
         }
     }
     if (c->dry) {   // scan scratch of both passes, then nothing is launched
-        if (!chunked) PHJ_TRY(scan_u32(c, nullptr, nt1 * pl.nb1, 1, nt1 * pl.nb1, c->scan_scratch));
+        if (!chunked && !priv) PHJ_TRY(scan_u32(c, nullptr, nt1 * pl.nb1, 1, nt1 * pl.nb1, c->scan_scratch));
         if (pl.npass == 2 && n) PHJ_TRY(scan_u32(c, nullptr, nt2 * pl.nb2, 1, nt2 * pl.nb2, c->scan_scratch));
         return PHJ_OK;
     }
@@ -744,12 +812,52 @@ int partition_side(phj_ctx* c, int s, const Plan& pl, bool p1_only = false) {
         }
         a.gen = S.gen;
     }
-    if (wc1)
-        PHJ_TRY(launch_pass_wc(c, pl.hk, true, a, nt1, tile, std::string(tag) + ".p1", n, nt1 * pl.nb1));
-    else
-        PHJ_TRY(launch_pass(c, pl.hk, true, p1_aos, a, nt1, std::string(tag) + ".p1", n, nt1 * pl.nb1));
     uint32_t* tb2 = pl.npass == 2 ? static_cast<uint32_t*>(S.tbase2.p) : nullptr;
-    if (chunked) {
+    uint32_t* pw = static_cast<uint32_t*>(S.priv.p);
+    PrivArgs q{};
+    if (priv) {
+        q.log = pw;
+        q.ccount = pw + 2 * pw_ch;
+        q.clast = q.ccount + pw_cw;
+        q.cfill = q.clast + pw_cw;
+        q.nused = q.cfill + 2 * pw_cw;   // after offw
+        q.rchunks = prch;
+        q.per = pper;
+        q.ntiles = nt1;
+        uint32_t* offw = q.cfill + pw_cw;
+        uint32_t* nch = q.nused + pG;
+        uint32_t* ntup = nch + pl.nb1;
+        uint32_t* ebase = ntup + pl.nb1;
+        uint32_t* ent = pw + pw_ch;
+        a.nt_load = c->tune.nt_load ? 1u : 0u;
+        const size_t lds = scatter_priv_lds_bytes(4096, pl.nb1);
+        PHJ_TRY(timer_begin(c, (std::string(tag) + ".p1.scatter").c_str(), static_cast<uint64_t>(n) * 32));
+        const void* kfn = pl.hk == kMurmur3 ? reinterpret_cast<const void*>(&k_scatter_priv<512, 8, kMurmur3>)
+                                            : reinterpret_cast<const void*>(&k_scatter_priv<512, 8, kXXH3>);
+        void* kargs[] = {&a, &q};
+        PHJ_HIP(c, hipLaunchKernel(kfn, dim3(pG), dim3(512), kargs, lds, c->ks));
+        PHJ_LAUNCHED(c, "k_scatter_priv");
+        PHJ_TRY(timer_end(c));
+        hipLaunchKernelGGL(k_priv_offsets, dim3(pl.nb1), dim3(kBlock), 0, c->ks, q.ccount, q.cfill, pG, pl.nb1, offw, nch,
+                           ntup);
+        PHJ_LAUNCHED(c, "k_priv_offsets");
+        hipLaunchKernelGGL(k_priv_finish, dim3(1), dim3(1024), 0, c->ks, nch, ntup, pl.nb1, ebase, tb2,
+                           static_cast<uint32_t*>(S.bounds1.p));
+        PHJ_LAUNCHED(c, "k_priv_finish");
+        hipLaunchKernelGGL(k_priv_list, dim3(static_cast<uint32_t>((pw_ch + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->ks,
+                           q.log, q.nused, q.clast, q.cfill, offw, ebase, pG, pl.nb1, prch, ent);
+        PHJ_LAUNCHED(c, "k_priv_list");
+        S.p2_ent = ent;
+        S.p2_ebase = ebase;
+    } else if (wc1) {
+        PHJ_TRY(launch_pass_wc(c, pl.hk, true, a, nt1, tile, std::string(tag) + ".p1", n, nt1 * pl.nb1));
+    } else {
+        PHJ_TRY(launch_pass(c, pl.hk, true, p1_aos, a, nt1, std::string(tag) + ".p1", n, nt1 * pl.nb1));
+    }
+    if (!priv) S.p2_ent = S.p2_ebase = nullptr;
+    if (priv) {
+        // bounds1 / tile_base2 written by k_priv_finish
+    } else if (chunked) {
         hipLaunchKernelGGL(k_pass1_finish_sizes, dim3(1), dim3(1024), 0, c->ks, a.chunk_cursor, pl.nb1, nshards, n, tile2,
                            static_cast<uint32_t*>(S.bounds1.p), tb2);
         PHJ_LAUNCHED(c, "k_pass1_finish_sizes");
@@ -784,7 +892,7 @@ int partition_side(phj_ctx* c, int s, const Plan& pl, bool p1_only = false) {
                 PHJ_LAUNCHED(c, "k_tile_chunks");
                 b.tile_start = ts;
                 b.tile_cnt = tc;
-            } else {
+            } else {   // stable layout or private chains: tile -> digit
                 hipLaunchKernelGGL(k_tile_seg, dim3((pl.nb1 + kWaves - 1) / kWaves), dim3(kBlock), 0, c->ks, tb2,
                                    pl.nb1, static_cast<uint32_t*>(S.tseg2.p));
                 PHJ_LAUNCHED(c, "k_tile_seg");
@@ -1173,12 +1281,17 @@ int probe_p1(phj_ctx* c, const Plan& pl) {
     pa.count = static_cast<unsigned long long*>(c->count.p);
     pa.seed = pl.seed;
     pa.nb2 = pl.nb2;
+    pa.ent = PS.p2_ent;
+    pa.ebase = PS.p2_ebase;
     const size_t lds = probe_p1_lds_bytes(4096, pl.nb2, 8);
     const int diag = env_int("PHJ_P1_DIAG", 0), wpe = env_int("PHJ_P1_WPE", 6);
     const void* kfn;
     if (diag == 1)
         kfn = pl.hk == kMurmur3 ? reinterpret_cast<const void*>(&k_probe_p1<512, 8, kMurmur3, 1>)
                                 : reinterpret_cast<const void*>(&k_probe_p1<512, 8, kXXH3, 1>);
+    else if (pa.ent)   // tiles from the private chains' chunk lists
+        kfn = pl.hk == kMurmur3 ? reinterpret_cast<const void*>(&k_probe_p1<512, 8, kMurmur3, 0, 6, true>)
+                                : reinterpret_cast<const void*>(&k_probe_p1<512, 8, kXXH3, 0, 6, true>);
     else if (wpe == 4)   // waves per SIMD the compiler budgets registers for (6: 3 workgroups per CU, measured best)
         kfn = pl.hk == kMurmur3 ? reinterpret_cast<const void*>(&k_probe_p1<512, 8, kMurmur3, 0, 4>)
                                 : reinterpret_cast<const void*>(&k_probe_p1<512, 8, kXXH3, 0, 4>);
@@ -1217,7 +1330,7 @@ int join_nopart(phj_ctx* c, const phj_join_params* p, phj_join_result* r, uint32
         return set_err(c, PHJ_ERR_INVALID,
                        "LinearProbingHashTable::LinearProbingHashTable: numberOfObjects must be greater than zero.");
     if (R.n >= (1ull << 32)) return set_err(c, PHJ_ERR_RANGE, "build side above 2^32 tuples");
-    const double ratio = p->table_ratio > 0 ? p->table_ratio : kNPDefaultRatio;
+    const double ratio = p->table_ratio > 0 ? p->table_ratio : c->tune.np_ratio;
     if (ratio < 1.0) return set_err(c, PHJ_ERR_INVALID, "table_ratio must be >= 1");
     const double nbd = std::ceil(static_cast<double>(R.n) * ratio / kNPSlots);
     if (nbd >= 4294967295.0) return set_err(c, PHJ_ERR_RANGE, "table too large");
@@ -1580,6 +1693,12 @@ int ctx_create_device(int device, phj_ctx** out) {
     c->tune.np_diag = env_int("PHJ_NP_DIAG", 0);
     c->tune.np_coop = env_int("PHJ_NP_COOP", 0);
     c->tune.p2probe = env_int("PHJ_P2PROBE", 1);
+    c->tune.p1_var = env_int("PHJ_P1_VAR", 3) & 3;
+    // measured: 2.05 vs 1.47 ms at 200M; the private chains'
+    // partial 64-B segments are written separately (WRREQ 61M vs 52M)
+    c->tune.p1_priv = env_int("PHJ_P1_PRIV", 0);
+    c->tune.p1_bits = std::max(0, env_int("PHJ_P1_BITS", 0));
+    if (const char* r = std::getenv("PHJ_NP_RATIO")) c->tune.np_ratio = std::max(1.0, std::atof(r));
     c->tune.p1_slots = env_int("PHJ_P1_SLOTS", 0);
     c->tune.p1_tps = std::max(1, env_int("PHJ_P1_TPS", static_cast<int>(kTilesPerShard)));
     c->tune.p1_min_tiles = std::max(0, env_int("PHJ_P1_MIN_TILES", 32768));
@@ -1687,7 +1806,7 @@ void phj_ctx_destroy(phj_ctx* c) {
     (void)hipStreamSynchronize(c->aux);
     for (SideState& S : c->side) {
         for (DevBuf* b : {&S.owned, &S.kA, &S.pA, &S.kB, &S.pB, &S.hist1, &S.hist2, &S.bounds1, &S.tbase2,
-                          &S.bounds, &S.partials, &S.tseg2, &S.dig, &S.ccur, &S.ctab, &S.tstart})
+                          &S.bounds, &S.partials, &S.tseg2, &S.dig, &S.ccur, &S.ctab, &S.tstart, &S.priv})
             free_buf(*b);
     }
     for (DevBuf* b : {&c->scan_partials, &c->prep, &c->tkeys, &c->tpays, &c->toffs, &c->gcursor, &c->items, &c->biglist,

@@ -1092,6 +1092,11 @@ struct P1ProbeArgs {
     uint64_t seed;
     uint32_t nb2;             // digits of pass 2 (final partition = d1 * nb2 + d2)
     uint32_t pad;
+    // pass 1 into workgroup-private chains (k_scatter_priv): tile t of digit d
+    // is entries [ebase[d] + (t - tile_base[d]) * 64, +64) of the chunk list,
+    // one chunk (g << 6 | fill - 1) per wave row. nullptr: tiles from a.tile_start
+    const uint32_t* ent;
+    const uint32_t* ebase;
 };
 
 // arr: 2 arrays of P+1 entries: m_p and NB_p + 1 (last entries 0), for the
@@ -1134,7 +1139,7 @@ __global__ __launch_bounds__(kBlock) void k_csr_desc(const uint32_t* tkb, const 
 // ~1.2 8-B keys), as in the NoPartitioning probe a lane's four 16-B loads of
 // one bucket cost more than the extra dependent level. DIAG (timing only):
 // 1 = no table reads.
-template <int BLOCK, int ITEMS, int HK, int DIAG = 0, int WPE = 4>
+template <int BLOCK, int ITEMS, int HK, int DIAG = 0, int WPE = 4, bool CHK = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void k_probe_p1(P1ProbeArgs pa) {
     constexpr int T = BLOCK * ITEMS;
     constexpr int PB = 4;   // probes in flight per lane per batch
@@ -1158,21 +1163,37 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
         const uint32_t wbase = wave * 64 * ITEMS;
         const longlong2* rel = reinterpret_cast<const longlong2*>(a.in_keys);
         int64_t key[ITEMS];
-        uint32_t cnt = 0, d1 = 0;
-        auto load = [&](uint32_t t, uint32_t& c, uint32_t& d) {
+        uint32_t vm = 0, d1 = 0;   // vm bit i: item i holds a key
+        auto load = [&](uint32_t t, uint32_t& m, uint32_t& d) {
+            d = a.tile_seg[t];
+            m = 0;
+            if constexpr (CHK) {   // 64 chunks, wave row r = wave * ITEMS + i holds chunk r
+                const uint32_t e0 = pa.ebase[d] + (t - a.tile_base[d]) * 64;
+                const uint32_t ne = min(64u, pa.ebase[d + 1] - e0);
+                const uint32_t wv = __builtin_amdgcn_readfirstlane(wave);   // rows are wave-uniform: scalar loads
+#pragma unroll
+                for (int i = 0; i < ITEMS; i++) {
+                    const uint32_t r = wv * ITEMS + i;
+                    const uint32_t en = r < ne ? pa.ent[e0 + r] : 0u;
+                    const bool v = r < ne && lane <= (en & 63u);
+                    key[i] = v ? rel[static_cast<size_t>(en >> 6) * 64 + lane].x : 0;
+                    m |= v ? (1u << i) : 0u;
+                }
+                return;
+            }
             TileLoc L;
             locate_tile<T>(a, t, L);
-            c = L.hi - L.lo;
-            d = a.tile_seg[t];
+            const uint32_t c = L.hi - L.lo;
             // pass-1 output as AoS tuples (the default) or as a key column (PHJ_P1_AOS=0)
             const bool soa = a.in_pays != nullptr;
 #pragma unroll
             for (int i = 0; i < ITEMS; i++) {
                 const uint32_t e = wbase + i * 64 + lane;
                 key[i] = e < c ? (soa ? a.in_keys[L.lo + e] : rel[L.lo + e].x) : 0;
+                m |= e < c ? (1u << i) : 0u;
             }
         };
-        load(tile, cnt, d1);
+        load(tile, vm, d1);
         for (;;) {
             const uint32_t pbase = d1 * pa.nb2;
             for (uint32_t d = tid; d < nb; d += BLOCK) {
@@ -1183,12 +1204,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
             uint32_t dig[ITEMS], rank[ITEMS];
 #pragma unroll
             for (int i = 0; i < ITEMS; i++) {
-                const uint32_t e = wbase + i * 64 + lane;
                 const uint64_t h = hash64<HK>(static_cast<uint64_t>(key[i]), pa.seed);
                 dig[i] = static_cast<uint32_t>(q_from_hash(h, a.f) >> a.f.shift) & a.f.dmask;
-                if (e < cnt) rank[i] = atomicAdd(&cnt_d[dig[i]], 1u);
+                if ((vm >> i) & 1u) rank[i] = atomicAdd(&cnt_d[dig[i]], 1u);
             }
             __syncthreads();
+            uint32_t cnt;   // keys of the tile, grouped into [0, cnt)
             {
                 const uint32_t dpt = (nb + BLOCK - 1) / BLOCK;
                 const uint32_t d0 = tid * dpt;
@@ -1197,6 +1218,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                     if (d0 + j < nb) local += cnt_d[d0 + j];
                 uint32_t tot;
                 uint32_t run = block_exclusive_scan_t<BLOCK / 64>(local, tmp, tot);
+                cnt = tot;
                 for (uint32_t j = 0; j < dpt; j++) {
                     const uint32_t d = d0 + j;
                     if (d < nb) {
@@ -1209,13 +1231,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
             __syncthreads();
 #pragma unroll
             for (int i = 0; i < ITEMS; i++) {
-                const uint32_t e = wbase + i * 64 + lane;
-                if (e < cnt) skey[cnt_d[dig[i]] + rank[i]] = key[i];
+                if ((vm >> i) & 1u) skey[cnt_d[dig[i]] + rank[i]] = key[i];
             }
             // the next tile's keys go out now, into the same registers
             const uint32_t next = tile + g8;
-            uint32_t ncnt = 0, nd1 = 0;
-            load(next < t_hi ? next : tile, ncnt, nd1);
+            uint32_t nvm = 0, nd1 = 0;
+            load(next < t_hi ? next : tile, nvm, nd1);
             __syncthreads();
             // probe in grouped order: consecutive lanes mostly share a table
 #pragma unroll
@@ -1259,7 +1280,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
             }
             if (next >= t_hi) break;
             tile = next;
-            cnt = ncnt;
+            vm = nvm;
             d1 = nd1;
             __syncthreads();   // LDS reads of this tile before the next tile's counts
         }

@@ -554,22 +554,36 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(PassArgs a) {
 // loaded beside its cursor add, or else waits for the table entry: that
 // chunk's owner claimed earlier, so it is resident and publishes without
 // waiting, and the wait always ends.
-template <int BLOCK, int ITEMS, int HK>
+//
+// VAR bit 0 (the tile's order is free here): rank by one LDS atomic per tuple
+// on a single per-digit counter row instead of the stable 64-lane match
+// ranking (nbits + 1 ballots per tuple). VAR bit 1: the sorted tile is held as
+// 16-B tuples (one ds_write_b128 / ds_read_b128 per tuple instead of two
+// 8-B column accesses).
+template <int BLOCK, int ITEMS, int HK, int VAR = 0>
 __global__ __launch_bounds__(BLOCK)
 __attribute__((amdgpu_waves_per_eu((BLOCK * ITEMS <= 4096 ? 2 : 1) * BLOCK / 256)))   // what the LDS lets share a CU
 void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
     constexpr int NW = BLOCK / 64;
     constexpr int T = BLOCK * ITEMS;
+    constexpr bool ARANK = (VAR & 1) != 0, LAOS = (VAR & 2) != 0;
+    // both: a digit's three write offsets packed in one 16-B LDS entry (one
+    // ds_read_b128 per tuple in the write loop), placed in the counter rows
+    // the atomic ranking leaves unused
+    constexpr bool PACK = ARANK && LAOS && NW >= 8;
+    constexpr int NWR = ARANK ? 1 : NW;   // counter rows
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t nb = a.nbins;
     int64_t* skey = reinterpret_cast<int64_t*>(smem);
     int64_t* spay = skey + T;
+    longlong2* stup = reinterpret_cast<longlong2*>(smem);     // LAOS: [T] tuples over skey/spay
     uint32_t* wcnt = reinterpret_cast<uint32_t*>(spay + T);  // [NW][nb]
     uint32_t* gofs = wcnt + NW * nb;                          // [nb] k <  dsplit: slot = gofs + k
     uint32_t* dstart = gofs + nb;                             // [nb] k >= dsplit: slot = dstart + k
     uint32_t* tmp = dstart + nb;                              // 16 words
     const SortedDigits sdig{tmp + 16, nb <= 256};             // [T]
     uint32_t* dsplit = static_cast<uint32_t*>(sdig.end(T));   // [nb]
+    uint4* wdesc = reinterpret_cast<uint4*>(wcnt + ((nb + 3u) & ~3u));   // PACK: [nb] {k < split: slot - k, else, split}
 
     const uint32_t x = blockIdx.x % a.nshards, slots = gridDim.x / a.nshards;
     const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -610,23 +624,27 @@ void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
 
     for (;;) {
         const uint32_t lo = tile * T, cnt = min(static_cast<uint32_t>(T), a.n - lo);
-        for (uint32_t i = tid; i < NW * nb; i += BLOCK) wcnt[i] = 0;
+        for (uint32_t i = tid; i < NWR * nb; i += BLOCK) wcnt[i] = 0;
         __syncthreads();
         uint32_t dig[ITEMS], rank[ITEMS];
-        uint32_t* my = wcnt + wave * nb;
+        uint32_t* my = wcnt + (ARANK ? 0u : wave * nb);
 #pragma unroll
         for (int i = 0; i < ITEMS; i++) {
             const uint32_t e = wbase + i * 64 + lane;
             const bool valid = e < cnt;
             const uint32_t d = valid ? digit_of<HK>(static_cast<uint64_t>(key[i]), a.f) : 0u;
-            const uint64_t peers = match_digit(d, valid, a.nbits);
             dig[i] = d;
             rank[i] = 0;
-            if (valid) {
-                const uint32_t before = my[d];
-                const uint64_t lt = peers & lanemask_lt();
-                rank[i] = before + __popcll(lt);
-                if (lt == 0) my[d] = before + __popcll(peers);
+            if constexpr (ARANK) {
+                if (valid) rank[i] = atomicAdd(&my[d], 1u);
+            } else {
+                const uint64_t peers = match_digit(d, valid, a.nbits);
+                if (valid) {
+                    const uint32_t before = my[d];
+                    const uint64_t lt = peers & lanemask_lt();
+                    rank[i] = before + __popcll(lt);
+                    if (lt == 0) my[d] = before + __popcll(peers);
+                }
             }
         }
         __syncthreads();
@@ -636,14 +654,14 @@ void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
         {
             if (tid < nb) {
 #pragma unroll
-                for (int w = 0; w < NW; w++) c += wcnt[w * nb + tid];
+                for (int w = 0; w < NWR; w++) c += wcnt[w * nb + tid];
             }
             uint32_t total;
             uint32_t run = block_exclusive_scan_t<NW>(c, tmp, total);
             ds = run;
             if (tid < nb) {
 #pragma unroll
-                for (int w = 0; w < NW; w++) {
+                for (int w = 0; w < NWR; w++) {
                     const uint32_t v = wcnt[w * nb + tid];
                     wcnt[w * nb + tid] = run;
                     run += v;
@@ -666,8 +684,12 @@ void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
             const uint32_t e = wbase + i * 64 + lane;
             if (e < cnt) {
                 const uint32_t pos = my[dig[i]] + rank[i];
-                skey[pos] = key[i];
-                spay[pos] = pay[i];
+                if constexpr (LAOS) {
+                    stup[pos] = make_longlong2(key[i], pay[i]);
+                } else {
+                    skey[pos] = key[i];
+                    spay[pos] = pay[i];
+                }
                 sdig.put(pos, dig[i]);
             }
         }
@@ -709,9 +731,13 @@ void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
             }
             // sorted element k of digit d goes to chain slot v0 + (k - ds)
             const uint32_t split = ds + (T - off);
-            gofs[d] = id0 * T + off - ds;      // k <  split: chunk k0
-            dstart[d] = id1 * T - split;       // k >= split: chunk k1 (uint32 wrap-around)
-            dsplit[d] = split;
+            if constexpr (PACK) {
+                wdesc[d] = make_uint4(id0 * T + off - ds, id1 * T - split, split, 0u);
+            } else {
+                gofs[d] = id0 * T + off - ds;      // k <  split: chunk k0
+                dstart[d] = id1 * T - split;       // k >= split: chunk k1 (uint32 wrap-around)
+                dsplit[d] = split;
+            }
         }
         __syncthreads();
 #pragma unroll
@@ -719,15 +745,260 @@ void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
             const uint32_t k = i * BLOCK + tid;
             if (k < cnt) {
                 const uint32_t d = sdig.get(k);
-                const uint32_t o = (k < dsplit[d] ? gofs[d] : dstart[d]) + k;
-                store_tuple<true>(a, o, skey[k], spay[k]);
-                if (a.out_dig) store_next_digit<HK>(a, o, skey[k]);
+                uint32_t o;
+                if constexpr (PACK) {
+                    const uint4 w = wdesc[d];
+                    o = (k < w.z ? w.x : w.y) + k;
+                } else {
+                    o = (k < dsplit[d] ? gofs[d] : dstart[d]) + k;
+                }
+                int64_t tk, tp;
+                if constexpr (LAOS) {
+                    const longlong2 t = stup[k];
+                    tk = t.x;
+                    tp = t.y;
+                } else {
+                    tk = skey[k];
+                    tp = spay[k];
+                }
+                store_tuple<true>(a, o, tk, tp);
+                if (a.out_dig) store_next_digit<HK>(a, o, tk);
             }
         }
         if (next >= t_end) break;
         tile = next;
         __syncthreads();   // LDS reads of this tile's stores before the next tile's counts
     }
+}
+
+// ---------------------------------------------------------------------------
+// Pass 1 into workgroup-private chains (unordered partitions, consumed by the
+// on-chip pass-2 probe). Every persistent workgroup w owns a contiguous run
+// of tiles and a private region of 64-slot chunks; digit d of w is a chain of
+// chunks whose state (open chunk, its fill, chunks taken) lives in thread d's
+// registers. A tile's run of digit d fills the open chunk, then as many fresh
+// chunks as it needs, taken consecutively from the region by one block scan
+// of (count | chunks << 16) that also gives the tile-local digit starts. So
+// no atomic leaves the CU, and the partial lines of a chain are only ever
+// written by one CU (one L2). Each fresh chunk's (digit, rank in its chain)
+// goes to a log; k_priv_offsets / k_priv_finish / k_priv_list turn the logs
+// into per-digit chunk lists, which the probe reads 64 chunks (one per wave
+// row) per tile. Reference: the per-worker scatter of HashJoin.hpp:394-412
+// (same partition contents; order inside a partition unspecified).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kPrivCh = 64;         // slots per chunk = lanes of a probe row
+constexpr uint32_t kPrivRankBits = 21;   // log entry: (digit << 21) | rank in chain
+
+__host__ __device__ constexpr size_t scatter_priv_lds_bytes(int T, uint32_t nb) {
+    return static_cast<size_t>(T) * (nb <= 256 ? 17 : 18) + static_cast<size_t>((nb + 3u) & ~3u) * 4 +
+           static_cast<size_t>(nb) * 16 + 64;
+}
+
+struct PrivArgs {
+    uint32_t* log;       // [chunk id] (digit << kPrivRankBits) | rank of the chunk in its chain
+    uint32_t* ccount;    // [wg][nb] chunks of chain (wg, d)
+    uint32_t* clast;     // [wg][nb] its last chunk
+    uint32_t* cfill;     // [wg][nb] tuples in that chunk (1..64; 0 for an empty chain)
+    uint32_t* nused;     // [wg] chunks taken
+    uint32_t rchunks;    // chunks reserved per workgroup (>= per * T / 64 + nb)
+    uint32_t per;        // tiles per workgroup
+    uint32_t ntiles;
+    uint32_t pad;
+};
+
+template <int BLOCK, int ITEMS, int HK>
+__global__ __launch_bounds__(BLOCK)
+__attribute__((amdgpu_waves_per_eu((BLOCK * ITEMS <= 4096 ? 2 : 1) * BLOCK / 256)))   // what the LDS lets share a CU
+void k_scatter_priv(PassArgs a, PrivArgs q) {
+    constexpr int NW = BLOCK / 64;
+    constexpr int T = BLOCK * ITEMS;
+    constexpr uint32_t CH = kPrivCh;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t nb = a.nbins;
+    longlong2* stup = reinterpret_cast<longlong2*>(smem);                    // [T] the sorted tile
+    uint32_t* wcnt = reinterpret_cast<uint32_t*>(stup + T);                  // [nb] counts, then starts
+    uint4* wdesc = reinterpret_cast<uint4*>(wcnt + ((nb + 3u) & ~3u));       // [nb] {k < split: slot - k, else, split}
+    uint32_t* tmp = reinterpret_cast<uint32_t*>(wdesc + nb);                 // 16 words
+    const SortedDigits sdig{tmp + 16, nb <= 256};                            // [T]
+
+    const uint32_t w = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const uint32_t rb = w * q.rchunks;
+    uint32_t tile = w * q.per;
+    const uint32_t t_end = min(q.ntiles, tile + q.per);
+    const uint32_t wbase = wave * 64 * ITEMS;
+    uint32_t cur = 0, fill = CH, cc = 0, nxt = 0;   // chain (w, tid); fill == CH: no open chunk
+    int64_t key[ITEMS], pay[ITEMS];
+    const longlong2* rel = reinterpret_cast<const longlong2*>(a.in_keys);
+    auto load = [&](uint32_t t) {
+        const uint32_t lo = t * T;
+#pragma unroll
+        for (int i = 0; i < ITEMS; i++) {
+            const uint32_t ix = min(lo + wbase + i * 64 + lane, a.n - 1);
+            if (a.nt_load) {
+                typedef long long v2i __attribute__((ext_vector_type(2)));
+                const v2i v = __builtin_nontemporal_load(reinterpret_cast<const v2i*>(rel) + ix);
+                key[i] = v.x;
+                pay[i] = v.y;
+            } else {
+                const longlong2 v = rel[ix];
+                key[i] = v.x;
+                pay[i] = v.y;
+            }
+        }
+    };
+    if (tile < t_end) load(tile);
+    while (tile < t_end) {
+        const uint32_t lo = tile * T, cnt = min(static_cast<uint32_t>(T), a.n - lo);
+        for (uint32_t i = tid; i < nb; i += BLOCK) wcnt[i] = 0;
+        __syncthreads();
+        uint32_t dig[ITEMS], rank[ITEMS];
+#pragma unroll
+        for (int i = 0; i < ITEMS; i++) {
+            const uint32_t e = wbase + i * 64 + lane;
+            const bool valid = e < cnt;
+            const uint32_t d = valid ? digit_of<HK>(static_cast<uint64_t>(key[i]), a.f) : 0u;
+            dig[i] = d;
+            rank[i] = valid ? atomicAdd(&wcnt[d], 1u) : 0u;
+        }
+        __syncthreads();
+        const uint32_t c = tid < nb ? wcnt[tid] : 0u;
+        const uint32_t room = CH - fill;
+        const uint32_t m = c > room ? (c - room + CH - 1) / CH : 0u;
+        uint32_t tot;
+        const uint32_t ex = block_exclusive_scan_t<NW>(c | (m << 16), tmp, tot);
+        if (tid < nb && c) {
+            const uint32_t ds = ex & 0xffffu, nbase = rb + nxt + (ex >> 16);
+            wcnt[tid] = ds;
+            wdesc[tid] = make_uint4(cur * CH + fill - ds, nbase * CH - (ds + room), ds + room, 0u);
+            for (uint32_t j = 0; j < m; j++) q.log[nbase + j] = (tid << kPrivRankBits) | (cc + j);
+            if (m) {
+                cur = nbase + m - 1;
+                fill = c - room - (m - 1) * CH;
+                cc += m;
+            } else {
+                fill += c;
+            }
+        }
+        nxt += tot >> 16;
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < ITEMS; i++) {
+            const uint32_t e = wbase + i * 64 + lane;
+            if (e < cnt) {
+                const uint32_t pos = wcnt[dig[i]] + rank[i];
+                stup[pos] = make_longlong2(key[i], pay[i]);
+                sdig.put(pos, dig[i]);
+            }
+        }
+        const uint32_t next = tile + 1;
+        load(next < t_end ? next : tile);   // unconditional (a last one goes unused)
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < ITEMS; i++) {
+            const uint32_t k = i * BLOCK + tid;
+            if (k < cnt) {
+                const uint4 wd = wdesc[sdig.get(k)];
+                const longlong2 t = stup[k];
+                store_tuple<true>(a, (k < wd.z ? wd.x : wd.y) + k, t.x, t.y);
+            }
+        }
+        tile = next;
+        __syncthreads();   // LDS reads of this tile before the next tile's counts
+    }
+    for (uint32_t d = tid; d < nb; d += BLOCK) {   // d == tid (host: nb <= BLOCK)
+        const size_t i = static_cast<size_t>(w) * nb + d;
+        q.ccount[i] = cc;
+        q.clast[i] = cur;
+        q.cfill[i] = cc ? fill : 0u;
+    }
+    if (tid == 0) q.nused[w] = nxt;
+}
+
+// Per digit d (one workgroup each): offw[d][w] = chunks of chains (w' < w, d),
+// nch[d] = chunks of digit d, ntup[d] = its tuples.
+__global__ __launch_bounds__(kBlock) void k_priv_offsets(const uint32_t* ccount, const uint32_t* cfill, uint32_t G,
+                                                         uint32_t nb, uint32_t* offw, uint32_t* nch, uint32_t* ntup) {
+    __shared__ uint32_t tmp[16];
+    const uint32_t d = blockIdx.x, tid = threadIdx.x;
+    uint32_t carry = 0, tup = 0;
+    for (uint32_t w0 = 0; w0 < G; w0 += kBlock) {
+        const uint32_t w = w0 + tid;
+        const uint32_t v = w < G ? ccount[static_cast<size_t>(w) * nb + d] : 0u;
+        if (v) tup += (v - 1) * kPrivCh + cfill[static_cast<size_t>(w) * nb + d];
+        uint32_t tot;
+        const uint32_t ex = block_exclusive_scan(v, tmp, tot);
+        if (w < G) offw[static_cast<size_t>(d) * G + w] = carry + ex;
+        carry += tot;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) tup += __shfl_xor(tup, o, 64);
+    if ((tid & 63) == 0) tmp[tid >> 6] = tup;
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t t = 0;
+        for (int i = 0; i < kWaves; i++) t += tmp[i];
+        nch[d] = carry;
+        ntup[d] = t;
+    }
+}
+
+// One workgroup, nb <= 1024: ebase = exclusive scan of nch (entry offsets),
+// tile_base2 = exclusive scan of ceil(nch / 64) (probe tiles of 64 chunks),
+// bounds1 = exclusive scan of ntup (the pass-1 partition bounds).
+__global__ __launch_bounds__(1024) void k_priv_finish(const uint32_t* nch, const uint32_t* ntup, uint32_t nb,
+                                                      uint32_t* ebase, uint32_t* tile_base2, uint32_t* bounds1) {
+    __shared__ uint32_t tmp[3][16];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint32_t v[3] = {0, 0, 0};
+    if (tid < nb) {
+        v[0] = nch[tid];
+        v[1] = (v[0] + 63) / 64;
+        v[2] = ntup[tid];
+    }
+    uint32_t x[3] = {v[0], v[1], v[2]};
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            const uint32_t y = __shfl_up(x[j], o, 64);
+            if (lane >= (uint32_t)o) x[j] += y;
+        }
+    }
+    if (lane == 63) {
+#pragma unroll
+        for (int j = 0; j < 3; j++) tmp[j][wave] = x[j];
+    }
+    __syncthreads();
+    uint32_t b[3] = {0, 0, 0};
+    for (uint32_t w = 0; w < wave; w++) {
+#pragma unroll
+        for (int j = 0; j < 3; j++) b[j] += tmp[j][w];
+    }
+    if (tid < nb) {
+        ebase[tid] = b[0] + x[0] - v[0];
+        tile_base2[tid] = b[1] + x[1] - v[1];
+        bounds1[tid] = b[2] + x[2] - v[2];
+    }
+    if (tid == 1023) {
+        ebase[nb] = b[0] + x[0];
+        tile_base2[nb] = b[1] + x[1];
+        bounds1[nb] = b[2] + x[2];
+    }
+}
+
+// Every taken chunk g of workgroup w lands in its digit's list at
+// ebase[d] + offw[d][w] + rank: entry (g << 6) | (fill - 1).
+__global__ __launch_bounds__(kBlock) void k_priv_list(const uint32_t* log, const uint32_t* nused, const uint32_t* clast,
+                                                      const uint32_t* cfill, const uint32_t* offw, const uint32_t* ebase,
+                                                      uint32_t G, uint32_t nb, uint32_t rchunks, uint32_t* ent) {
+    const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t w = g / rchunks;
+    if (w >= G || g - w * rchunks >= nused[w]) return;
+    const uint32_t e = log[g];
+    const uint32_t d = e >> kPrivRankBits, r = e & ((1u << kPrivRankBits) - 1);
+    const size_t cw = static_cast<size_t>(w) * nb + d;
+    const uint32_t fill = g == clast[cw] ? cfill[cw] : kPrivCh;
+    ent[ebase[d] + offw[static_cast<size_t>(d) * G + w] + r] = (g << 6) | (fill - 1);
 }
 
 // ---------------------------------------------------------------------------

@@ -19,12 +19,26 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP kernels)")
 
 
+_GPU = None
+
+
 def _gpu_available():
-    try:
-        import torch
-        return torch.cuda.is_available()
-    except Exception:
-        return False
+    # Asked once, before any test has loaded libphj_hip.so: torch carries its
+    # own HIP/HSA runtime, which does not see the card if the system runtime
+    # (the library's) opened it first.
+    global _GPU
+    if _GPU is None:
+        try:
+            import torch
+            _GPU = torch.cuda.is_available()
+        except Exception:
+            _GPU = False
+    return _GPU
+
+
+def pytest_collection_modifyitems(config, items):
+    if any(it.get_closest_marker("gpu") for it in items):
+        _gpu_available()
 
 
 @pytest.fixture(scope="session")

@@ -8,7 +8,7 @@ digit column (PHJ_DCOL), tile order
 (PHJ_XCD_REMAP), write-combining scatter (PHJ_WC), the one-pass limit of
 hash % P (PHJ_ONEPASS_MAX), the join's sub-partitioning of large partitions
 (PHJ_SUBPART), the chunked pass 1 of unordered partitions (PHJ_P1_CHUNK) and its
-persistent workgroups per shard (PHJ_P1_SLOTS) and shard count (PHJ_P1_TPS), fused LDS join vs HBM tables (PHJ_FUSED), the
+persistent workgroups per shard (PHJ_P1_SLOTS), shard count (PHJ_P1_TPS) and tile ranking / LDS layout (PHJ_P1_VAR), the workgroup-private chains of the on-chip probe's pass 1 (PHJ_P1_PRIV), fused LDS join vs HBM tables (PHJ_FUSED), the
 partitioned bucket tables vs CSR tables (PHJ_PTAB) and the CSR probe
 schedule (PHJ_PROBE_WAVE, PHJ_PROBE_ITEMS). Each is
 checked against the oracle's stable partition (or, for the unordered layout,
@@ -68,6 +68,15 @@ SCHEDULES = [
     {"PHJ_NP_COOP": "1"},                                       # ... four lanes per bucket
     {"PHJ_P2PROBE": "0"},                                       # radix: probe side's pass 2 through HBM
     {"PHJ_P2PROBE": "0", "PHJ_P1_MIN_TILES": "0"},              # ... after the chunked pass 1
+    {"PHJ_P1_PRIV": "1"},                                       # on-chip probe after workgroup-private chains
+    {"PHJ_P1_PRIV": "1", "PHJ_P1_BITS": "5"},                   # ... pass split 5 + rest
+    {"PHJ_P1_BITS": "6"},                                       # shared chains, pass split 6 + rest
+    {"PHJ_NP_RATIO": "1.25"},                                   # NoPartitioning default table ratio
+    {"PHJ_P1_MIN_TILES": "0", "PHJ_P1_VAR": "0"},               # chunked pass 1: stable ballot ranking
+    {"PHJ_P1_MIN_TILES": "0", "PHJ_P1_VAR": "1"},               # ... LDS-atomic ranking
+    {"PHJ_P1_MIN_TILES": "0", "PHJ_P1_VAR": "2"},               # ... tuple-wide LDS tile
+    {"PHJ_P1_MIN_TILES": "0", "PHJ_P1_VAR": "3"},               # ... both, packed write offsets
+    {"PHJ_P1_MIN_TILES": "0", "PHJ_P1_VAR": "3", "PHJ_BLOCK": "256", "PHJ_TILE": "4096"},  # ... 4 waves: no packing
 ]
 
 CASES = [((8, 8), 0, phj.HASH_MURMUR3), ((11, 0), 0, phj.HASH_XXH3), ((1, 0), 1000, phj.HASH_XXH3),
