@@ -75,6 +75,7 @@ struct Tuning {
     int p2probe = 1;         // radix join, 2 passes: the probe side's pass 2 on-chip (k_probe_p1)
     int p1_priv = 0;
     int p1_bits = 0;
+    int p1_ko = 1;           // chunked pass 1 consumed by the counting probe: keys only (k_scatter_chunked VAR 5)
     double np_ratio = kNPDefaultRatio;   // NoPartitioning: slots per build tuple when the params leave it 0         // 2-pass join: pass-1 digit bits (0: the plan's split; rebalance_plan)         // pass 1 consumed on chip: workgroup-private chains (k_scatter_priv)
     int p1_var = 3;          // chunked pass 1 variant (k_scatter_chunked VAR: 1 atomic rank, 2 tuple LDS)
 };
@@ -505,18 +506,19 @@ int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const st
         // counter start at zero
         PHJ_HIP(c, hipMemsetAsync(a.chunk_cursor, 0, chunk_state_bytes(a.nbins), c->ks));
         c->since_ev++;
-        PHJ_TRY(timer_begin(c, sname.c_str(), n * 32 + (a.out_dig ? n * (a.dig_wide ? 2 : 1) : 0)));
+        PHJ_TRY(timer_begin(c, sname.c_str(), n * (a.keys_only ? 24 : 32) + (a.out_dig ? n * (a.dig_wide ? 2 : 1) : 0)));
         if constexpr (IN_AOS && OUT_AOS && ITEMS <= 8) {
             // persistent: as many workgroups per shard as fit the chip at once
             // (two per CU at 81 KB of LDS), never more than the shard's tiles
             const uint32_t ntiles = static_cast<uint32_t>((n + T - 1) / T);
             const uint32_t per = (ntiles + a.nshards - 1) / a.nshards;
-            const uint32_t fit = std::max<uint32_t>(1, static_cast<uint32_t>(160 * 1024 / sc_lds));
+            const size_t lds = a.keys_only ? sc_lds - static_cast<size_t>(T) * 8 : sc_lds;   // no payload rows
+            const uint32_t fit = std::max<uint32_t>(1, static_cast<uint32_t>(160 * 1024 / lds));
             uint32_t slots = std::max<uint32_t>(1, std::min<uint32_t>(per, fit * c->num_cus / a.nshards));
             if (c->tune.p1_slots > 0) slots = std::min<uint32_t>(per, c->tune.p1_slots);
             if (c->tune.p1_slots < 0) slots = per;   // one tile per workgroup
             const void* kfn = nullptr;
-            switch (c->tune.p1_var & 3) {
+            switch (a.keys_only ? 5 : (c->tune.p1_var & 3)) {
 #define PHJ_P1_VARIANT(V)                                                                            \
     case V:                                                                                          \
         kfn = hk == kMurmur3 ? reinterpret_cast<const void*>(&k_scatter_chunked<BLOCK, ITEMS, kMurmur3, V>) \
@@ -526,11 +528,12 @@ int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const st
                 PHJ_P1_VARIANT(1)
                 PHJ_P1_VARIANT(2)
                 PHJ_P1_VARIANT(3)
+                PHJ_P1_VARIANT(5)
 #undef PHJ_P1_VARIANT
             }
             PassArgs ak = a;
             void* kargs[] = {&ak, const_cast<uint32_t*>(&ntiles), const_cast<uint32_t*>(&per)};
-            PHJ_HIP(c, hipLaunchKernel(kfn, dim3(slots * a.nshards), dim3(BLOCK), kargs, sc_lds, c->ks));
+            PHJ_HIP(c, hipLaunchKernel(kfn, dim3(slots * a.nshards), dim3(BLOCK), kargs, lds, c->ks));
             PHJ_LAUNCHED(c, sname);
         } else {
             (void)grid;
@@ -801,6 +804,8 @@ int partition_side(phj_ctx* c, int s, const Plan& pl, bool p1_only = false) {
         a.dig2_mask = pl.dmask2;
     }
     if (chunked) {
+        // the counting probe consumes pass 1 on chip and reads only keys
+        a.keys_only = p1_only && c->tune.p1_ko ? 1u : 0u;
         a.chunk_cursor = static_cast<uint32_t*>(S.ccur.p);
         a.chunk_tab = static_cast<unsigned long long*>(S.ctab.p);
         a.maxch = maxch;
@@ -881,6 +886,7 @@ int partition_side(phj_ctx* c, int s, const Plan& pl, bool p1_only = false) {
         b.tile_base = tb2;
         b.tile_seg = static_cast<const uint32_t*>(S.tseg2.p);
         b.nseg = pl.nb1;
+        b.keys_only = a.keys_only;
         if (n) {
             if (chunked) {
                 uint32_t* ts = static_cast<uint32_t*>(S.tstart.p);
@@ -1698,6 +1704,7 @@ int ctx_create_device(int device, phj_ctx** out) {
     // partial 64-B segments are written separately (WRREQ 61M vs 52M)
     c->tune.p1_priv = env_int("PHJ_P1_PRIV", 0);
     c->tune.p1_bits = std::max(0, env_int("PHJ_P1_BITS", 0));
+    c->tune.p1_ko = env_int("PHJ_P1_KO", 1);
     if (const char* r = std::getenv("PHJ_NP_RATIO")) c->tune.np_ratio = std::max(1.0, std::atof(r));
     c->tune.p1_slots = env_int("PHJ_P1_SLOTS", 0);
     c->tune.p1_tps = std::max(1, env_int("PHJ_P1_TPS", static_cast<int>(kTilesPerShard)));
@@ -2093,9 +2100,9 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
         PHJ_TRY(rc);
         PHJ_HIP(c, hipStreamWaitEvent(c->stream, tr, 0));
         PHJ_TRY(mark(c, &t1));
-        // algorithmic bytes: the pass-1 tuples read once (16 B); the CSR tables
-        // are re-read from L2, not HBM
-        PHJ_TRY(timer_begin(c, "probe", S.n * 16));
+        // algorithmic bytes: the pass-1 output read once (16-B tuples, or 8-B
+        // keys after a keys-only pass 1); the CSR tables are re-read from L2
+        PHJ_TRY(timer_begin(c, "probe", S.n * (S.p2.keys_only ? 8 : 16)));
         PHJ_TRY(probe_p1(c, pl));
         PHJ_TRY(timer_end(c));
         PHJ_TRY(mark(c, &p1));

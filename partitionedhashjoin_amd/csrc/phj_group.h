@@ -473,7 +473,7 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
     PHJ_HIP(c, hipStreamWaitEvent(c->stream, p2 ? b1 : x1, 0));
     PHJ_TRY(mark(c, &t1));
     if (p2) {
-        PHJ_TRY(timer_begin(c, "probe", c->side[PHJ_SIDE_PROBE].n * 16));
+        PHJ_TRY(timer_begin(c, "probe", c->side[PHJ_SIDE_PROBE].n * (c->side[PHJ_SIDE_PROBE].p2.keys_only ? 8 : 16)));
         PHJ_TRY(probe_p1(c, pl));
         PHJ_TRY(timer_end(c));
         PHJ_TRY(mark(c, &p1));

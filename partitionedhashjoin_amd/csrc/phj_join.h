@@ -1185,7 +1185,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
             locate_tile<T>(a, t, L);
             const uint32_t c = L.hi - L.lo;
             // pass-1 output as AoS tuples (the default) or as a key column (PHJ_P1_AOS=0)
-            const bool soa = a.in_pays != nullptr;
+            const bool soa = a.in_pays != nullptr || a.keys_only;
 #pragma unroll
             for (int i = 0; i < ITEMS; i++) {
                 const uint32_t e = wbase + i * 64 + lane;

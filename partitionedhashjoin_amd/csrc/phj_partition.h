@@ -126,7 +126,7 @@ struct PassArgs {
     uint32_t maxch;             // chunks of one chain (bound)
     uint32_t pool_stride;       // chunks of one shard's pool
     uint32_t nshards;           // chains per digit (<= kShards)
-    uint32_t pad3;
+    uint32_t keys_only;         // chunked pass 1 for the counting probe: only the key column is written / read
     DigitFn f;
 };
 
@@ -559,25 +559,28 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(PassArgs a) {
 // on a single per-digit counter row instead of the stable 64-lane match
 // ranking (nbits + 1 ballots per tuple). VAR bit 1: the sorted tile is held as
 // 16-B tuples (one ds_write_b128 / ds_read_b128 per tuple instead of two
-// 8-B column accesses).
+// 8-B column accesses). VAR bit 2 (the counting probe consumes the output,
+// HashJoin.hpp:295-301 reads only the key): keys only, loaded, sorted and
+// written (8 B per tuple out instead of 16; half the LDS, three workgroups
+// per CU).
 template <int BLOCK, int ITEMS, int HK, int VAR = 0>
 __global__ __launch_bounds__(BLOCK)
-__attribute__((amdgpu_waves_per_eu((BLOCK * ITEMS <= 4096 ? 2 : 1) * BLOCK / 256)))   // what the LDS lets share a CU
+__attribute__((amdgpu_waves_per_eu(((VAR & 4) ? 3 : (BLOCK * ITEMS <= 4096 ? 2 : 1)) * BLOCK / 256)))   // what the LDS lets share a CU
 void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
     constexpr int NW = BLOCK / 64;
     constexpr int T = BLOCK * ITEMS;
-    constexpr bool ARANK = (VAR & 1) != 0, LAOS = (VAR & 2) != 0;
-    // both: a digit's three write offsets packed in one 16-B LDS entry (one
-    // ds_read_b128 per tuple in the write loop), placed in the counter rows
-    // the atomic ranking leaves unused
-    constexpr bool PACK = ARANK && LAOS && NW >= 8;
+    constexpr bool ARANK = (VAR & 1) != 0, KO = (VAR & 4) != 0, LAOS = (VAR & 2) != 0 && !KO;
+    // atomic ranking + one 16-B access per element: a digit's three write
+    // offsets packed in one 16-B LDS entry (one ds_read_b128 per element in
+    // the write loop), placed in the counter rows the atomic ranking leaves unused
+    constexpr bool PACK = ARANK && (LAOS || KO) && NW >= 8;
     constexpr int NWR = ARANK ? 1 : NW;   // counter rows
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t nb = a.nbins;
     int64_t* skey = reinterpret_cast<int64_t*>(smem);
     int64_t* spay = skey + T;
     longlong2* stup = reinterpret_cast<longlong2*>(smem);     // LAOS: [T] tuples over skey/spay
-    uint32_t* wcnt = reinterpret_cast<uint32_t*>(spay + T);  // [NW][nb]
+    uint32_t* wcnt = reinterpret_cast<uint32_t*>(KO ? skey + T : spay + T);  // [NW][nb]
     uint32_t* gofs = wcnt + NW * nb;                          // [nb] k <  dsplit: slot = gofs + k
     uint32_t* dstart = gofs + nb;                             // [nb] k >= dsplit: slot = dstart + k
     uint32_t* tmp = dstart + nb;                              // 16 words
@@ -608,7 +611,11 @@ void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
 #pragma unroll
         for (int i = 0; i < ITEMS; i++) {
             const uint32_t ix = min(lo + wbase + i * 64 + lane, a.n - 1);
-            if (a.nt_load) {
+            if constexpr (KO) {
+                pay[i] = 0;
+                if (a.nt_load) key[i] = __builtin_nontemporal_load(&rel[ix].x);
+                else key[i] = rel[ix].x;
+            } else if (a.nt_load) {
                 typedef long long v2i __attribute__((ext_vector_type(2)));
                 const v2i v = __builtin_nontemporal_load(reinterpret_cast<const v2i*>(rel) + ix);
                 key[i] = v.x;
@@ -684,7 +691,9 @@ void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
             const uint32_t e = wbase + i * 64 + lane;
             if (e < cnt) {
                 const uint32_t pos = my[dig[i]] + rank[i];
-                if constexpr (LAOS) {
+                if constexpr (KO) {
+                    skey[pos] = key[i];
+                } else if constexpr (LAOS) {
                     stup[pos] = make_longlong2(key[i], pay[i]);
                 } else {
                     skey[pos] = key[i];
@@ -753,7 +762,10 @@ void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
                     o = (k < dsplit[d] ? gofs[d] : dstart[d]) + k;
                 }
                 int64_t tk, tp;
-                if constexpr (LAOS) {
+                if constexpr (KO) {
+                    a.out_keys[o] = skey[k];
+                    continue;
+                } else if constexpr (LAOS) {
                     const longlong2 t = stup[k];
                     tk = t.x;
                     tp = t.y;
