@@ -1151,6 +1151,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
     uint32_t* cnt_d = reinterpret_cast<uint32_t*>(sdesc + nb);    // [nb] counts, then starts
     uint32_t* tmp = cnt_d + nb;                                   // 16 words
     __shared__ uint32_t red[BLOCK / 64];
+    // (measured: carrying the digit and bucket bits beside the key in LDS
+    // instead of re-hashing after the grouping costs registers: 25 VGPRs
+    // spilled at 6 waves/SIMD, probe 1.27 -> 1.44 ms)
 
     const uint32_t total = a.tile_base[a.nseg];
     const uint32_t xcd = blockIdx.x & 7u, g8 = gridDim.x >> 3;
@@ -1194,12 +1197,15 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
             }
         };
         load(tile, vm, d1);
+        uint32_t staged = 0xffffffffu;   // d1 whose table descriptors sit in LDS
         for (;;) {
             const uint32_t pbase = d1 * pa.nb2;
+            const bool restage = d1 != staged;   // consecutive tiles mostly share d1
             for (uint32_t d = tid; d < nb; d += BLOCK) {
                 cnt_d[d] = 0;
-                sdesc[d] = pa.desc[pbase + d];
+                if (restage) sdesc[d] = pa.desc[pbase + d];
             }
+            staged = d1;
             __syncthreads();
             uint32_t dig[ITEMS], rank[ITEMS];
 #pragma unroll
@@ -1271,10 +1277,20 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                         o1[i] = ob.y;
                     }
                 }
+                // the first two keys of every bucket are requested together (one
+                // L2 round trip for all PB probes; buckets average ~1.5 keys),
+                // the rest walked only when a bucket holds more
+                int64_t f[PB][2];
 #pragma unroll
                 for (int i = 0; i < PB; i++) {
-                    bool hit = DIAG == 1 && ds[i].w != 0;
-                    for (uint32_t j = o0[i]; j < o1[i] && !hit; j++) hit = pa.tkeys[ds[i].x + j] == k2[i];
+#pragma unroll
+                    for (int j = 0; j < 2; j++) f[i][j] = o0[i] + j < o1[i] ? pa.tkeys[ds[i].x + o0[i] + j] : 0;
+                }
+#pragma unroll
+                for (int i = 0; i < PB; i++) {
+                    bool hit = (DIAG == 1 && ds[i].w != 0) || (o0[i] < o1[i] && f[i][0] == k2[i]) ||
+                               (o0[i] + 1 < o1[i] && f[i][1] == k2[i]);
+                    for (uint32_t j = o0[i] + 2; j < o1[i] && !hit; j++) hit = pa.tkeys[ds[i].x + j] == k2[i];
                     hits += hit ? 1u : 0u;
                 }
             }
