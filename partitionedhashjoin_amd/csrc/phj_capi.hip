@@ -64,6 +64,8 @@ struct Tuning {
     int p1_slots = 0;     // chunked pass 1: workgroups per shard (0 = fill the chip once, -1 = one per tile)
     int p1_tps = static_cast<int>(kTilesPerShard);   // chunked pass 1: tiles per shard (sets the shard count)
     int p1_min_tiles = 32768;  // chunked pass 1: smallest relation (in 4096-tuple tiles, ~134M tuples)
+    int p1_ko_tps = 1024;      // ... the keys-only form for the counting probe: tiles per shard
+    int p1_ko_min_tiles = 0;   // ... and its smallest relation (measured: wins at 25M-200M)
     int np_nt = 1;        // NoPartitioning probe: 1 nontemporal S loads, 2 also the bucket loads
     int np_items = 4;     // NoPartitioning probe: S keys per thread per round (4 or 8)
     bool np_region = true;   // NoPartitioning build: partition R into table regions, build each in LDS
@@ -725,15 +727,19 @@ int partition_side(phj_ctx* c, int s, const Plan& pl, bool p1_only = false) {
     // Measured: it pays at 200M tuples (16 chains per digit) and
     // loses to the stable pass below ~100M, where fewer shards (more
     // workgroups per cursor line) or more partial chunks cost more than the
-    // histogram read saves; so it starts at p1_min_tiles tiles.
+    // histogram read saves; so it starts at p1_min_tiles tiles. The keys-only
+    // form for the on-chip probe (half the bytes, three workgroups per CU)
+    // wins at every size measured (25M-200M), with shards of p1_ko_tps tiles.
+    const bool ko = p1_only && c->tune.p1_ko;
     const bool chunked = !priv && pl.npass == 2 && !pl.stable && c->tune.p1_chunk && (dcol || p1_only) && p1_aos && n > 0 &&
-                         nt1 >= static_cast<uint32_t>(c->tune.p1_min_tiles) &&
+                         nt1 >= static_cast<uint32_t>(ko ? c->tune.p1_ko_min_tiles : c->tune.p1_min_tiles) &&
                          tile == tile2 && pl.nb1 <= static_cast<uint32_t>(tile_shape(c, pl.nb1).block) &&
                          tile / tile_shape(c, pl.nb1).block <= 8 &&   // registers: the next tile is prefetched
                          (3 * (static_cast<uint64_t>(n) / tile + kShards) + kShards * pl.nb1) * tile < (1ull << 32);
     // chains per digit: ~kTilesPerShard tiles each, a power of two <= kShards
     uint32_t nshards = 1;
-    while (nshards < kShards && static_cast<uint64_t>(nshards) * c->tune.p1_tps < nt1) nshards <<= 1;
+    const uint32_t tps = static_cast<uint32_t>(ko ? c->tune.p1_ko_tps : c->tune.p1_tps);
+    while (nshards < kShards && static_cast<uint64_t>(nshards) * tps < nt1) nshards <<= 1;
     // pool of pass-1 chunks, one region per shard: a shard takes at most
     // `per` tiles, each with two chunks reserved up front (k_scatter_chunked;
     // unused ones are never touched), then at most per + nb1 chunks for its
@@ -805,7 +811,7 @@ int partition_side(phj_ctx* c, int s, const Plan& pl, bool p1_only = false) {
     }
     if (chunked) {
         // the counting probe consumes pass 1 on chip and reads only keys
-        a.keys_only = p1_only && c->tune.p1_ko ? 1u : 0u;
+        a.keys_only = ko ? 1u : 0u;
         a.chunk_cursor = static_cast<uint32_t*>(S.ccur.p);
         a.chunk_tab = static_cast<unsigned long long*>(S.ctab.p);
         a.maxch = maxch;
@@ -1709,6 +1715,8 @@ int ctx_create_device(int device, phj_ctx** out) {
     c->tune.p1_slots = env_int("PHJ_P1_SLOTS", 0);
     c->tune.p1_tps = std::max(1, env_int("PHJ_P1_TPS", static_cast<int>(kTilesPerShard)));
     c->tune.p1_min_tiles = std::max(0, env_int("PHJ_P1_MIN_TILES", 32768));
+    c->tune.p1_ko_tps = std::max(1, env_int("PHJ_P1_KO_TPS", 1024));
+    c->tune.p1_ko_min_tiles = std::max(0, env_int("PHJ_P1_KO_MIN_TILES", 0));
     {
         const int ev = env_int("PHJ_EVENTS", 1);   // 0 default, 1 no system fence, 2 device release
         c->tune.ev_flags = ev == 0 ? hipEventDefault : ev == 2 ? hipEventReleaseToDevice : hipEventDisableSystemFence;

@@ -10,6 +10,6 @@ for v in "$@"; do
 import json
 for l in open('gpurun_out/rehearse_ab.jsonl'):
     d=json.loads(l); k=d['kernels_ms']
-    print(d['world'], d['rank0_device_ms'], d['matches_rank0'], {a: v for a, v in k.items() if a.startswith('S') or a in ('build','probe','exchange')})
+    print(d['world'], d['rank0_device_ms'], d['matches_rank0'], k)
 "
 done
