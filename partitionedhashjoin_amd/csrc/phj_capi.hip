@@ -1301,6 +1301,9 @@ int probe_p1(phj_ctx* c, const Plan& pl) {
     if (diag == 1)
         kfn = pl.hk == kMurmur3 ? reinterpret_cast<const void*>(&k_probe_p1<512, 8, kMurmur3, 1>)
                                 : reinterpret_cast<const void*>(&k_probe_p1<512, 8, kXXH3, 1>);
+    else if (env_int("PHJ_P1_GRP", 1) == 0)   // measurement: keys probed ungrouped, from registers
+        kfn = pl.hk == kMurmur3 ? reinterpret_cast<const void*>(&k_probe_p1<512, 8, kMurmur3, 0, 4, false, false>)
+                                : reinterpret_cast<const void*>(&k_probe_p1<512, 8, kXXH3, 0, 4, false, false>);
     else if (pa.ent)   // tiles from the private chains' chunk lists
         kfn = pl.hk == kMurmur3 ? reinterpret_cast<const void*>(&k_probe_p1<512, 8, kMurmur3, 0, 6, true>)
                                 : reinterpret_cast<const void*>(&k_probe_p1<512, 8, kXXH3, 0, 6, true>);

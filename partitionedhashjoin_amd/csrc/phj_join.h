@@ -1139,7 +1139,7 @@ __global__ __launch_bounds__(kBlock) void k_csr_desc(const uint32_t* tkb, const 
 // ~1.2 8-B keys), as in the NoPartitioning probe a lane's four 16-B loads of
 // one bucket cost more than the extra dependent level. DIAG (timing only):
 // 1 = no table reads.
-template <int BLOCK, int ITEMS, int HK, int DIAG = 0, int WPE = 4, bool CHK = false>
+template <int BLOCK, int ITEMS, int HK, int DIAG = 0, int WPE = 4, bool CHK = false, bool GRP = true>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void k_probe_p1(P1ProbeArgs pa) {
     constexpr int T = BLOCK * ITEMS;
     constexpr int PB = 4;   // probes in flight per lane per batch
@@ -1207,6 +1207,62 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
             }
             staged = d1;
             __syncthreads();
+            if constexpr (!GRP) {
+                // ungrouped: every key probes straight from registers (hashed
+                // once); the next tile's keys load into a second register set
+                int64_t kc[ITEMS];
+#pragma unroll
+                for (int i = 0; i < ITEMS; i++) kc[i] = key[i];
+                const uint32_t vc = vm;
+                const uint32_t next = tile + g8;
+                uint32_t nvm = 0, nd1 = 0;
+                load(next < t_hi ? next : tile, nvm, nd1);
+#pragma unroll
+                for (int i0 = 0; i0 < ITEMS; i0 += PB) {
+                    uint4 ds[PB];
+                    uint32_t hb[PB];
+#pragma unroll
+                    for (int i = 0; i < PB; i++) {
+                        ds[i] = make_uint4(0, 0, 1, 0);
+                        hb[i] = 0;
+                        if ((vc >> (i0 + i)) & 1u) {
+                            const uint64_t h = hash64<HK>(static_cast<uint64_t>(kc[i0 + i]), pa.seed);
+                            hb[i] = static_cast<uint32_t>(h >> 32);
+                            ds[i] = sdesc[static_cast<uint32_t>(q_from_hash(h, a.f) >> a.f.shift) & a.f.dmask];
+                        }
+                    }
+                    uint32_t o0[PB], o1[PB];
+#pragma unroll
+                    for (int i = 0; i < PB; i++) {
+                        o0[i] = o1[i] = 0;
+                        if (ds[i].w) {
+                            typedef uint32_t u32x2 __attribute__((ext_vector_type(2), aligned(4)));
+                            const u32x2 ob = *reinterpret_cast<const u32x2*>(pa.toffs + ds[i].y + (hb[i] & (ds[i].z - 1u)));
+                            o0[i] = ob.x;
+                            o1[i] = ob.y;
+                        }
+                    }
+                    int64_t f[PB][2];
+#pragma unroll
+                    for (int i = 0; i < PB; i++) {
+#pragma unroll
+                        for (int j = 0; j < 2; j++) f[i][j] = o0[i] + j < o1[i] ? pa.tkeys[ds[i].x + o0[i] + j] : 0;
+                    }
+#pragma unroll
+                    for (int i = 0; i < PB; i++) {
+                        const int64_t k2 = kc[i0 + i];
+                        bool hit = (o0[i] < o1[i] && f[i][0] == k2) || (o0[i] + 1 < o1[i] && f[i][1] == k2);
+                        for (uint32_t j = o0[i] + 2; j < o1[i] && !hit; j++) hit = pa.tkeys[ds[i].x + j] == k2;
+                        hits += hit ? 1u : 0u;
+                    }
+                }
+                if (next >= t_hi) break;
+                tile = next;
+                vm = nvm;
+                d1 = nd1;
+                __syncthreads();   // sdesc reads of this tile before a restage
+                continue;
+            }
             uint32_t dig[ITEMS], rank[ITEMS];
 #pragma unroll
             for (int i = 0; i < ITEMS; i++) {
