@@ -1668,7 +1668,13 @@ int ctx_create_device(int device, phj_ctx** out) {
         delete c;
         return PHJ_ERR_HIP;
     }
-    if (hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess) {
+    // PHJ_AUX_PRIO=1: the build side's stream (R partition, exchange, tables:
+    // the multi-GPU step's critical chain) at the highest priority, so its
+    // small kernels are dispatched ahead of S's pass-1 workgroups
+    int least = 0, greatest = 0;
+    const bool prio = env_int("PHJ_AUX_PRIO", 0) != 0 && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess;
+    if ((prio ? hipStreamCreateWithPriority(&c->aux, hipStreamNonBlocking, greatest)
+              : hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking)) != hipSuccess) {
         (void)hipStreamDestroy(c->stream);
         delete c;
         return PHJ_ERR_HIP;

@@ -444,6 +444,16 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
                        hipMemcpyDeviceToDevice, c->ks) != hipSuccess)
         rc = set_err(c, PHJ_ERR_HIP, "pack bounds");
     c->since_ev += 2;
+    // the S shard's pass 1 is issued on the main stream BEFORE the exchange:
+    // an exchange with a host-side wait (the local rehearsal's barrier, a
+    // blocking collective) must not hold back S, which needs nothing from R
+    // (measured W=8 rehearsal: S.p1 started only after the exchange, 0.47 ms in)
+    const bool s_early = !(G.rehearse && i > 0);
+    if (rc == PHJ_OK && s_early) {
+        c->ks = c->stream;
+        rc = partition_side(c, PHJ_SIDE_PROBE, pl, p2);
+        c->ks = c->aux;
+    }
     if (rc == PHJ_OK) rc = mark(c, &x0);
     if (rc == PHJ_OK) rc = timer_begin(c, "exchange", static_cast<uint64_t>(G.world - 1) * L.elems * 8);
     const int rx = allgather_blocks(G, i, L.elems, rc == PHJ_OK);
@@ -468,8 +478,7 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
         r->total_ms = 0;
         return PHJ_OK;
     }
-    // S shard on the main stream, concurrently with R and the exchange
-    PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, pl, p2));
+    // (the S shard's pass 1 went out on the main stream before the exchange)
     PHJ_HIP(c, hipStreamWaitEvent(c->stream, p2 ? b1 : x1, 0));
     PHJ_TRY(mark(c, &t1));
     if (p2) {
