@@ -77,6 +77,8 @@ struct Tuning {
     int p2probe = 1;         // radix join, 2 passes: the probe side's pass 2 on-chip (k_probe_p1)
     int p1_priv = 0;
     int p1_bits = 0;
+    int p1_home = 1;         // on-chip probe reads one 16-B home slot per key (k_csr_home)
+    int p1_bshift = 0;       // CSR tables of the on-chip probe: buckets x 2^bshift
     int p1_ko = 1;           // chunked pass 1 consumed by the counting probe: keys only (k_scatter_chunked VAR 5)
     double np_ratio = kNPDefaultRatio;   // NoPartitioning: slots per build tuple when the params leave it 0         // 2-pass join: pass-1 digit bits (0: the plan's split; rebalance_plan)         // pass 1 consumed on chip: workgroup-private chains (k_scatter_priv)
     int p1_var = 3;          // chunked pass 1 variant (k_scatter_chunked VAR: 1 atomic rank, 2 tuple LDS)
@@ -159,6 +161,8 @@ struct phj_ctx {
     bool own_stream = false;
     SideState side[2];
     DevBuf scan_partials, prep, tkeys, tpays, toffs, gcursor, items, count, biglist;
+    DevBuf thome;   // home slots of the CSR tables (k_csr_home, PHJ_P1_HOME)
+    bool home_ok = false;   // the last build_csr wrote them
     DevBuf np_tab, np_pays;
     DevBuf np_ovf, np_ovfb, np_ovfn;   // region build: overflow tuples, their start buckets, count
     DevBuf np_hot, np_img;             // hot-key cache: sampled keys + count, LDS image (keys, states)
@@ -1222,7 +1226,13 @@ int build_csr(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned* segs)
     const size_t stride = static_cast<size_t>(P) + 1;
     PHJ_TRY(ensure(c, c->prep, stride * 2 * 4));
     PHJ_TRY(ensure(c, c->tkeys, std::max<uint64_t>(1, nR) * 8));
-    const size_t noffs = nR + 2 * static_cast<size_t>(P) + 1;
+    const uint32_t bshift = static_cast<uint32_t>(std::min(3, std::max(0, c->tune.p1_bshift)));
+    const size_t noffs = (nR << bshift) + 2 * static_cast<size_t>(P) + 1;
+    // home slots for the single-device join; over the N gathered segments of
+    // a multi-GPU member the extra build pass sits on the critical R chain
+    // (rehearsal W=8: 0.73 -> 0.77 ms with them), so they are skipped there
+    c->home_ok = c->tune.p1_home && nseg == 1;
+    if (c->home_ok) PHJ_TRY(ensure(c, c->thome, noffs * 16));
     PHJ_TRY(ensure(c, c->toffs, noffs * 4));
     PHJ_TRY(ensure(c, c->gcursor, noffs * 4));
     PHJ_TRY(ensure(c, c->biglist, static_cast<size_t>(P) * 4));
@@ -1230,7 +1240,7 @@ int build_csr(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned* segs)
     PHJ_TRY(ensure(c, c->items, static_cast<size_t>(P) * 16));   // desc[P]
     if (c->dry) return scan_u32(c, nullptr, P + 1, 2, static_cast<uint32_t>(stride));
     uint32_t* prep = static_cast<uint32_t*>(c->prep.p);
-    hipLaunchKernelGGL(k_csr_prep, dim3((P + 1 + kBlock - 1) / kBlock), dim3(kBlock), 0, c->ks, L, prep);
+    hipLaunchKernelGGL(k_csr_prep, dim3((P + 1 + kBlock - 1) / kBlock), dim3(kBlock), 0, c->ks, L, prep, bshift);
     PHJ_LAUNCHED(c, "k_csr_prep");
     PHJ_TRY(scan_u32(c, prep, P + 1, 2, static_cast<uint32_t>(stride)));
     const uint32_t* tkb = prep;
@@ -1251,7 +1261,8 @@ int build_csr(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned* segs)
     ba.bigcount = static_cast<uint32_t*>(c->count.p) + 2;
     PHJ_HIP(c, hipMemsetAsync(ba.bigcount, 0, 4, c->ks));
     const uint64_t expect = (nR + P - 1) / P;
-    const uint32_t kcap = expect * 2 > 8192 ? 256u : std::max<uint32_t>(256, next_pow2_u32(static_cast<uint32_t>(expect * 2)));
+    const uint32_t kcap = expect * 2 > 8192 ? 256u
+                          : std::max<uint32_t>(256, next_pow2_u32(static_cast<uint32_t>(expect * 2)) << bshift);
     ba.ocap = std::min<uint32_t>(2048, std::max<uint32_t>(64, kcap));
     const uint32_t sgrid = (P + kWaves - 1) / kWaves;
     const size_t slds = static_cast<size_t>(ba.ocap) * 4 * kWaves;
@@ -1267,6 +1278,12 @@ int build_csr(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned* segs)
     else
         hipLaunchKernelGGL((k_build_big<kXXH3>), dim3(256), dim3(kBlock), blds, c->ks, ba);
     PHJ_LAUNCHED(c, "k_build_big");
+    if (c->home_ok) {
+        hipLaunchKernelGGL(k_csr_home, dim3((P + kWaves - 1) / kWaves), dim3(kBlock), 0, c->ks,
+                           static_cast<const uint4*>(c->items.p), ba.toffs, ba.tkeys, P,
+                           static_cast<longlong2*>(c->thome.p));
+        PHJ_LAUNCHED(c, "k_csr_home");
+    }
     return PHJ_OK;
 }
 
@@ -1294,6 +1311,7 @@ int probe_p1(phj_ctx* c, const Plan& pl) {
     pa.seed = pl.seed;
     pa.nb2 = pl.nb2;
     pa.ent = PS.p2_ent;
+    pa.home = c->home_ok ? static_cast<const longlong2*>(c->thome.p) : nullptr;
     pa.ebase = PS.p2_ebase;
     const size_t lds = probe_p1_lds_bytes(4096, pl.nb2, 8);
     const int diag = env_int("PHJ_P1_DIAG", 0), wpe = env_int("PHJ_P1_WPE", 6);
@@ -1304,6 +1322,9 @@ int probe_p1(phj_ctx* c, const Plan& pl) {
     else if (env_int("PHJ_P1_GRP", 1) == 0)   // measurement: keys probed ungrouped, from registers
         kfn = pl.hk == kMurmur3 ? reinterpret_cast<const void*>(&k_probe_p1<512, 8, kMurmur3, 0, 4, false, false>)
                                 : reinterpret_cast<const void*>(&k_probe_p1<512, 8, kXXH3, 0, 4, false, false>);
+    else if (pa.home && !pa.ent)   // one home slot per probe
+        kfn = pl.hk == kMurmur3 ? reinterpret_cast<const void*>(&k_probe_p1<512, 8, kMurmur3, 0, 6, false, true, true>)
+                                : reinterpret_cast<const void*>(&k_probe_p1<512, 8, kXXH3, 0, 6, false, true, true>);
     else if (pa.ent)   // tiles from the private chains' chunk lists
         kfn = pl.hk == kMurmur3 ? reinterpret_cast<const void*>(&k_probe_p1<512, 8, kMurmur3, 0, 6, true>)
                                 : reinterpret_cast<const void*>(&k_probe_p1<512, 8, kXXH3, 0, 6, true>);
@@ -1719,6 +1740,8 @@ int ctx_create_device(int device, phj_ctx** out) {
     // partial 64-B segments are written separately (WRREQ 61M vs 52M)
     c->tune.p1_priv = env_int("PHJ_P1_PRIV", 0);
     c->tune.p1_bits = std::max(0, env_int("PHJ_P1_BITS", 0));
+    c->tune.p1_home = env_int("PHJ_P1_HOME", 1);
+    c->tune.p1_bshift = env_int("PHJ_P1_BSHIFT", 0);
     c->tune.p1_ko = env_int("PHJ_P1_KO", 1);
     if (const char* r = std::getenv("PHJ_NP_RATIO")) c->tune.np_ratio = std::max(1.0, std::atof(r));
     c->tune.p1_slots = env_int("PHJ_P1_SLOTS", 0);
@@ -1833,7 +1856,7 @@ void phj_ctx_destroy(phj_ctx* c) {
                           &S.bounds, &S.partials, &S.tseg2, &S.dig, &S.ccur, &S.ctab, &S.tstart, &S.priv})
             free_buf(*b);
     }
-    for (DevBuf* b : {&c->scan_partials, &c->prep, &c->tkeys, &c->tpays, &c->toffs, &c->gcursor, &c->items, &c->biglist,
+    for (DevBuf* b : {&c->thome, &c->scan_partials, &c->prep, &c->tkeys, &c->tpays, &c->toffs, &c->gcursor, &c->items, &c->biglist,
                       &c->count, &c->np_tab, &c->np_pays, &c->np_ovf, &c->np_ovfb, &c->np_ovfn, &c->np_hot, &c->np_img, &c->fitems, &c->split, &c->mat_mark, &c->mat_cnt, &c->mat_rows})
         free_buf(*b);
     for (hipEvent_t e : c->evpool) (void)hipEventDestroy(e);

@@ -1097,11 +1097,12 @@ struct P1ProbeArgs {
     // one chunk (g << 6 | fill - 1) per wave row. nullptr: tiles from a.tile_start
     const uint32_t* ent;
     const uint32_t* ebase;
+    const longlong2* home;    // HOME probe: k_csr_home's slots (indexed like toffs)
 };
 
 // arr: 2 arrays of P+1 entries: m_p and NB_p + 1 (last entries 0), for the
 // CSR tables of k_build_small when no probe work list is needed.
-__global__ __launch_bounds__(kBlock) void k_csr_prep(SegList L, uint32_t* arr) {
+__global__ __launch_bounds__(kBlock) void k_csr_prep(SegList L, uint32_t* arr, uint32_t bshift) {
     const uint32_t P = L.P;
     const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
     if (p > P) return;
@@ -1114,7 +1115,23 @@ __global__ __launch_bounds__(kBlock) void k_csr_prep(SegList L, uint32_t* arr) {
     uint32_t m = 0;
     for (uint32_t g = 0; g < L.nseg; g++) m += L.seg[g].bounds[p + 1] - L.seg[g].bounds[p];
     arr[p] = m;
-    arr[stride + p] = table_buckets(m) + 1;
+    arr[stride + p] = (table_buckets(m) << (m > 1 ? bshift : 0u)) + 1;
+}
+
+// Home slots over a built CSR table (one wave per partition): home[ob + i] =
+// {first key of bucket i, its key count | (offset of its second key) << 32},
+// so a probe reads one 16-B slot and only walks tkeys for a bucket holding
+// more than one key and not matching the first.
+__global__ __launch_bounds__(kBlock) void k_csr_home(const uint4* desc, const uint32_t* toffs, const int64_t* tkeys,
+                                                     uint32_t P, longlong2* home) {
+    const uint32_t p = blockIdx.x * kWaves + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (p >= P) return;
+    const uint4 d = desc[p];   // {kb, ob, nbk, m}
+    for (uint32_t i = lane; i < d.z; i += 64) {
+        const uint32_t o0 = toffs[d.y + i], o1 = toffs[d.y + i + 1];
+        const int64_t k0 = o1 > o0 ? tkeys[d.x + o0] : 0;
+        home[d.y + i] = make_longlong2(k0, static_cast<int64_t>((static_cast<uint64_t>(o0 + 1) << 32) | (o1 - o0)));
+    }
 }
 
 // desc[p] = {kb, ob, nbk, m} from the scanned table bases.
@@ -1139,7 +1156,7 @@ __global__ __launch_bounds__(kBlock) void k_csr_desc(const uint32_t* tkb, const 
 // ~1.2 8-B keys), as in the NoPartitioning probe a lane's four 16-B loads of
 // one bucket cost more than the extra dependent level. DIAG (timing only):
 // 1 = no table reads.
-template <int BLOCK, int ITEMS, int HK, int DIAG = 0, int WPE = 4, bool CHK = false, bool GRP = true>
+template <int BLOCK, int ITEMS, int HK, int DIAG = 0, int WPE = 4, bool CHK = false, bool GRP = true, bool HOME = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void k_probe_p1(P1ProbeArgs pa) {
     constexpr int T = BLOCK * ITEMS;
     constexpr int PB = 4;   // probes in flight per lane per batch
@@ -1319,6 +1336,24 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                         if constexpr (DIAG == 1) ds[i].w = (k2[i] & 1) ? 1u : 0u;
                         else ds[i] = sdesc[static_cast<uint32_t>(q_from_hash(h, a.f) >> a.f.shift) & a.f.dmask];
                     }
+                }
+                if constexpr (HOME) {
+                    // one 16-B home slot per probe: first key, count, rest offset
+                    longlong2 hs[PB];
+#pragma unroll
+                    for (int i = 0; i < PB; i++) {
+                        hs[i] = make_longlong2(0, 0);
+                        if (ds[i].w) hs[i] = pa.home[ds[i].y + (hb[i] & (ds[i].z - 1u))];
+                    }
+#pragma unroll
+                    for (int i = 0; i < PB; i++) {
+                        const uint32_t cntb = static_cast<uint32_t>(hs[i].y);
+                        bool hit = cntb != 0 && hs[i].x == k2[i];
+                        const uint32_t r0 = static_cast<uint32_t>(static_cast<uint64_t>(hs[i].y) >> 32);
+                        for (uint32_t j = 1; j < cntb && !hit; j++) hit = pa.tkeys[ds[i].x + r0 + j - 1] == k2[i];
+                        hits += hit ? 1u : 0u;
+                    }
+                    continue;
                 }
                 uint32_t o0[PB], o1[PB];
 #pragma unroll

@@ -71,7 +71,10 @@ SCHEDULES = [
     {"PHJ_P1_PRIV": "1"},                                       # on-chip probe after workgroup-private chains
     {"PHJ_P1_PRIV": "1", "PHJ_P1_BITS": "5"},                   # ... pass split 5 + rest
     {"PHJ_P1_BITS": "6"},
-    {"PHJ_P1_GRP": "0"},                                        # on-chip probe without the d2 grouping
+    {"PHJ_P1_GRP": "0"},
+    {"PHJ_P1_HOME": "0"},                                       # on-chip probe: CSR offset pair + keys
+    {"PHJ_P1_HOME": "0", "PHJ_P1_BSHIFT": "2"},                 # ... 4x the buckets
+    {"PHJ_P1_BSHIFT": "1"},                                     # home slots over 2x the buckets                                        # on-chip probe without the d2 grouping
     {"PHJ_P1_KO": "0", "PHJ_P1_MIN_TILES": "0"},                # chunked pass 1 writes whole tuples for the probe                                       # shared chains, pass split 6 + rest
     {"PHJ_NP_RATIO": "1.25"},                                   # NoPartitioning default table ratio
     {"PHJ_P1_MIN_TILES": "0", "PHJ_P1_VAR": "0"},               # chunked pass 1: stable ballot ranking
