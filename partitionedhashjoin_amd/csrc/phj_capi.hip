@@ -80,6 +80,7 @@ struct Tuning {
     int p1_home = 1;         // on-chip probe reads one 16-B home slot per key (k_csr_home)
     int p1_bshift = 0;       // CSR tables of the on-chip probe: buckets x 2^bshift
     int p1_ko = 1;           // chunked pass 1 consumed by the counting probe: keys only (k_scatter_chunked VAR 5)
+    int p1_hcode = 1;        // ... written as hash codes; the CSR tables hold codes, the probe never hashes (VAR 13)
     double np_ratio = kNPDefaultRatio;   // NoPartitioning: slots per build tuple when the params leave it 0         // 2-pass join: pass-1 digit bits (0: the plan's split; rebalance_plan)         // pass 1 consumed on chip: workgroup-private chains (k_scatter_priv)
     int p1_var = 3;          // chunked pass 1 variant (k_scatter_chunked VAR: 1 atomic rank, 2 tuple LDS)
 };
@@ -126,6 +127,7 @@ struct SideState {
     const uint32_t* p2_ent = nullptr;     // ... the probe's chunk list and its per-digit offsets
     const uint32_t* p2_ebase = nullptr;
     uint32_t gen = 0;            // chunked pass 1: tag of the current chunk-table entries
+    bool hcoded = false;         // the last pass 1 wrote hash codes (keys only, PHJ_P1_HCODE)
     phj_partitioned view{};
     PassArgs p2{};               // p1_only: the pass-2 tile mapping over the pass-1 output
     uint32_t nt2 = 0;            // ... and its tile bound
@@ -163,6 +165,7 @@ struct phj_ctx {
     DevBuf scan_partials, prep, tkeys, tpays, toffs, gcursor, items, count, biglist;
     DevBuf thome;   // home slots of the CSR tables (k_csr_home, PHJ_P1_HOME)
     bool home_ok = false;   // the last build_csr wrote them
+    bool tables_hcoded = false;   // the last build_csr stored hash codes
     DevBuf np_tab, np_pays;
     DevBuf np_ovf, np_ovfb, np_ovfn;   // region build: overflow tuples, their start buckets, count
     DevBuf np_hot, np_img;             // hot-key cache: sampled keys + count, LDS image (keys, states)
@@ -524,7 +527,7 @@ int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const st
             if (c->tune.p1_slots > 0) slots = std::min<uint32_t>(per, c->tune.p1_slots);
             if (c->tune.p1_slots < 0) slots = per;   // one tile per workgroup
             const void* kfn = nullptr;
-            switch (a.keys_only ? 5 : (c->tune.p1_var & 3)) {
+            switch (a.keys_only ? (c->tune.p1_hcode ? 13 : 5) : (c->tune.p1_var & 3)) {
 #define PHJ_P1_VARIANT(V)                                                                            \
     case V:                                                                                          \
         kfn = hk == kMurmur3 ? reinterpret_cast<const void*>(&k_scatter_chunked<BLOCK, ITEMS, kMurmur3, V>) \
@@ -535,6 +538,7 @@ int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const st
                 PHJ_P1_VARIANT(2)
                 PHJ_P1_VARIANT(3)
                 PHJ_P1_VARIANT(5)
+                PHJ_P1_VARIANT(13)
 #undef PHJ_P1_VARIANT
             }
             PassArgs ak = a;
@@ -740,6 +744,7 @@ int partition_side(phj_ctx* c, int s, const Plan& pl, bool p1_only = false) {
                          tile == tile2 && pl.nb1 <= static_cast<uint32_t>(tile_shape(c, pl.nb1).block) &&
                          tile / tile_shape(c, pl.nb1).block <= 8 &&   // registers: the next tile is prefetched
                          (3 * (static_cast<uint64_t>(n) / tile + kShards) + kShards * pl.nb1) * tile < (1ull << 32);
+    S.hcoded = chunked && ko && c->tune.p1_hcode;   // k_scatter_chunked VAR 13
     // chains per digit: ~kTilesPerShard tiles each, a power of two <= kShards
     uint32_t nshards = 1;
     const uint32_t tps = static_cast<uint32_t>(ko ? c->tune.p1_ko_tps : c->tune.p1_tps);
@@ -1228,10 +1233,10 @@ int build_csr(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned* segs)
     PHJ_TRY(ensure(c, c->tkeys, std::max<uint64_t>(1, nR) * 8));
     const uint32_t bshift = static_cast<uint32_t>(std::min(3, std::max(0, c->tune.p1_bshift)));
     const size_t noffs = (nR << bshift) + 2 * static_cast<size_t>(P) + 1;
-    // home slots for the single-device join; over the N gathered segments of
-    // a multi-GPU member the extra build pass sits on the critical R chain
-    // (rehearsal W=8: 0.73 -> 0.77 ms with them), so they are skipped there
-    c->home_ok = c->tune.p1_home && nseg == 1;
+    // home slots, written by the build kernels as they place the keys (a
+    // separate k_csr_home pass over every table sat on the critical R chain of
+    // a multi-GPU member: rehearsal W=8 0.73 -> 0.77 ms; PHJ_P1_HOME=2 keeps it)
+    c->home_ok = c->tune.p1_home != 0;
     if (c->home_ok) PHJ_TRY(ensure(c, c->thome, noffs * 16));
     PHJ_TRY(ensure(c, c->toffs, noffs * 4));
     PHJ_TRY(ensure(c, c->gcursor, noffs * 4));
@@ -1259,6 +1264,7 @@ int build_csr(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned* segs)
     ba.seed = pl.seed;
     ba.biglist = static_cast<uint32_t*>(c->biglist.p);
     ba.bigcount = static_cast<uint32_t*>(c->count.p) + 2;
+    ba.home = c->home_ok && c->tune.p1_home != 2 ? static_cast<longlong2*>(c->thome.p) : nullptr;
     PHJ_HIP(c, hipMemsetAsync(ba.bigcount, 0, 4, c->ks));
     const uint64_t expect = (nR + P - 1) / P;
     const uint32_t kcap = expect * 2 > 8192 ? 256u
@@ -1266,19 +1272,26 @@ int build_csr(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned* segs)
     ba.ocap = std::min<uint32_t>(2048, std::max<uint32_t>(64, kcap));
     const uint32_t sgrid = (P + kWaves - 1) / kWaves;
     const size_t slds = static_cast<size_t>(ba.ocap) * 4 * kWaves;
+    // the probe side's pass 1 wrote hash codes: the tables hold codes too
+    const bool hout = c->side[PHJ_SIDE_PROBE].hcoded;
     if (pl.hk == kMurmur3)
-        hipLaunchKernelGGL((k_build_small<kMurmur3, kBuildKPL>), dim3(sgrid), dim3(kBlock), slds, c->ks, ba);
+        hipLaunchKernelGGL((hout ? k_build_small<kMurmur3, kBuildKPL, true> : k_build_small<kMurmur3, kBuildKPL, false>),
+                           dim3(sgrid), dim3(kBlock), slds, c->ks, ba);
     else
-        hipLaunchKernelGGL((k_build_small<kXXH3, kBuildKPL>), dim3(sgrid), dim3(kBlock), slds, c->ks, ba);
+        hipLaunchKernelGGL((hout ? k_build_small<kXXH3, kBuildKPL, true> : k_build_small<kXXH3, kBuildKPL, false>),
+                           dim3(sgrid), dim3(kBlock), slds, c->ks, ba);
     PHJ_LAUNCHED(c, "k_build_small");
     ba.ocap = 16384;
     const size_t blds = 64 + static_cast<size_t>(ba.ocap) * 4;
     if (pl.hk == kMurmur3)
-        hipLaunchKernelGGL((k_build_big<kMurmur3>), dim3(256), dim3(kBlock), blds, c->ks, ba);
+        hipLaunchKernelGGL((hout ? k_build_big<kMurmur3, true> : k_build_big<kMurmur3, false>), dim3(256), dim3(kBlock),
+                           blds, c->ks, ba);
     else
-        hipLaunchKernelGGL((k_build_big<kXXH3>), dim3(256), dim3(kBlock), blds, c->ks, ba);
+        hipLaunchKernelGGL((hout ? k_build_big<kXXH3, true> : k_build_big<kXXH3, false>), dim3(256), dim3(kBlock), blds,
+                           c->ks, ba);
     PHJ_LAUNCHED(c, "k_build_big");
-    if (c->home_ok) {
+    c->tables_hcoded = hout;
+    if (c->home_ok && !ba.home) {
         hipLaunchKernelGGL(k_csr_home, dim3((P + kWaves - 1) / kWaves), dim3(kBlock), 0, c->ks,
                            static_cast<const uint4*>(c->items.p), ba.toffs, ba.tkeys, P,
                            static_cast<longlong2*>(c->thome.p));
@@ -1294,6 +1307,20 @@ bool use_p2probe(const phj_ctx* c, const Plan& pl, uint64_t nS) {
     return c->tune.p2probe && pl.npass == 2 && tile_shape(c, pl.nb2).tile == 4096 && tile_shape(c, pl.nb2).block == 512 &&
            pass_tile(c, static_cast<uint32_t>(std::min<uint64_t>(nS, 0xffffffffu)), pl.nb1, &wc) == 4096 && !wc &&
            probe_p1_lds_bytes(4096, pl.nb2, 8) <= 160 * 1024;
+}
+
+template <int HK>
+const void* probe_p1_kernel(int diag, bool grp, bool home, bool ent, int wpe) {
+    if (diag == 1) return reinterpret_cast<const void*>(&k_probe_p1<512, 8, HK, 1>);
+    if (!grp)   // measurement: keys probed ungrouped, from registers
+        return reinterpret_cast<const void*>(&k_probe_p1<512, 8, HK, 0, 4, false, false>);
+    if (home && !ent)   // one home slot per probe
+        return reinterpret_cast<const void*>(&k_probe_p1<512, 8, HK, 0, 6, false, true, true>);
+    if (ent)   // tiles from the private chains' chunk lists
+        return reinterpret_cast<const void*>(&k_probe_p1<512, 8, HK, 0, 6, true>);
+    if (wpe == 4)   // waves per SIMD the compiler budgets registers for (6: 3 workgroups per CU, measured best)
+        return reinterpret_cast<const void*>(&k_probe_p1<512, 8, HK, 0, 4>);
+    return reinterpret_cast<const void*>(&k_probe_p1<512, 8, HK, 0, 6>);
 }
 
 // Probe the partitioned-by-pass-1 probe side (partition_side p1_only) against
@@ -1315,25 +1342,13 @@ int probe_p1(phj_ctx* c, const Plan& pl) {
     pa.ebase = PS.p2_ebase;
     const size_t lds = probe_p1_lds_bytes(4096, pl.nb2, 8);
     const int diag = env_int("PHJ_P1_DIAG", 0), wpe = env_int("PHJ_P1_WPE", 6);
-    const void* kfn;
-    if (diag == 1)
-        kfn = pl.hk == kMurmur3 ? reinterpret_cast<const void*>(&k_probe_p1<512, 8, kMurmur3, 1>)
-                                : reinterpret_cast<const void*>(&k_probe_p1<512, 8, kXXH3, 1>);
-    else if (env_int("PHJ_P1_GRP", 1) == 0)   // measurement: keys probed ungrouped, from registers
-        kfn = pl.hk == kMurmur3 ? reinterpret_cast<const void*>(&k_probe_p1<512, 8, kMurmur3, 0, 4, false, false>)
-                                : reinterpret_cast<const void*>(&k_probe_p1<512, 8, kXXH3, 0, 4, false, false>);
-    else if (pa.home && !pa.ent)   // one home slot per probe
-        kfn = pl.hk == kMurmur3 ? reinterpret_cast<const void*>(&k_probe_p1<512, 8, kMurmur3, 0, 6, false, true, true>)
-                                : reinterpret_cast<const void*>(&k_probe_p1<512, 8, kXXH3, 0, 6, false, true, true>);
-    else if (pa.ent)   // tiles from the private chains' chunk lists
-        kfn = pl.hk == kMurmur3 ? reinterpret_cast<const void*>(&k_probe_p1<512, 8, kMurmur3, 0, 6, true>)
-                                : reinterpret_cast<const void*>(&k_probe_p1<512, 8, kXXH3, 0, 6, true>);
-    else if (wpe == 4)   // waves per SIMD the compiler budgets registers for (6: 3 workgroups per CU, measured best)
-        kfn = pl.hk == kMurmur3 ? reinterpret_cast<const void*>(&k_probe_p1<512, 8, kMurmur3, 0, 4>)
-                                : reinterpret_cast<const void*>(&k_probe_p1<512, 8, kXXH3, 0, 4>);
-    else
-        kfn = pl.hk == kMurmur3 ? reinterpret_cast<const void*>(&k_probe_p1<512, 8, kMurmur3, 0, 6>)
-                                : reinterpret_cast<const void*>(&k_probe_p1<512, 8, kXXH3, 0, 6>);
+    const bool grp = env_int("PHJ_P1_GRP", 1) != 0;
+    // hash codes on both sides (pass 1 VAR 13 + tables built from codes): the
+    // probe's two hashes per key become the identity
+    if (PS.hcoded != c->tables_hcoded) return set_err(c, PHJ_ERR_INVALID, "probe side and tables disagree on hash codes");
+    const void* kfn = PS.hcoded ? probe_p1_kernel<kHashed>(diag, grp, pa.home != nullptr, pa.ent != nullptr, wpe)
+                      : pl.hk == kMurmur3 ? probe_p1_kernel<kMurmur3>(diag, grp, pa.home != nullptr, pa.ent != nullptr, wpe)
+                                          : probe_p1_kernel<kXXH3>(diag, grp, pa.home != nullptr, pa.ent != nullptr, wpe);
     // persistent: as many workgroups as fit the chip at once (a multiple of 8:
     // XCD x owns tiles [x, x + 1) * ntiles / 8), never many more than tiles
     int per_cu = 0;
@@ -1743,6 +1758,7 @@ int ctx_create_device(int device, phj_ctx** out) {
     c->tune.p1_home = env_int("PHJ_P1_HOME", 1);
     c->tune.p1_bshift = env_int("PHJ_P1_BSHIFT", 0);
     c->tune.p1_ko = env_int("PHJ_P1_KO", 1);
+    c->tune.p1_hcode = env_int("PHJ_P1_HCODE", 1);
     if (const char* r = std::getenv("PHJ_NP_RATIO")) c->tune.np_ratio = std::max(1.0, std::atof(r));
     c->tune.p1_slots = env_int("PHJ_P1_SLOTS", 0);
     c->tune.p1_tps = std::max(1, env_int("PHJ_P1_TPS", static_cast<int>(kTilesPerShard)));

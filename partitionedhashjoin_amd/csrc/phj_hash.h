@@ -18,7 +18,17 @@
 
 namespace phj {
 
-enum HashKind : int { kXXH3 = 0, kMurmur3 = 1 };
+// kHashed: the column already holds hash codes h(k) (the keys-only pass 1 of
+// the counting join writes them, the CSR build stores them), so hashing is
+// the identity. Sound because both hashes are bijections of the 64-bit keys:
+// fmix64 is xor-shifts and multiplies by odd constants; XXH3's 8-byte path is
+// a half swap, an xor, x ^ rotl(x,49) ^ rotl(x,24) (the linear map
+// 1 + R^49 + R^24 is a unit of GF(2)[R]/(R^64 + 1): it is 1 at R = 1), odd
+// multiplies, h ^ ((h >> 35) + 8) (bits 30..63 pass through and determine the
+// rest) and an xorshift. So h(r) == h(s) iff r == s, and comparing codes
+// counts exactly the key matches of HashJoin.hpp:295-301. tests/test_oracle.py
+// inverts both on random and extreme keys.
+enum HashKind : int { kXXH3 = 0, kMurmur3 = 1, kHashed = 2 };
 
 PHJ_HD uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
 
@@ -51,6 +61,9 @@ template <int HK>
 PHJ_HD uint64_t hash64(uint64_t key, uint64_t seed) {
     if constexpr (HK == kMurmur3) {
         return murmur3_fmix64(key, seed);
+    } else if constexpr (HK == kHashed) {
+        (void)seed;
+        return key;
     } else {
         return xxh3_8(key, seed);
     }

@@ -135,6 +135,7 @@ struct BuildArgs {
     uint32_t ocap;         // LDS bucket-counter capacity (per wave in k_build_small)
     uint32_t pad;
     uint64_t seed;
+    longlong2* home;       // non-null: the build also writes the home slots (indexed like toffs)
 };
 
 // LDS ordering between lanes of one wave (stores before loads of other lanes).
@@ -153,7 +154,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 // 64 * KPL tuples or a bucket array beyond the wave's LDS slice are appended to
 // biglist for k_build_big. The order inside a bucket is irrelevant to the
 // semi-join count (set membership).
-template <int HK, int KPL>
+template <int HK, int KPL, bool HOUT = false>   // HOUT: store hash codes (phj_hash.h kHashed)
 __global__ __launch_bounds__(kBlock) void k_build_small(BuildArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -179,6 +180,8 @@ __global__ __launch_bounds__(kBlock) void k_build_small(BuildArgs a) {
         uint32_t* offs = a.toffs + ob;
         if (m == 0) {
             for (uint32_t i = lane; i <= nbk; i += 64) offs[i] = 0;
+            if (a.home)
+                for (uint32_t i = lane; i < nbk; i += 64) a.home[ob + i] = make_longlong2(0, 0);
             continue;
         }
         if (nbk > a.ocap || m > 64u * KPL) {
@@ -214,7 +217,9 @@ __global__ __launch_bounds__(kBlock) void k_build_small(BuildArgs a) {
         wave_lds_sync();
 #pragma unroll
         for (int j = 0; j < KPL; j++) {
-            bkt[j] = bucket_of(hash64<HK>(static_cast<uint64_t>(key[j]), a.seed), nbk);
+            const uint64_t h = hash64<HK>(static_cast<uint64_t>(key[j]), a.seed);
+            bkt[j] = bucket_of(h, nbk);
+            if constexpr (HOUT) key[j] = static_cast<int64_t>(h);
             if (j * 64 + lane < m) atomicAdd(&cnt[bkt[j]], 1u);
         }
         wave_lds_sync();
@@ -231,10 +236,20 @@ __global__ __launch_bounds__(kBlock) void k_build_small(BuildArgs a) {
             if (i < nbk) {
                 cnt[i] = carry + x - v;
                 offs[i] = carry + x - v;
+                // home slot, second half: key count | offset of the bucket's second key
+                if (a.home)
+                    reinterpret_cast<int64_t*>(a.home + ob + i)[1] =
+                        static_cast<int64_t>((static_cast<uint64_t>(carry + x - v + 1) << 32) | v);
             }
             carry += __shfl(x, 63, 64);
         }
         if (lane == 0) offs[nbk] = m;
+        wave_lds_sync();
+        // every bucket's start, read before any placement moves it: the tuple
+        // placed there is the bucket's first key (home slot, first half)
+        uint32_t st[KPL];
+#pragma unroll
+        for (int j = 0; j < KPL; j++) st[j] = a.home ? cnt[bkt[j]] : 0xffffffffu;
         wave_lds_sync();
 #pragma unroll
         for (int j = 0; j < KPL; j++) {
@@ -242,6 +257,7 @@ __global__ __launch_bounds__(kBlock) void k_build_small(BuildArgs a) {
                 const uint32_t pos = atomicAdd(&cnt[bkt[j]], 1u);
                 a.tkeys[kb + pos] = key[j];
                 if (spays_all) a.tpays[kb + pos] = pay[j];
+                if (pos == st[j]) reinterpret_cast<int64_t*>(a.home + ob + bkt[j])[0] = key[j];
             }
         }
         wave_lds_sync();
@@ -265,7 +281,7 @@ __device__ __forceinline__ void block_scan_array(uint32_t len, LoadF ld, StoreF 
 
 // One workgroup per partition of biglist (bucket arrays beyond a wave's LDS
 // slice): LDS counters up to ocap buckets, global atomics beyond.
-template <int HK>
+template <int HK, bool HOUT = false>
 __global__ __launch_bounds__(kBlock) void k_build_big(BuildArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint32_t* tmp = reinterpret_cast<uint32_t*>(smem);        // 16 words
@@ -278,9 +294,11 @@ __global__ __launch_bounds__(kBlock) void k_build_big(BuildArgs a) {
         uint32_t* offs = a.toffs + ob;
         if (m == 0) {
             for (uint32_t i = threadIdx.x; i <= nbk; i += kBlock) offs[i] = 0;
+            if (a.home)
+                for (uint32_t i = threadIdx.x; i < nbk; i += kBlock) a.home[ob + i] = make_longlong2(0, 0);
             continue;
         }
-        const bool in_lds = (nbk <= a.ocap);
+        const bool in_lds = (nbk <= a.ocap);   // (m > 0 here)
         uint32_t* cnt = in_lds ? lcnt : (a.gcursor + ob);
         for (uint32_t i = threadIdx.x; i < nbk; i += kBlock) {
             if (in_lds) cnt[i] = 0;
@@ -328,15 +346,24 @@ __global__ __launch_bounds__(kBlock) void k_build_big(BuildArgs a) {
             for (uint32_t i = threadIdx.x; i < c; i += kBlock) {
                 const int64_t key = S.keys[lo + i];
                 const int64_t pay = S.pays ? S.pays[lo + i] : 0;
-                const uint32_t b = bucket_of(hash64<HK>(static_cast<uint64_t>(key), a.seed), nbk);
+                const uint64_t h = hash64<HK>(static_cast<uint64_t>(key), a.seed);
+                const uint32_t b = bucket_of(h, nbk);
                 uint32_t pos;
                 if (in_lds) pos = atomicAdd(&cnt[b], 1u);
                 else pos = __hip_atomic_fetch_add(&cnt[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                a.tkeys[kb + pos] = key;
+                a.tkeys[kb + pos] = HOUT ? static_cast<int64_t>(h) : key;
                 if (S.pays) a.tpays[kb + pos] = pay;
             }
         }
         __syncthreads();
+        if (a.home) {   // home slots from the placed table (written by this workgroup)
+            for (uint32_t i = threadIdx.x; i < nbk; i += kBlock) {
+                const uint32_t o0 = offs[i], o1 = i + 1 < nbk ? offs[i + 1] : m;
+                const int64_t k0 = o1 > o0 ? a.tkeys[kb + o0] : 0;
+                a.home[ob + i] = make_longlong2(k0, static_cast<int64_t>((static_cast<uint64_t>(o0 + 1) << 32) | (o1 - o0)));
+            }
+            __syncthreads();
+        }
     }
 }
 

@@ -562,7 +562,9 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(PassArgs a) {
 // 8-B column accesses). VAR bit 2 (the counting probe consumes the output,
 // HashJoin.hpp:295-301 reads only the key): keys only, loaded, sorted and
 // written (8 B per tuple out instead of 16; half the LDS, three workgroups
-// per CU).
+// per CU). VAR bit 3 (with bit 2): the key is written as its hash code, which
+// the digit needed anyway, so the probe and its tables never hash again
+// (PHJ_P1_HCODE, phj_hash.h kHashed).
 template <int BLOCK, int ITEMS, int HK, int VAR = 0>
 __global__ __launch_bounds__(BLOCK)
 __attribute__((amdgpu_waves_per_eu(((VAR & 4) ? 3 : (BLOCK * ITEMS <= 4096 ? 2 : 1)) * BLOCK / 256)))   // what the LDS lets share a CU
@@ -570,6 +572,7 @@ void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
     constexpr int NW = BLOCK / 64;
     constexpr int T = BLOCK * ITEMS;
     constexpr bool ARANK = (VAR & 1) != 0, KO = (VAR & 4) != 0, LAOS = (VAR & 2) != 0 && !KO;
+    constexpr bool HC = KO && (VAR & 8) != 0;   // keys only, written as hash codes
     // atomic ranking + one 16-B access per element: a digit's three write
     // offsets packed in one 16-B LDS entry (one ds_read_b128 per element in
     // the write loop), placed in the counter rows the atomic ranking leaves unused
@@ -639,7 +642,15 @@ void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
         for (int i = 0; i < ITEMS; i++) {
             const uint32_t e = wbase + i * 64 + lane;
             const bool valid = e < cnt;
-            const uint32_t d = valid ? digit_of<HK>(static_cast<uint64_t>(key[i]), a.f) : 0u;
+            uint32_t d;
+            if constexpr (HC) {
+                // the key's hash code goes out in its place (phj_hash.h: kHashed)
+                const uint64_t h = hash64<HK>(static_cast<uint64_t>(key[i]), a.f.seed);
+                d = valid ? static_cast<uint32_t>(q_from_hash(h, a.f) >> a.f.shift) & a.f.dmask : 0u;
+                key[i] = static_cast<int64_t>(h);
+            } else {
+                d = valid ? digit_of<HK>(static_cast<uint64_t>(key[i]), a.f) : 0u;
+            }
             dig[i] = d;
             rank[i] = 0;
             if constexpr (ARANK) {

@@ -73,6 +73,10 @@ SCHEDULES = [
     {"PHJ_P1_BITS": "6"},
     {"PHJ_P1_GRP": "0"},
     {"PHJ_P1_HOME": "0"},                                       # on-chip probe: CSR offset pair + keys
+    {"PHJ_P1_HOME": "2"},                                       # home slots from a separate pass (k_csr_home)
+    {"PHJ_P1_HCODE": "0"},                                      # keys-only pass 1 writes raw keys (the probe hashes)
+    {"PHJ_P1_HCODE": "0", "PHJ_P1_HOME": "0"},                  # ... with the CSR offset-pair probe
+    {"PHJ_P1_GRP": "0"},                                        # ungrouped probe over hash codes
     {"PHJ_P1_HOME": "0", "PHJ_P1_BSHIFT": "2"},                 # ... 4x the buckets
     {"PHJ_P1_BSHIFT": "1"},                                     # home slots over 2x the buckets                                        # on-chip probe without the d2 grouping
     {"PHJ_P1_KO": "0", "PHJ_P1_MIN_TILES": "0"},                # chunked pass 1 writes whole tuples for the probe                                       # shared chains, pass split 6 + rest
