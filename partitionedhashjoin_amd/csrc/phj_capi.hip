@@ -157,6 +157,11 @@ struct phj_ctx {
     int device = 0;
     hipStream_t stream = nullptr;  // the ctx stream (own or borrowed)
     hipStream_t aux = nullptr;     // ctx-owned: R-side partitioning runs here beside S
+    // PHJ_CU_SPLIT=k: CU-masked streams for the single-device on-chip join, k
+    // CUs of every 32 for R's chain (partition + tables), the rest for S's
+    // pass 1, so R is not starved behind S's persistent workgroups
+    hipStream_t r_split = nullptr, s_split = nullptr;
+    int s_split_cus = 0;
     hipStream_t ks = nullptr;      // stream the current launches go to (stream or aux)
     DevBuf* scan_scratch = nullptr; // scan partials of the side being partitioned
     int num_cus = 256;
@@ -220,6 +225,8 @@ int ensure(phj_ctx* c, DevBuf& b, size_t bytes) {
     if (b.p) {
         PHJ_HIP(c, hipStreamSynchronize(c->stream));
         PHJ_HIP(c, hipStreamSynchronize(c->aux));
+        if (c->r_split) PHJ_HIP(c, hipStreamSynchronize(c->r_split));
+        if (c->s_split) PHJ_HIP(c, hipStreamSynchronize(c->s_split));
         PHJ_HIP(c, hipFree(b.p));
         b.p = nullptr;
         b.bytes = 0;
@@ -1773,6 +1780,23 @@ int ctx_create_device(int device, phj_ctx** out) {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
     }
+    {
+        const int k = env_int("PHJ_CU_SPLIT", 0);
+        if (k > 0 && k < 32 && c->num_cus % 32 == 0) {
+            std::vector<uint32_t> rm(static_cast<size_t>(c->num_cus) / 32, 0), sm(rm.size(), 0);
+            for (size_t w = 0; w < rm.size(); w++) {
+                rm[w] = (1u << k) - 1u;
+                sm[w] = ~rm[w];
+            }
+            if (hipExtStreamCreateWithCUMask(&c->r_split, static_cast<uint32_t>(rm.size()), rm.data()) != hipSuccess ||
+                hipExtStreamCreateWithCUMask(&c->s_split, static_cast<uint32_t>(sm.size()), sm.data()) != hipSuccess) {
+                if (c->r_split) (void)hipStreamDestroy(c->r_split);
+                c->r_split = c->s_split = nullptr;
+            } else {
+                c->s_split_cus = c->num_cus - k * (c->num_cus / 32);
+            }
+        }
+    }
     c->tune.wc_items = env_int("PHJ_WC_ITEMS", 8) == 4 ? 4 : 8;
     c->tune.wc_lw = env_int("PHJ_WC_LW", 8) == 16 ? 16 : 8;
     c->tune.wc_wgs = std::max(64, env_int("PHJ_WC_WGS", 1024));
@@ -1867,6 +1891,8 @@ void phj_ctx_destroy(phj_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     (void)hipStreamSynchronize(c->aux);
+    if (c->r_split) (void)hipStreamSynchronize(c->r_split);
+    if (c->s_split) (void)hipStreamSynchronize(c->s_split);
     for (SideState& S : c->side) {
         for (DevBuf* b : {&S.owned, &S.kA, &S.pA, &S.kB, &S.pB, &S.hist1, &S.hist2, &S.bounds1, &S.tbase2,
                           &S.bounds, &S.partials, &S.tseg2, &S.dig, &S.ccur, &S.ctab, &S.tstart, &S.priv})
@@ -1878,6 +1904,8 @@ void phj_ctx_destroy(phj_ctx* c) {
     for (hipEvent_t e : c->evpool) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->stream);
     (void)hipStreamDestroy(c->aux);
+    if (c->r_split) (void)hipStreamDestroy(c->r_split);
+    if (c->s_split) (void)hipStreamDestroy(c->s_split);
     delete c;
 }
 
@@ -1889,6 +1917,8 @@ int phj_ctx_set_stream(phj_ctx* c, void* stream) {
     PHJ_HIP(c, hipSetDevice(c->device));
     PHJ_HIP(c, hipStreamSynchronize(c->stream));
     PHJ_HIP(c, hipStreamSynchronize(c->aux));
+    if (c->r_split) PHJ_HIP(c, hipStreamSynchronize(c->r_split));
+    if (c->s_split) PHJ_HIP(c, hipStreamSynchronize(c->s_split));
     if (c->own_stream) {
         PHJ_HIP(c, hipStreamDestroy(c->stream));
         c->own_stream = false;
@@ -1913,6 +1943,8 @@ int phj_ctx_synchronize(phj_ctx* c) {
         return PHJ_OK;
     }
     PHJ_HIP(c, hipStreamSynchronize(c->aux));
+    if (c->r_split) PHJ_HIP(c, hipStreamSynchronize(c->r_split));
+    if (c->s_split) PHJ_HIP(c, hipStreamSynchronize(c->s_split));
     PHJ_HIP(c, hipStreamSynchronize(c->stream));
     return PHJ_OK;
 }
@@ -2143,10 +2175,26 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
         // S: pass 1 only (its pass 2 runs inside the probe); R: both passes and
         // its bucket tables on the aux stream, beside S
         PHJ_TRY(mark(c, &t0));
-        PHJ_HIP(c, hipStreamWaitEvent(c->aux, t0, 0));
-        PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, pl, true));
-        c->ks = c->aux;
-        int rc = partition_side(c, PHJ_SIDE_BUILD, pl);
+        const bool split = c->r_split != nullptr;
+        hipStream_t rs = split ? c->r_split : c->aux;
+        PHJ_HIP(c, hipStreamWaitEvent(rs, t0, 0));
+        hipEvent_t sd = nullptr;
+        int rc = PHJ_OK;
+        if (split) {   // S's pass 1 on its CU share (persistent grid sized to it)
+            PHJ_HIP(c, hipStreamWaitEvent(c->s_split, t0, 0));
+            c->ks = c->s_split;
+            const int cus = c->num_cus;
+            c->num_cus = c->s_split_cus;
+            rc = partition_side(c, PHJ_SIDE_PROBE, pl, true);
+            c->num_cus = cus;
+            if (rc == PHJ_OK) rc = mark(c, &sd);
+            c->ks = c->stream;
+            PHJ_TRY(rc);
+        } else {
+            PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, pl, true));
+        }
+        c->ks = rs;
+        rc = partition_side(c, PHJ_SIDE_BUILD, pl);
         if (rc == PHJ_OK) rc = mark(c, &b0);
         if (rc == PHJ_OK) rc = timer_begin(c, "build", R.n * 8 * 2);
         if (rc == PHJ_OK) rc = build_csr(c, pl, 1, &R.view);
@@ -2154,6 +2202,7 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
         if (rc == PHJ_OK) rc = mark(c, &tr);
         c->ks = c->stream;
         PHJ_TRY(rc);
+        if (sd) PHJ_HIP(c, hipStreamWaitEvent(c->stream, sd, 0));
         PHJ_HIP(c, hipStreamWaitEvent(c->stream, tr, 0));
         PHJ_TRY(mark(c, &t1));
         // algorithmic bytes: the pass-1 output read once (16-B tuples, or 8-B
