@@ -62,6 +62,7 @@ struct Tuning {
     int fused_kpl = 4;    // fused join: S keys per lane per probe round (2, 4 or 8)
     bool p1_chunk = true; // 2-pass, unordered partitions: chunked pass 1 without a histogram pass
     int p1_slots = 0;     // chunked pass 1: workgroups per shard (0 = fill the chip once, -1 = one per tile)
+    int p1_wpc2 = 3;      // ... keys-only: workgroups per CU x 2 (0 = fill the chip once)
     int p1_tps = static_cast<int>(kTilesPerShard);   // chunked pass 1: tiles per shard (sets the shard count)
     int p1_min_tiles = 32768;  // chunked pass 1: smallest relation (in 4096-tuple tiles, ~134M tuples)
     int p1_ko_tps = 1024;      // ... the keys-only form for the counting probe: tiles per shard
@@ -531,6 +532,13 @@ int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const st
             const size_t lds = a.keys_only ? sc_lds - static_cast<size_t>(T) * 8 : sc_lds;   // no payload rows
             const uint32_t fit = std::max<uint32_t>(1, static_cast<uint32_t>(160 * 1024 / lds));
             uint32_t slots = std::max<uint32_t>(1, std::min<uint32_t>(per, fit * c->num_cus / a.nshards));
+            // keys-only (the on-chip join): PHJ_P1_WPC2 half-workgroups per CU, not
+            // every slot the LDS allows, so R's partition and tables on the aux
+            // stream get CUs beside S's persistent pass 1 instead of queueing behind it
+            if (a.keys_only && c->tune.p1_wpc2 > 0)
+                slots = std::max<uint32_t>(
+                    1, std::min<uint32_t>(per, std::min<uint32_t>(fit * 2, static_cast<uint32_t>(c->tune.p1_wpc2)) *
+                                                   c->num_cus / (2 * a.nshards)));
             if (c->tune.p1_slots > 0) slots = std::min<uint32_t>(per, c->tune.p1_slots);
             if (c->tune.p1_slots < 0) slots = per;   // one tile per workgroup
             const void* kfn = nullptr;
@@ -1768,6 +1776,7 @@ int ctx_create_device(int device, phj_ctx** out) {
     c->tune.p1_hcode = env_int("PHJ_P1_HCODE", 1);
     if (const char* r = std::getenv("PHJ_NP_RATIO")) c->tune.np_ratio = std::max(1.0, std::atof(r));
     c->tune.p1_slots = env_int("PHJ_P1_SLOTS", 0);
+    c->tune.p1_wpc2 = std::max(0, env_int("PHJ_P1_WPC2", 3));
     c->tune.p1_tps = std::max(1, env_int("PHJ_P1_TPS", static_cast<int>(kTilesPerShard)));
     c->tune.p1_min_tiles = std::max(0, env_int("PHJ_P1_MIN_TILES", 32768));
     c->tune.p1_ko_tps = std::max(1, env_int("PHJ_P1_KO_TPS", 1024));

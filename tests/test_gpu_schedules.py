@@ -73,6 +73,8 @@ SCHEDULES = [
     {"PHJ_P1_BITS": "6"},
     {"PHJ_P1_GRP": "0"},
     {"PHJ_P1_HOME": "0"},                                       # on-chip probe: CSR offset pair + keys
+    {"PHJ_P1_WPC2": "0"},                                       # keys-only pass 1 on every LDS slot (3 per CU)
+    {"PHJ_P1_WPC2": "1"},                                       # ... on half a workgroup per CU
     {"PHJ_CU_SPLIT": "4"},                                      # R chain and S pass 1 on CU-masked streams
     {"PHJ_P1_HOME": "2"},                                       # home slots from a separate pass (k_csr_home)
     {"PHJ_P1_HCODE": "0"},                                      # keys-only pass 1 writes raw keys (the probe hashes)
