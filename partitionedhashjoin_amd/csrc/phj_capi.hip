@@ -1329,8 +1329,11 @@ const void* probe_p1_kernel(int diag, bool grp, bool home, bool ent, int wpe) {
     if (diag == 1) return reinterpret_cast<const void*>(&k_probe_p1<512, 8, HK, 1>);
     if (!grp)   // measurement: keys probed ungrouped, from registers
         return reinterpret_cast<const void*>(&k_probe_p1<512, 8, HK, 0, 4, false, false>);
-    if (home && !ent)   // one home slot per probe
+    if (home && !ent) {   // one home slot per probe
+        if constexpr (HK == kHashed)   // no hashing left: registers for 8 waves per SIMD (PHJ_P1_WPE=8)
+            if (wpe == 8) return reinterpret_cast<const void*>(&k_probe_p1<512, 8, HK, 0, 8, false, true, true>);
         return reinterpret_cast<const void*>(&k_probe_p1<512, 8, HK, 0, 6, false, true, true>);
+    }
     if (ent)   // tiles from the private chains' chunk lists
         return reinterpret_cast<const void*>(&k_probe_p1<512, 8, HK, 0, 6, true>);
     if (wpe == 4)   // waves per SIMD the compiler budgets registers for (6: 3 workgroups per CU, measured best)
