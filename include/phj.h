@@ -253,6 +253,20 @@ int phj_partitioned_download(phj_ctx *ctx, const phj_partitioned *v, int64_t *ke
 int phj_hash_keys(phj_ctx *ctx, int hash, uint64_t seed, const int64_t *keys, uint64_t n,
                   uint64_t *out);
 
+/* ---- test hook: the probe side's pass 1 of the counting join ----
+ * Replaces nothing in the reference: it exposes the intermediate that
+ * phj_join's on-chip probe consumes instead of the reference's partitioned
+ * probe table (src/RadixCluster/HashJoin.hpp:394-412, first of two passes),
+ * so tests can compare it with the oracle at full size. Runs the probe side's
+ * pass 1 for params (single-device ctx, radix join taking the on-chip path)
+ * and copies its output, concatenated in pass-2 tile order (pass-1 digit
+ * major, unordered inside a digit), to keys[0, n) (n = |S|), and the digit
+ * bounds to bounds1[0, nb1 + 1). *nb1 = pass-1 digits; *codes = 1 when the
+ * output holds hash codes h(key) (the keys-only pass), 0 for keys. bounds1
+ * must hold at least 2049 entries. */
+int phj_probe_pass1(phj_ctx *ctx, const phj_join_params *p, int64_t *keys, uint64_t n, uint32_t *bounds1,
+                    uint32_t *nb1, int *codes);
+
 #ifdef __cplusplus
 }
 #endif

@@ -58,6 +58,7 @@ def lib():
             "or_murmur3": (_u64, [_i64, _u64]),
             "or_hash": (_u64, [_i, _i64, _u64]),
             "or_hash_mod": (_u64, [_i, _i64, _u64, _u64]),
+            "or_hash_many": (None, [_i, _P, _u64, _u64, _P]),
             "or_lcg_step": (_i64, [_i64]),
             "or_lcg_next": (_d, [C.POINTER(_i64)]),
             "or_zipf_generate": (_u64, [_d, _u64, C.POINTER(_i64)]),
@@ -137,8 +138,10 @@ def murmur3(key: int, seed: int) -> int:
 
 
 def hash_keys(kind: int, keys, seed: int) -> np.ndarray:
-    L = lib()
-    return np.array([L.or_hash(kind, int(k), seed) for k in keys], dtype=np.uint64)
+    keys = np.ascontiguousarray(np.asarray(keys, dtype=np.int64))
+    out = np.zeros(keys.shape[0], dtype=np.uint64)
+    lib().or_hash_many(kind, _ptr(keys), keys.shape[0], seed, _ptr(out))
+    return out
 
 
 # ---- generators ----

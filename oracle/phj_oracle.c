@@ -130,6 +130,11 @@ uint64_t or_hash(int kind, int64_t key, uint64_t seed) {
     return kind == OR_HASH_MURMUR3 ? or_murmur3(key, seed) : or_xxh3_64(key, seed);
 }
 
+/* or_hash over an array (test infrastructure: full-size code checks). */
+void or_hash_many(int kind, const int64_t* keys, uint64_t n, uint64_t seed, uint64_t* out) {
+    for (uint64_t i = 0; i < n; i++) out[i] = or_hash(kind, keys[i], seed);
+}
+
 /* XXHasher::Hash(key, cardinality) = hash % cardinality (XXHasher.hpp:19-22). */
 uint64_t or_hash_mod(int kind, int64_t key, uint64_t seed, uint64_t card) {
     return or_hash(kind, key, seed) % card;

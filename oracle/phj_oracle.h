@@ -42,6 +42,7 @@ enum { OR_HASH_XXH3 = 0, OR_HASH_MURMUR3 = 1 };
 uint64_t or_xxh3_64(int64_t key, uint64_t seed);
 uint64_t or_murmur3(int64_t key, uint64_t seed);
 uint64_t or_hash(int kind, int64_t key, uint64_t seed);
+void or_hash_many(int kind, const int64_t* keys, uint64_t n, uint64_t seed, uint64_t* out);
 /* hash(key) % cardinality, exactly XXHasher::Hash */
 uint64_t or_hash_mod(int kind, int64_t key, uint64_t seed, uint64_t card);
 

@@ -240,6 +240,18 @@ class Context:
             bounds.ctypes.data_as(C.c_void_p)))
         return keys, pays, bounds
 
+    def probe_pass1(self, params: JoinParams):
+        """Test hook (phj_probe_pass1): the probe side's pass-1 output as the
+        counting join's on-chip probe consumes it, pass-1 digit major.
+        Returns (keys or hash codes, bounds1 (nb1 + 1), is_codes)."""
+        n = self.relation_ptr(SIDE_PROBE)[1]
+        out = np.zeros(n, dtype=np.int64)
+        b1 = np.zeros(2049, dtype=np.uint32)
+        nb1, codes = C.c_uint32(), C.c_int()
+        self._check(self._L.phj_probe_pass1(self._h, C.byref(params), out.ctypes.data_as(C.c_void_p), n,
+                                            b1.ctypes.data_as(C.c_void_p), C.byref(nb1), C.byref(codes)))
+        return out, b1[:nb1.value + 1].copy(), bool(codes.value)
+
     def hash_keys(self, kind: int, seed: int, keys) -> np.ndarray:
         keys = np.ascontiguousarray(np.asarray(keys, dtype=np.int64))
         out = np.zeros(keys.shape[0], dtype=np.uint64)

@@ -23,6 +23,7 @@
 #include "phj_mat.h"
 #include "phj_partition.h"
 #include "phj_partition_wc.h"
+#include "phj_table.h"
 
 using namespace phj;
 
@@ -169,9 +170,8 @@ struct phj_ctx {
     bool own_stream = false;
     SideState side[2];
     DevBuf scan_partials, prep, tkeys, tpays, toffs, gcursor, items, count, biglist;
-    DevBuf thome;   // home slots of the CSR tables (k_csr_home, PHJ_P1_HOME)
-    bool home_ok = false;   // the last build_csr wrote them
-    bool tables_hcoded = false;   // the last build_csr stored hash codes
+    DevBuf ht_tab, ht_desc;   // on-chip join: code tables, descriptors (build_ht)
+    DevBuf r_codes, r_bounds;         // ... the build side's codes in partition order and bounds (single device)
     DevBuf np_tab, np_pays;
     DevBuf np_ovf, np_ovfb, np_ovfn;   // region build: overflow tuples, their start buckets, count
     DevBuf np_hot, np_img;             // hot-key cache: sampled keys + count, LDS image (keys, states)
@@ -1225,148 +1225,171 @@ int build_and_probe(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned*
     return PHJ_OK;
 }
 
-// CSR bucket tables (k_build_small / k_build_big) over `nseg` partitioned
-// build segments, keys only, plus the per-partition descriptors of k_probe_p1.
-int build_csr(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned* segs) {
+// ---- the counting join's on-chip path (phj_table.h) ----
+
+// The build side of the on-chip join on this device's relation: pass 1 as
+// hash codes, contiguous per pass-1 digit (k_hist + scan + k_scatter_codes,
+// 512 x 4096 tiles), then pass 2 into final partition order (k_ht_hist + scan
+// + k_ht_scatter). `out` receives |R| codes, `bounds` the P + 1 partition
+// bounds: one build segment of build_ht (they may point into an exchange block).
+int partition_build(phj_ctx* c, const Plan& pl, int64_t* out, uint32_t* bounds) {
+    SideState& S = c->side[PHJ_SIDE_BUILD];
+    c->scan_scratch = &S.partials;
+    if (!S.rel && S.n > 0) return set_err(c, PHJ_ERR_STATE, "relation not bound");
+    if (S.n >= (1ull << 32) - 2 * 4096) return set_err(c, PHJ_ERR_RANGE, "relation above 2^32 tuples per device");
+    constexpr int BLOCK = 512, ITEMS = 8, T = BLOCK * ITEMS;
+    const uint32_t n = static_cast<uint32_t>(S.n), nb = pl.nb1, P = pl.Ppad;
+    const uint32_t nt = (n + T - 1) / T, hlen = nt * nb;
+    const uint32_t h2len = P * kHtTpd + 1;
+    PHJ_TRY(ensure(c, S.hist1, std::max<size_t>(1, hlen) * 4));
+    PHJ_TRY(ensure(c, S.bounds1, (static_cast<size_t>(nb) + 1) * 4));
+    PHJ_TRY(ensure(c, S.kA, std::max<size_t>(1, n) * 8));
+    PHJ_TRY(ensure(c, S.hist2, static_cast<size_t>(h2len) * 4));
+    if (c->dry) {
+        if (hlen) PHJ_TRY(scan_u32(c, nullptr, hlen, 1, hlen, c->scan_scratch));
+        return scan_u32(c, nullptr, h2len, 1, h2len, c->scan_scratch);
+    }
+    if (n == 0) {
+        PHJ_HIP(c, hipMemsetAsync(bounds, 0, (static_cast<size_t>(P) + 1) * 4, c->ks));
+        c->since_ev++;
+        return PHJ_OK;
+    }
+    PassArgs a{};
+    a.in_keys = reinterpret_cast<const int64_t*>(S.rel);
+    a.out_keys = static_cast<int64_t*>(S.kA.p);
+    a.hist = static_cast<uint32_t*>(S.hist1.p);
+    a.nseg = 1;
+    a.n = n;
+    a.ntiles1 = nt;
+    a.nbins = nb;
+    a.nbits = pl.bits1;
+    a.f = digit_fn(pl, 1);
+    a.xcd_remap = c->tune.xcd_remap ? 1u : 0u;
+    const uint32_t grid = a.xcd_remap ? (nt + 7) & ~7u : nt;
+    const size_t hlds = static_cast<size_t>(BLOCK / 64) * nb * 4;
+    auto* b1 = static_cast<uint32_t*>(S.bounds1.p);
+    PHJ_TRY(timer_begin(c, "R.p1.hist", static_cast<uint64_t>(n) * 16));
+    if (pl.hk == kMurmur3) hipLaunchKernelGGL((k_hist<BLOCK, ITEMS, true, kMurmur3>), dim3(grid), dim3(BLOCK), hlds, c->ks, a);
+    else hipLaunchKernelGGL((k_hist<BLOCK, ITEMS, true, kXXH3>), dim3(grid), dim3(BLOCK), hlds, c->ks, a);
+    PHJ_LAUNCHED(c, "k_hist");
+    PHJ_TRY(timer_end(c));
+    PHJ_TRY(timer_begin(c, "R.p1.scan", static_cast<uint64_t>(hlen) * 12));
+    PHJ_TRY(scan_u32(c, a.hist, hlen, 1, hlen, c->scan_scratch));
+    hipLaunchKernelGGL(k_pass1_finish, dim3(1), dim3(1024), 0, c->ks, a.hist, nt, nb, n, static_cast<uint32_t>(T), b1,
+                       static_cast<uint32_t*>(nullptr));
+    PHJ_LAUNCHED(c, "k_pass1_finish");
+    PHJ_TRY(timer_end(c));
+    // algorithmic bytes: the 16-B tuple read, the 8-B code written
+    PHJ_TRY(timer_begin(c, "R.p1.scatter", static_cast<uint64_t>(n) * 24));
+    const size_t slds = scatter_codes_lds_bytes(T, nb);
+    if (pl.hk == kMurmur3)
+        hipLaunchKernelGGL((k_scatter_codes<BLOCK, ITEMS, kMurmur3>), dim3(grid), dim3(BLOCK), slds, c->ks, a);
+    else
+        hipLaunchKernelGGL((k_scatter_codes<BLOCK, ITEMS, kXXH3>), dim3(grid), dim3(BLOCK), slds, c->ks, a);
+    PHJ_LAUNCHED(c, "k_scatter_codes");
+    PHJ_TRY(timer_end(c));
+    HtPass2Args b{};
+    b.codes = static_cast<const int64_t*>(S.kA.p);
+    b.b1 = b1;
+    b.hist = static_cast<uint32_t*>(S.hist2.p);
+    b.out = out;
+    b.bounds = bounds;
+    b.nb1 = nb;
+    b.nb2 = pl.nb2;
+    b.f2 = digit_fn(pl, 2);
+    const size_t lds2 = static_cast<size_t>(pl.nb2) * 4;
+    PHJ_TRY(timer_begin(c, "R.p2.hist", static_cast<uint64_t>(n) * 8));
+    hipLaunchKernelGGL(k_ht_hist, dim3(nb * kHtTpd), dim3(256), lds2, c->ks, b);
+    PHJ_LAUNCHED(c, "k_ht_hist");
+    PHJ_TRY(timer_end(c));
+    PHJ_TRY(timer_begin(c, "R.p2.scan", static_cast<uint64_t>(h2len) * 12));
+    PHJ_TRY(scan_u32(c, b.hist, h2len, 1, h2len, c->scan_scratch));
+    PHJ_TRY(timer_end(c));
+    PHJ_TRY(timer_begin(c, "R.p2.scatter", static_cast<uint64_t>(n) * 16));
+    hipLaunchKernelGGL(k_ht_scatter, dim3(nb * kHtTpd), dim3(256), lds2, c->ks, b);
+    PHJ_LAUNCHED(c, "k_ht_scatter");
+    return timer_end(c);
+}
+
+// Code tables of every final partition over `nseg` build segments (codes in
+// partition order + P + 1 bounds each, e.g. the all-gathered shards), plus
+// the descriptors k_probe_ht stages. nR = the codes of all segments.
+int build_ht(phj_ctx* c, const Plan& pl, int nseg, const int64_t* const* codes, const uint32_t* const* bounds,
+             uint64_t nR) {
+    if (nseg < 1 || nseg > kHtSegs) return set_err(c, PHJ_ERR_INVALID, "build segments must be in [1,16]");
     const uint32_t P = pl.Ppad;
-    SegList L{};
-    L.nseg = static_cast<uint32_t>(nseg);
-    L.P = P;
-    uint64_t nR = 0;
-    for (int g = 0; g < nseg; g++) {
-        if (segs[g].num_partitions != P) return set_err(c, PHJ_ERR_INVALID, "build segment partition count mismatch");
-        if (!c->dry && (!segs[g].bounds || (segs[g].n && !segs[g].keys)))
-            return set_err(c, PHJ_ERR_INVALID, "null build segment");
-        L.seg[g].keys = segs[g].keys;
-        L.seg[g].pays = nullptr;   // the count join tests keys only
-        L.seg[g].bounds = segs[g].bounds;
-        nR += segs[g].n;
-    }
-    if (nR >= (1ull << 32) - 1) return set_err(c, PHJ_ERR_RANGE, "build side above 2^32 tuples");
-    const size_t stride = static_cast<size_t>(P) + 1;
-    PHJ_TRY(ensure(c, c->prep, stride * 2 * 4));
-    PHJ_TRY(ensure(c, c->tkeys, std::max<uint64_t>(1, nR) * 8));
-    const uint32_t bshift = static_cast<uint32_t>(std::min(3, std::max(0, c->tune.p1_bshift)));
-    const size_t noffs = (nR << bshift) + 2 * static_cast<size_t>(P) + 1;
-    // home slots, written by the build kernels as they place the keys (a
-    // separate k_csr_home pass over every table sat on the critical R chain of
-    // a multi-GPU member: rehearsal W=8 0.73 -> 0.77 ms; PHJ_P1_HOME=2 keeps it)
-    c->home_ok = c->tune.p1_home != 0;
-    if (c->home_ok) PHJ_TRY(ensure(c, c->thome, noffs * 16));
-    PHJ_TRY(ensure(c, c->toffs, noffs * 4));
-    PHJ_TRY(ensure(c, c->gcursor, noffs * 4));
-    PHJ_TRY(ensure(c, c->biglist, static_cast<size_t>(P) * 4));
+    const uint64_t slots = 4 * nR + 2ull * P;
+    if (slots >= (1ull << 32)) return set_err(c, PHJ_ERR_RANGE, "build side too large for 32-bit table slots");
+    PHJ_TRY(ensure(c, c->ht_tab, slots * 8));
+    PHJ_TRY(ensure(c, c->ht_desc, static_cast<size_t>(P) * 8));
     PHJ_TRY(ensure(c, c->count, 16));
-    PHJ_TRY(ensure(c, c->items, static_cast<size_t>(P) * 16));   // desc[P]
-    if (c->dry) return scan_u32(c, nullptr, P + 1, 2, static_cast<uint32_t>(stride));
-    uint32_t* prep = static_cast<uint32_t*>(c->prep.p);
-    hipLaunchKernelGGL(k_csr_prep, dim3((P + 1 + kBlock - 1) / kBlock), dim3(kBlock), 0, c->ks, L, prep, bshift);
-    PHJ_LAUNCHED(c, "k_csr_prep");
-    PHJ_TRY(scan_u32(c, prep, P + 1, 2, static_cast<uint32_t>(stride)));
-    const uint32_t* tkb = prep;
-    const uint32_t* tob = prep + stride;
-    hipLaunchKernelGGL(k_csr_desc, dim3((P + kBlock - 1) / kBlock), dim3(kBlock), 0, c->ks, tkb, tob, P,
-                       static_cast<uint4*>(c->items.p));
-    PHJ_LAUNCHED(c, "k_csr_desc");
-    BuildArgs ba{};
-    ba.L = L;
-    ba.tkb = tkb;
-    ba.tob = tob;
-    ba.tkeys = static_cast<int64_t*>(c->tkeys.p);
-    ba.tpays = nullptr;
-    ba.toffs = static_cast<uint32_t*>(c->toffs.p);
-    ba.gcursor = static_cast<uint32_t*>(c->gcursor.p);
-    ba.seed = pl.seed;
-    ba.biglist = static_cast<uint32_t*>(c->biglist.p);
-    ba.bigcount = static_cast<uint32_t*>(c->count.p) + 2;
-    ba.home = c->home_ok && c->tune.p1_home != 2 ? static_cast<longlong2*>(c->thome.p) : nullptr;
-    PHJ_HIP(c, hipMemsetAsync(ba.bigcount, 0, 4, c->ks));
-    const uint64_t expect = (nR + P - 1) / P;
-    const uint32_t kcap = expect * 2 > 8192 ? 256u
-                          : std::max<uint32_t>(256, next_pow2_u32(static_cast<uint32_t>(expect * 2)) << bshift);
-    ba.ocap = std::min<uint32_t>(2048, std::max<uint32_t>(64, kcap));
-    const uint32_t sgrid = (P + kWaves - 1) / kWaves;
-    const size_t slds = static_cast<size_t>(ba.ocap) * 4 * kWaves;
-    // the probe side's pass 1 wrote hash codes: the tables hold codes too
-    const bool hout = c->side[PHJ_SIDE_PROBE].hcoded;
-    if (pl.hk == kMurmur3)
-        hipLaunchKernelGGL((hout ? k_build_small<kMurmur3, kBuildKPL, true> : k_build_small<kMurmur3, kBuildKPL, false>),
-                           dim3(sgrid), dim3(kBlock), slds, c->ks, ba);
-    else
-        hipLaunchKernelGGL((hout ? k_build_small<kXXH3, kBuildKPL, true> : k_build_small<kXXH3, kBuildKPL, false>),
-                           dim3(sgrid), dim3(kBlock), slds, c->ks, ba);
-    PHJ_LAUNCHED(c, "k_build_small");
-    ba.ocap = 16384;
-    const size_t blds = 64 + static_cast<size_t>(ba.ocap) * 4;
-    if (pl.hk == kMurmur3)
-        hipLaunchKernelGGL((hout ? k_build_big<kMurmur3, true> : k_build_big<kMurmur3, false>), dim3(256), dim3(kBlock),
-                           blds, c->ks, ba);
-    else
-        hipLaunchKernelGGL((hout ? k_build_big<kXXH3, true> : k_build_big<kXXH3, false>), dim3(256), dim3(kBlock), blds,
-                           c->ks, ba);
-    PHJ_LAUNCHED(c, "k_build_big");
-    c->tables_hcoded = hout;
-    if (c->home_ok && !ba.home) {
-        hipLaunchKernelGGL(k_csr_home, dim3((P + kWaves - 1) / kWaves), dim3(kBlock), 0, c->ks,
-                           static_cast<const uint4*>(c->items.p), ba.toffs, ba.tkeys, P,
-                           static_cast<longlong2*>(c->thome.p));
-        PHJ_LAUNCHED(c, "k_csr_home");
+    if (c->dry) return PHJ_OK;
+    HtArgs a{};
+    for (int g = 0; g < nseg; g++) {
+        a.codes[g] = codes[g];
+        a.bounds[g] = bounds[g];
     }
+    a.nseg = static_cast<uint32_t>(nseg);
+    a.nb1 = pl.nb1;
+    a.nb2 = pl.nb2;
+    a.table = static_cast<uint64_t*>(c->ht_tab.p);
+    a.desc = static_cast<uint2*>(c->ht_desc.p);
+    hipLaunchKernelGGL(k_ht_desc, dim3((pl.nb1 + 3) / 4), dim3(256), 0, c->ks, a);
+    PHJ_LAUNCHED(c, "k_ht_desc");
+    hipLaunchKernelGGL(k_ht_fill, dim3((P + kHtPpw - 1) / kHtPpw), dim3(256), 0, c->ks, a);
+    PHJ_LAUNCHED(c, "k_ht_fill");
     return PHJ_OK;
 }
 
-// phj_join takes the on-chip pass 2 (k_probe_p1, 512 x 4096 tiles) for a
-// 2-pass plan unless PHJ_P2PROBE=0 or a tuning knob changed the tile shape.
-bool use_p2probe(const phj_ctx* c, const Plan& pl, uint64_t nS) {
+// phj_join takes the on-chip path for a 2-pass plan unless PHJ_P2PROBE=0 or a
+// tuning knob changed the tile shape (the probe walks 512 x 4096 tiles).
+bool use_p2probe(const phj_ctx* c, const Plan& pl, uint64_t nS, uint64_t nR) {
     bool wc = false;
     return c->tune.p2probe && pl.npass == 2 && tile_shape(c, pl.nb2).tile == 4096 && tile_shape(c, pl.nb2).block == 512 &&
            pass_tile(c, static_cast<uint32_t>(std::min<uint64_t>(nS, 0xffffffffu)), pl.nb1, &wc) == 4096 && !wc &&
-           probe_p1_lds_bytes(4096, pl.nb2, 8) <= 160 * 1024;
+           probe_ht_lds_bytes(4096, pl.nb2) <= 160 * 1024 &&
+           4 * nR + 2ull * pl.Ppad < (1ull << 32);
 }
 
-template <int HK>
-const void* probe_p1_kernel(int diag, bool grp, bool home, bool ent, int wpe) {
-    if (diag == 1) return reinterpret_cast<const void*>(&k_probe_p1<512, 8, HK, 1>);
-    if (!grp)   // measurement: keys probed ungrouped, from registers
-        return reinterpret_cast<const void*>(&k_probe_p1<512, 8, HK, 0, 4, false, false>);
-    if (home && !ent) {   // one home slot per probe
-        if constexpr (HK == kHashed)   // no hashing left: registers for 8 waves per SIMD (PHJ_P1_WPE=8)
-            if (wpe == 8) return reinterpret_cast<const void*>(&k_probe_p1<512, 8, HK, 0, 8, false, true, true>);
-        return reinterpret_cast<const void*>(&k_probe_p1<512, 8, HK, 0, 6, false, true, true>);
-    }
-    if (ent)   // tiles from the private chains' chunk lists
-        return reinterpret_cast<const void*>(&k_probe_p1<512, 8, HK, 0, 6, true>);
-    if (wpe == 4)   // waves per SIMD the compiler budgets registers for (6: 3 workgroups per CU, measured best)
-        return reinterpret_cast<const void*>(&k_probe_p1<512, 8, HK, 0, 4>);
-    return reinterpret_cast<const void*>(&k_probe_p1<512, 8, HK, 0, 6>);
-}
-
-// Probe the partitioned-by-pass-1 probe side (partition_side p1_only) against
-// the CSR tables of build_csr; the count lands in c->count.
-int probe_p1(phj_ctx* c, const Plan& pl) {
+// Probe the probe side's pass-1 output (partition_side p1_only) against the
+// tables of build_ht; the count lands in c->count.
+int probe_ht(phj_ctx* c, const Plan& pl) {
     SideState& PS = c->side[PHJ_SIDE_PROBE];
     PHJ_HIP(c, hipMemsetAsync(c->count.p, 0, 8, c->ks));
     if (PS.nt2 == 0) return PHJ_OK;
-    P1ProbeArgs pa{};
+    HtProbeArgs pa{};
     pa.a = PS.p2;
-    pa.desc = static_cast<const uint4*>(c->items.p);
-    pa.toffs = static_cast<const uint32_t*>(c->toffs.p);
-    pa.tkeys = static_cast<const int64_t*>(c->tkeys.p);
+    pa.desc = static_cast<const uint2*>(c->ht_desc.p);
+    pa.table = static_cast<const uint64_t*>(c->ht_tab.p);
     pa.count = static_cast<unsigned long long*>(c->count.p);
     pa.seed = pl.seed;
     pa.nb2 = pl.nb2;
-    pa.ent = PS.p2_ent;
-    pa.home = c->home_ok ? static_cast<const longlong2*>(c->thome.p) : nullptr;
-    pa.ebase = PS.p2_ebase;
-    const size_t lds = probe_p1_lds_bytes(4096, pl.nb2, 8);
-    const int diag = env_int("PHJ_P1_DIAG", 0), wpe = env_int("PHJ_P1_WPE", 6);
-    const bool grp = env_int("PHJ_P1_GRP", 1) != 0;
-    // hash codes on both sides (pass 1 VAR 13 + tables built from codes): the
-    // probe's two hashes per key become the identity
-    if (PS.hcoded != c->tables_hcoded) return set_err(c, PHJ_ERR_INVALID, "probe side and tables disagree on hash codes");
-    const void* kfn = PS.hcoded ? probe_p1_kernel<kHashed>(diag, grp, pa.home != nullptr, pa.ent != nullptr, wpe)
-                      : pl.hk == kMurmur3 ? probe_p1_kernel<kMurmur3>(diag, grp, pa.home != nullptr, pa.ent != nullptr, wpe)
-                                          : probe_p1_kernel<kXXH3>(diag, grp, pa.home != nullptr, pa.ent != nullptr, wpe);
+    const size_t lds = std::max(probe_ht_lds_bytes(4096, pl.nb2), probe_ht2_lds_bytes(4096, pl.nb2));
+    // a keys-only pass 1 wrote codes (VAR 13); a stable pass 1 left whole tuples
+    const void* kfn = PS.hcoded ? reinterpret_cast<const void*>(&k_probe_ht<512, 8, kHashed>)
+                      : pl.hk == kMurmur3 ? reinterpret_cast<const void*>(&k_probe_ht<512, 8, kMurmur3>)
+                                          : reinterpret_cast<const void*>(&k_probe_ht<512, 8, kXXH3>);
+    if (PS.hcoded) {   // TEMPORARY measurement variants (PHJ_HT_VAR)
+        switch (env_int("PHJ_HT_VAR", 0)) {
+            case 1: kfn = reinterpret_cast<const void*>(&k_probe_ht<512, 8, kHashed, 4, 6>); break;
+            case 2: kfn = reinterpret_cast<const void*>(&k_probe_ht<512, 8, kHashed, 2, 4>); break;
+            case 3: kfn = reinterpret_cast<const void*>(&k_probe_ht<512, 8, kHashed, 4, 4>); break;
+            case 4: kfn = reinterpret_cast<const void*>(&k_probe_ht<512, 8, kHashed, 2, 6, true>); break;
+            case 5: kfn = reinterpret_cast<const void*>(&k_probe_ht<512, 8, kHashed, 2, 8>); break;
+            case 6: kfn = reinterpret_cast<const void*>(&k_probe_ht<512, 8, kHashed, 2, 6, false, 1>); break;
+            case 7: kfn = reinterpret_cast<const void*>(&k_probe_ht<512, 8, kHashed, 2, 6, false, 2>); break;
+            case 8: kfn = reinterpret_cast<const void*>(&k_probe_ht<512, 8, kHashed, 4, 6, false, 1>); break;
+            case 9: kfn = reinterpret_cast<const void*>(&k_probe_ht<512, 8, kHashed, 2, 6, true, 2>); break;
+            case 10: kfn = reinterpret_cast<const void*>(&k_probe_ht2<512, 8, kHashed, 2, 6>); break;
+            case 11: kfn = reinterpret_cast<const void*>(&k_probe_ht2<512, 8, kHashed, 2, 6, true>); break;
+            case 12: kfn = reinterpret_cast<const void*>(&k_probe_ht2<512, 8, kHashed, 4, 4>); break;
+            case 13: kfn = reinterpret_cast<const void*>(&k_probe_ht2<512, 8, kHashed, 2, 8>); break;
+            case 14: kfn = reinterpret_cast<const void*>(&k_probe_ht2<512, 8, kHashed, 2, 6, false, true>); break;
+            case 15: kfn = reinterpret_cast<const void*>(&k_probe_ht2<512, 8, kHashed, 2, 8, false, true>); break;
+            case 16: kfn = reinterpret_cast<const void*>(&k_probe_ht2<512, 8, kHashed, 2, 5, false, true>); break;
+            default: break;
+        }
+    }
     // persistent: as many workgroups as fit the chip at once (a multiple of 8:
     // XCD x owns tiles [x, x + 1) * ntiles / 8), never many more than tiles
     int per_cu = 0;
@@ -1376,7 +1399,7 @@ int probe_p1(phj_ctx* c, const Plan& pl) {
     const uint32_t grid = std::max<uint32_t>(8, std::min<uint32_t>(want, static_cast<uint32_t>(per_cu) * c->num_cus) & ~7u);
     void* kargs[] = {&pa};
     PHJ_HIP(c, hipLaunchKernel(kfn, dim3(grid), dim3(512), kargs, lds, c->ks));
-    PHJ_LAUNCHED(c, "k_probe_p1");
+    PHJ_LAUNCHED(c, "k_probe_ht");
     return PHJ_OK;
 }
 
@@ -1910,7 +1933,7 @@ void phj_ctx_destroy(phj_ctx* c) {
                           &S.bounds, &S.partials, &S.tseg2, &S.dig, &S.ccur, &S.ctab, &S.tstart, &S.priv})
             free_buf(*b);
     }
-    for (DevBuf* b : {&c->thome, &c->scan_partials, &c->prep, &c->tkeys, &c->tpays, &c->toffs, &c->gcursor, &c->items, &c->biglist,
+    for (DevBuf* b : {&c->ht_tab, &c->ht_desc, &c->r_codes, &c->r_bounds, &c->scan_partials, &c->prep, &c->tkeys, &c->tpays, &c->toffs, &c->gcursor, &c->items, &c->biglist,
                       &c->count, &c->np_tab, &c->np_pays, &c->np_ovf, &c->np_ovfb, &c->np_ovfn, &c->np_hot, &c->np_img, &c->fitems, &c->split, &c->mat_mark, &c->mat_cnt, &c->mat_rows})
         free_buf(*b);
     for (hipEvent_t e : c->evpool) (void)hipEventDestroy(e);
@@ -2183,44 +2206,32 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
     const uint32_t requested = pl.Ppad;   // reported; the join may sub-partition
     refine_plan(c, pl, R.n);
     hipEvent_t t0, t1, tr, b0, b1, p1;
-    if (use_p2probe(c, pl, S.n)) {
-        // S: pass 1 only (its pass 2 runs inside the probe); R: both passes and
-        // its bucket tables on the aux stream, beside S
+    if (use_p2probe(c, pl, S.n, R.n)) {
+        // S: pass 1 only (its pass 2 runs inside the probe); R: pass 1 as codes
+        // and its tables on the aux stream, beside S
         PHJ_TRY(mark(c, &t0));
-        const bool split = c->r_split != nullptr;
-        hipStream_t rs = split ? c->r_split : c->aux;
-        PHJ_HIP(c, hipStreamWaitEvent(rs, t0, 0));
-        hipEvent_t sd = nullptr;
-        int rc = PHJ_OK;
-        if (split) {   // S's pass 1 on its CU share (persistent grid sized to it)
-            PHJ_HIP(c, hipStreamWaitEvent(c->s_split, t0, 0));
-            c->ks = c->s_split;
-            const int cus = c->num_cus;
-            c->num_cus = c->s_split_cus;
-            rc = partition_side(c, PHJ_SIDE_PROBE, pl, true);
-            c->num_cus = cus;
-            if (rc == PHJ_OK) rc = mark(c, &sd);
-            c->ks = c->stream;
-            PHJ_TRY(rc);
-        } else {
-            PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, pl, true));
-        }
-        c->ks = rs;
-        rc = partition_side(c, PHJ_SIDE_BUILD, pl);
+        PHJ_HIP(c, hipStreamWaitEvent(c->aux, t0, 0));
+        PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, pl, true));
+        c->ks = c->aux;
+        int rc = ensure(c, c->r_codes, std::max<uint64_t>(1, R.n) * 8);
+        if (rc == PHJ_OK) rc = ensure(c, c->r_bounds, (static_cast<size_t>(pl.Ppad) + 1) * 4);
+        const int64_t* rcodes = static_cast<const int64_t*>(c->r_codes.p);
+        const uint32_t* rbnd = static_cast<const uint32_t*>(c->r_bounds.p);
+        if (rc == PHJ_OK) rc = partition_build(c, pl, static_cast<int64_t*>(c->r_codes.p), static_cast<uint32_t*>(c->r_bounds.p));
         if (rc == PHJ_OK) rc = mark(c, &b0);
-        if (rc == PHJ_OK) rc = timer_begin(c, "build", R.n * 8 * 2);
-        if (rc == PHJ_OK) rc = build_csr(c, pl, 1, &R.view);
+        // algorithmic bytes: the codes read, the tables written (~1.7 slots per code)
+        if (rc == PHJ_OK) rc = timer_begin(c, "build", R.n * 8 * 3);
+        if (rc == PHJ_OK) rc = build_ht(c, pl, 1, &rcodes, &rbnd, R.n);
         if (rc == PHJ_OK) rc = timer_end(c);
         if (rc == PHJ_OK) rc = mark(c, &tr);
         c->ks = c->stream;
         PHJ_TRY(rc);
-        if (sd) PHJ_HIP(c, hipStreamWaitEvent(c->stream, sd, 0));
         PHJ_HIP(c, hipStreamWaitEvent(c->stream, tr, 0));
         PHJ_TRY(mark(c, &t1));
         // algorithmic bytes: the pass-1 output read once (16-B tuples, or 8-B
-        // keys after a keys-only pass 1); the CSR tables are re-read from L2
+        // codes after a keys-only pass 1); the tables are re-read from L2
         PHJ_TRY(timer_begin(c, "probe", S.n * (S.p2.keys_only ? 8 : 16)));
-        PHJ_TRY(probe_p1(c, pl));
+        PHJ_TRY(probe_ht(c, pl));
         PHJ_TRY(timer_end(c));
         PHJ_TRY(mark(c, &p1));
         uint64_t m = 0;
@@ -2231,7 +2242,7 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
         r->probe_ms = elapsed(c, t1, p1);
         r->total_ms = elapsed(c, t0, p1);
         r->num_partitions = requested;
-        r->algorithmic_bytes = partition_bytes(pl, R.n) + S.n * (16 + 32) + R.n * 16 + S.n * 16;
+        r->algorithmic_bytes = R.n * (24 + 16) + S.n * (16 + 8) + R.n * 24 + S.n * 8;
         return fill_timers(c, r);
     }
     // Partition(R) || Partition(S) (HashJoin.hpp:210-216): S (the long one) is
@@ -2286,13 +2297,14 @@ int phj_prepare(phj_ctx* c, const phj_join_params* p) {
     Plan pl;
     PHJ_TRY(make_plan(c, p, pl));
     refine_plan(c, pl, c->side[PHJ_SIDE_BUILD].n);
-    if (use_p2probe(c, pl, c->side[PHJ_SIDE_PROBE].n)) {
+    if (use_p2probe(c, pl, c->side[PHJ_SIDE_PROBE].n, c->side[PHJ_SIDE_BUILD].n)) {
+        const uint64_t nR = c->side[PHJ_SIDE_BUILD].n;
         PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, pl, true));
-        PHJ_TRY(partition_side(c, PHJ_SIDE_BUILD, pl));
-        phj_partitioned rv{};
-        rv.n = c->side[PHJ_SIDE_BUILD].n;
-        rv.num_partitions = pl.Ppad;
-        PHJ_TRY(build_csr(c, pl, 1, &rv));
+        PHJ_TRY(ensure(c, c->r_codes, std::max<uint64_t>(1, nR) * 8));
+        PHJ_TRY(ensure(c, c->r_bounds, (static_cast<size_t>(pl.Ppad) + 1) * 4));
+        PHJ_TRY(partition_build(c, pl, nullptr, nullptr));
+        PHJ_TRY(build_ht(c, pl, 1, nullptr, nullptr, nR));
+        PHJ_TRY(ensure(c, c->count, 16));
         PHJ_HIP(c, hipStreamSynchronize(c->stream));
         return PHJ_OK;
     }
@@ -2394,6 +2406,46 @@ int phj_joined_download(phj_ctx* c, phj_joined* host, uint64_t n) {
     PHJ_HIP(c, hipSetDevice(c->device));
     PHJ_HIP(c, hipMemcpyAsync(host, c->mat_rows.p, n * sizeof(phj_joined), hipMemcpyDeviceToHost, c->stream));
     PHJ_HIP(c, hipStreamSynchronize(c->stream));
+    return PHJ_OK;
+}
+
+int phj_probe_pass1(phj_ctx* c, const phj_join_params* p, int64_t* keys, uint64_t n, uint32_t* bounds1,
+                    uint32_t* nb1, int* codes) {
+    if (!c) return PHJ_ERR_INVALID;
+    if (c->group) return set_err(c, PHJ_ERR_STATE, "phj_probe_pass1 takes a single-device context");
+    if (!p || !bounds1 || !nb1 || !codes || (n && !keys)) return set_err(c, PHJ_ERR_INVALID, "null argument");
+    (void)hipGetLastError();
+    PHJ_HIP(c, hipSetDevice(c->device));
+    if (p->algo != PHJ_ALGO_RADIX) return set_err(c, PHJ_ERR_INVALID, "radix join parameters required");
+    SideState& S = c->side[PHJ_SIDE_PROBE];
+    if (n != S.n) return set_err(c, PHJ_ERR_INVALID, "n must be the probe relation's size");
+    Plan pl;
+    PHJ_TRY(make_plan(c, p, pl));
+    refine_plan(c, pl, c->side[PHJ_SIDE_BUILD].n);
+    if (!use_p2probe(c, pl, S.n, c->side[PHJ_SIDE_BUILD].n))
+        return set_err(c, PHJ_ERR_STATE, "these params do not take the on-chip probe");
+    reset_timers(c);
+    c->ks = c->stream;
+    PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, pl, true));
+    const uint32_t nt = S.nt2;
+    PHJ_TRY(ensure(c, c->prep, (static_cast<size_t>(nt) + 1) * 4));
+    PHJ_TRY(ensure(c, S.kB, std::max<uint64_t>(1, n) * 8));
+    auto* off = static_cast<uint32_t*>(c->prep.p);
+    hipLaunchKernelGGL(k_tile_counts<4096>, dim3(nt / 256 + 1), dim3(256), 0, c->ks, S.p2, nt, off);
+    PHJ_LAUNCHED(c, "k_tile_counts");
+    PHJ_TRY(scan_u32(c, off, nt + 1, 1, nt + 1));
+    if (nt) {
+        hipLaunchKernelGGL(k_gather_pass1<4096>, dim3(nt), dim3(256), 0, c->ks, S.p2, off, static_cast<int64_t*>(S.kB.p));
+        PHJ_LAUNCHED(c, "k_gather_pass1");
+    }
+    uint32_t total = 0;
+    PHJ_HIP(c, hipMemcpyAsync(&total, off + nt, 4, hipMemcpyDeviceToHost, c->ks));
+    PHJ_HIP(c, hipMemcpyAsync(bounds1, S.bounds1.p, (static_cast<size_t>(pl.nb1) + 1) * 4, hipMemcpyDeviceToHost, c->ks));
+    if (n) PHJ_HIP(c, hipMemcpyAsync(keys, S.kB.p, n * 8, hipMemcpyDeviceToHost, c->ks));
+    PHJ_HIP(c, hipStreamSynchronize(c->ks));
+    if (total != n) return set_err(c, PHJ_ERR_STATE, "pass-1 tiles hold " + std::to_string(total) + " keys, not " + std::to_string(n));
+    *nb1 = pl.nb1;
+    *codes = S.hcoded ? 1 : 0;
     return PHJ_OK;
 }
 

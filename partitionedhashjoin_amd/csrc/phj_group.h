@@ -51,6 +51,7 @@ struct RcclApi {
     decltype(&ncclCommInitRank) CommInitRank = nullptr;
     decltype(&ncclCommInitAll) CommInitAll = nullptr;
     decltype(&ncclCommDestroy) CommDestroy = nullptr;
+    decltype(&ncclCommAbort) CommAbort = nullptr;
     decltype(&ncclAllGather) AllGather = nullptr;
     decltype(&ncclAllReduce) AllReduce = nullptr;
     decltype(&ncclBroadcast) Broadcast = nullptr;
@@ -82,6 +83,7 @@ RcclApi& rccl() {
         sym(a.CommInitRank, "ncclCommInitRank");
         sym(a.CommInitAll, "ncclCommInitAll");
         sym(a.CommDestroy, "ncclCommDestroy");
+        sym(a.CommAbort, "ncclCommAbort");
         sym(a.AllGather, "ncclAllGather");
         sym(a.AllReduce, "ncclAllReduce");
         sym(a.Broadcast, "ncclBroadcast");
@@ -212,6 +214,10 @@ struct MemberBufs {
     DevBuf send, recv, cnt, full;
     hipEvent_t packed = nullptr;
     bool rehearsal_packed = false;   // PHJ_REHEARSE: this member's block is packed (members > 0 pack once)
+    // local NoPartitioning exchange: this member's R shard, published before the
+    // barrier (peers never read a member's SideState, which it rebinds to its
+    // replicated relation while they copy)
+    const phj_tuple* shard = nullptr;
 };
 
 struct Group {
@@ -229,6 +235,10 @@ struct Group {
     bool rehearse = false;               // PHJ_REHEARSE (local exchange): members > 0 only feed the exchange
     int nlocal() const { return static_cast<int>(mem.size()); }
 };
+
+// Count buffer: {sum, failed} received, {count, failed} sent, then one word
+// per rank (exchange_sizes).
+size_t cnt_bytes(const Group& G) { return 32 + static_cast<size_t>(G.world) * 8; }
 
 // f(i) for every local member: on the member threads, or inline for one.
 int for_members(phj_ctx* shell, Group& G, const std::function<int(int)>& f) {
@@ -278,7 +288,7 @@ int exchange_sizes(phj_ctx* shell, Group& G, int side) {
     phj_ctx* c = G.mem[0];
     MemberBufs& B = G.buf[0];
     PHJ_HIP(shell, hipSetDevice(c->device));
-    PHJ_TRY(ensure(c, B.cnt, 16 + static_cast<size_t>(G.world) * 8));
+    PHJ_TRY(ensure(c, B.cnt, cnt_bytes(G)));
     auto* d = static_cast<uint64_t*>(B.cnt.p);
     const uint64_t mine = c->side[side].n;
     PHJ_HIP(shell, hipMemcpyAsync(d, &mine, 8, hipMemcpyHostToDevice, c->stream));
@@ -300,14 +310,29 @@ uint64_t total(const std::vector<uint64_t>& v) {
 // current launch stream (aux). `ok` = this member packed its block; with the
 // local exchange every member reaches the barrier even after an error, and
 // nobody copies when any member failed (its block may not exist).
+// With RCCL a member that failed before the collective still takes part in it
+// (its peers have enqueued theirs and would otherwise wait forever): it sends
+// whatever its block holds and reports the failure through the count
+// all-reduce (allreduce_count). Only when it has no buffers to take part with
+// does it abort its communicator, which ends the peers' collective with an error.
+int abort_comm(Group& G, int i, int rc) {
+    if (G.kind == Xchg::kRccl && G.comm[i]) {
+        (void)rccl().CommAbort(G.comm[i]);
+        G.comm[i] = nullptr;
+    }
+    return rc;
+}
+
 int allgather_blocks(Group& G, int i, uint64_t elems, bool ok, bool receive = true) {
     phj_ctx* c = G.mem[i];
     MemberBufs& B = G.buf[i];
     if (G.kind == Xchg::kRccl) {
-        if (!ok) return PHJ_ERR_STATE;
+        if (!G.comm[i]) return set_err(c, PHJ_ERR_STATE, "RCCL communicator aborted by an earlier failure");
+        if (!B.send.p || !B.recv.p || B.send.bytes < elems * 8 || B.recv.bytes < static_cast<size_t>(G.world) * elems * 8)
+            return abort_comm(G, i, ok ? set_err(c, PHJ_ERR_STATE, "exchange buffers missing") : PHJ_ERR_STATE);
         PHJ_NCCL(c, rccl().AllGather(B.send.p, B.recv.p, elems, ncclInt64, G.comm[i], c->ks));
         c->since_ev++;
-        return PHJ_OK;
+        return ok ? PHJ_OK : PHJ_ERR_STATE;
     }
     if (ok && hipEventRecord(B.packed, c->ks) != hipSuccess) ok = false;
     if (!ok) G.failed.store(1);
@@ -327,37 +352,62 @@ int allgather_blocks(Group& G, int i, uint64_t elems, bool ok, bool receive = tr
     return PHJ_OK;
 }
 
-// Sum of the members' device counts: RCCL all-reduce on the main stream into
-// B.cnt, or (local) the host adds the members' counts afterwards.
-int allreduce_count(Group& G, int i, const void* local_count) {
+// Sum of the members' device counts: RCCL all-reduce of {count, failed} on the
+// main stream (B.cnt words 2-3 -> 0-1), so a member that failed after the
+// exchange makes every rank return an error; or (local) the host adds the
+// members' counts afterwards and the member threads carry the errors.
+// `failed`: this member has no valid count but still takes part.
+int allreduce_count(Group& G, int i, const void* local_count, bool failed = false) {
     phj_ctx* c = G.mem[i];
     MemberBufs& B = G.buf[i];
     if (G.kind == Xchg::kRccl) {
-        PHJ_NCCL(c, rccl().AllReduce(local_count, B.cnt.p, 1, ncclUint64, ncclSum, G.comm[i], c->stream));
+        if (!G.comm[i]) return set_err(c, PHJ_ERR_STATE, "RCCL communicator aborted by an earlier failure");
+        auto* d = static_cast<uint64_t*>(B.cnt.p);
+        if (!d) return abort_comm(G, i, set_err(c, PHJ_ERR_STATE, "count buffer missing"));
+        PHJ_HIP(c, hipMemsetAsync(d + 2, 0, 16, c->stream));
+        if (failed) PHJ_HIP(c, hipMemsetAsync(d + 3, 1, 1, c->stream));
+        else PHJ_HIP(c, hipMemcpyAsync(d + 2, local_count, 8, hipMemcpyDeviceToDevice, c->stream));
+        PHJ_NCCL(c, rccl().AllReduce(d + 2, d, 2, ncclUint64, ncclSum, G.comm[i], c->stream));
     } else {
+        if (failed) return PHJ_OK;
         PHJ_HIP(c, hipMemcpyAsync(B.cnt.p, local_count, 8, hipMemcpyDeviceToDevice, c->stream));
     }
     c->since_ev++;
     return PHJ_OK;
 }
 
-int read_count(phj_ctx* c, const DevBuf& b, uint64_t* out) {
-    unsigned long long h = 0;
-    PHJ_HIP(c, hipMemcpyAsync(&h, b.p, 8, hipMemcpyDeviceToHost, c->stream));
+int read_count(Group& G, int i, uint64_t* out) {
+    phj_ctx* c = G.mem[i];
+    unsigned long long h[2] = {0, 0};
+    PHJ_HIP(c, hipMemcpyAsync(h, G.buf[i].cnt.p, 16, hipMemcpyDeviceToHost, c->stream));
     PHJ_HIP(c, hipStreamSynchronize(c->stream));
-    *out = h;
+    if (G.kind == Xchg::kRccl && h[1] != 0)
+        return set_err(c, PHJ_ERR_STATE, std::to_string(h[1]) + " rank(s) failed during the join");
+    *out = h[0];
     return PHJ_OK;
 }
 
-int member_alloc_radix(Group& G, int i, const Plan& pl) {
-    phj_ctx* c = G.mem[i];
-    MemberBufs& B = G.buf[i];
+// The exchange block carries the pass-1 codes and digit bounds of the on-chip
+// join (R's pass 2 happens inside the table build), or the fully partitioned
+// keys and final bounds of the fused join.
+bool member_p2(const Group& G, const phj_ctx* c, const Plan& pl) {
+    return use_p2probe(c, pl, c->side[PHJ_SIDE_PROBE].n, total(G.n[PHJ_SIDE_BUILD]));
+}
+
+PackLayout member_layout(const Group& G, const Plan& pl, bool p2) {
+    (void)p2;   // both forms ship codes / keys in final partition order + P + 1 bounds
     uint64_t maxn = 0;
     for (uint64_t x : G.n[PHJ_SIDE_BUILD]) maxn = std::max(maxn, x);
-    const PackLayout L = pack_layout(maxn, pl.Ppad);
+    return pack_layout(maxn, pl.Ppad);
+}
+
+int member_alloc_radix(Group& G, int i, const Plan& pl, bool p2) {
+    phj_ctx* c = G.mem[i];
+    MemberBufs& B = G.buf[i];
+    const PackLayout L = member_layout(G, pl, p2);
     PHJ_TRY(ensure(c, B.send, L.elems * 8));
     PHJ_TRY(ensure(c, B.recv, static_cast<size_t>(G.world) * L.elems * 8));
-    PHJ_TRY(ensure(c, B.cnt, 16 + static_cast<size_t>(G.world) * 8));
+    PHJ_TRY(ensure(c, B.cnt, cnt_bytes(G)));
     if (!B.packed) PHJ_HIP(c, hipEventCreateWithFlags(&B.packed, hipEventDisableTiming));
     return PHJ_OK;
 }
@@ -375,26 +425,37 @@ void gathered_segments(const Group& G, int i, const PackLayout& L, uint32_t P, p
     }
 }
 
+// The gathered blocks as build_ht segments: codes and partition bounds per rank.
+void gathered_codes(const Group& G, int i, const PackLayout& L, const int64_t** codes, const uint32_t** b1) {
+    const int64_t* base = static_cast<const int64_t*>(G.buf[i].recv.p);
+    for (int g = 0; g < G.world; g++) {
+        codes[g] = base + static_cast<size_t>(g) * L.elems;
+        b1[g] = reinterpret_cast<const uint32_t*>(base + static_cast<size_t>(g) * L.elems + L.maxn);
+    }
+}
+
 int member_prepare_radix(Group& G, int i, const Plan& pl) {
     phj_ctx* c = G.mem[i];
     PHJ_HIP(c, hipSetDevice(c->device));
-    PHJ_TRY(member_alloc_radix(G, i, pl));
+    const bool p2 = member_p2(G, c, pl);
+    PHJ_TRY(member_alloc_radix(G, i, pl, p2));
     struct DryScope {
         phj_ctx* c;
         ~DryScope() { c->dry = false; }
     } scope{c};
     c->dry = true;
-    const bool p2 = use_p2probe(c, pl, c->side[PHJ_SIDE_PROBE].n);
     PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, pl, p2));
-    PHJ_TRY(partition_side(c, PHJ_SIDE_BUILD, pl));
-    uint64_t maxn = 0;
-    for (uint64_t x : G.n[PHJ_SIDE_BUILD]) maxn = std::max(maxn, x);
-    const PackLayout L = pack_layout(maxn, pl.Ppad);
-    std::vector<phj_partitioned> segs(G.world);
-    gathered_segments(G, i, L, pl.Ppad, segs.data());
-    hipEvent_t b0, b1, p1;
-    if (p2) PHJ_TRY(build_csr(c, pl, G.world, segs.data()));
-    else PHJ_TRY(build_and_probe(c, pl, G.world, segs.data(), &b0, &b1, &p1));
+    const PackLayout L = member_layout(G, pl, p2);
+    if (p2) {
+        PHJ_TRY(partition_build(c, pl, nullptr, nullptr));
+        PHJ_TRY(build_ht(c, pl, G.world, nullptr, nullptr, total(G.n[PHJ_SIDE_BUILD])));
+    } else {
+        PHJ_TRY(partition_side(c, PHJ_SIDE_BUILD, pl));
+        std::vector<phj_partitioned> segs(G.world);
+        gathered_segments(G, i, L, pl.Ppad, segs.data());
+        hipEvent_t b0, b1, p1;
+        PHJ_TRY(build_and_probe(c, pl, G.world, segs.data(), &b0, &b1, &p1));
+    }
     PHJ_HIP(c, hipStreamSynchronize(c->stream));
     return PHJ_OK;
 }
@@ -403,14 +464,12 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
     phj_ctx* c = G.mem[i];
     MemberBufs& B = G.buf[i];
     std::memset(r, 0, sizeof(*r));
-    uint64_t maxn = 0;
-    for (uint64_t x : G.n[PHJ_SIDE_BUILD]) maxn = std::max(maxn, x);
-    const PackLayout L = pack_layout(maxn, pl.Ppad);
     const uint32_t P = pl.Ppad;
     SideState& R = c->side[PHJ_SIDE_BUILD];
-    // the probe side's pass 2 on-chip (k_probe_p1) against CSR tables built
-    // over the gathered segments on the aux stream, beside the S pass 1
-    const bool p2 = use_p2probe(c, pl, c->side[PHJ_SIDE_PROBE].n);
+    // the probe side's pass 2 on-chip (k_probe_ht) against code tables built
+    // over the gathered pass-1 blocks on the aux stream, beside the S pass 1
+    const bool p2 = member_p2(G, c, pl);
+    const PackLayout L = member_layout(G, pl, p2);
     std::vector<phj_partitioned> segs(G.world);   // filled once the exchange buffers exist
     hipEvent_t t0 = nullptr, x0 = nullptr, x1 = nullptr, t1, b0 = nullptr, b1 = nullptr, p1, te;
     // up to the exchange every step runs even after an error (no early
@@ -418,7 +477,7 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
     int rc = hipSetDevice(c->device) == hipSuccess ? PHJ_OK : set_err(c, PHJ_ERR_HIP, "hipSetDevice");
     if (rc == PHJ_OK) {
         reset_timers(c);
-        rc = member_alloc_radix(G, i, pl);
+        rc = member_alloc_radix(G, i, pl, p2);
     }
     if (rc == PHJ_OK) rc = mark(c, &t0);
     if (rc == PHJ_OK && hipStreamWaitEvent(c->aux, t0, 0) != hipSuccess) rc = set_err(c, PHJ_ERR_HIP, "wait t0");
@@ -435,15 +494,21 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
         r->total_ms = 0;
         return PHJ_OK;
     }
-    if (rc == PHJ_OK) rc = partition_side(c, PHJ_SIDE_BUILD, pl);
-    if (rc == PHJ_OK && R.n &&
-        hipMemcpyAsync(B.send.p, R.view.keys, R.n * 8, hipMemcpyDeviceToDevice, c->ks) != hipSuccess)
-        rc = set_err(c, PHJ_ERR_HIP, "pack keys");
-    if (rc == PHJ_OK &&
-        hipMemcpyAsync(static_cast<int64_t*>(B.send.p) + L.maxn, R.view.bounds, (static_cast<size_t>(P) + 1) * 4,
-                       hipMemcpyDeviceToDevice, c->ks) != hipSuccess)
-        rc = set_err(c, PHJ_ERR_HIP, "pack bounds");
-    c->since_ev += 2;
+    if (p2) {   // the R shard as codes in partition order, straight into the exchange block
+        if (rc == PHJ_OK)
+            rc = partition_build(c, pl, static_cast<int64_t*>(B.send.p),
+                                 reinterpret_cast<uint32_t*>(static_cast<int64_t*>(B.send.p) + L.maxn));
+    } else {
+        if (rc == PHJ_OK) rc = partition_side(c, PHJ_SIDE_BUILD, pl);
+        if (rc == PHJ_OK && R.n &&
+            hipMemcpyAsync(B.send.p, R.view.keys, R.n * 8, hipMemcpyDeviceToDevice, c->ks) != hipSuccess)
+            rc = set_err(c, PHJ_ERR_HIP, "pack keys");
+        if (rc == PHJ_OK &&
+            hipMemcpyAsync(static_cast<int64_t*>(B.send.p) + L.maxn, R.view.bounds, (static_cast<size_t>(P) + 1) * 4,
+                           hipMemcpyDeviceToDevice, c->ks) != hipSuccess)
+            rc = set_err(c, PHJ_ERR_HIP, "pack bounds");
+        c->since_ev += 2;
+    }
     // the S shard's pass 1 is issued on the main stream BEFORE the exchange:
     // an exchange with a host-side wait (the local rehearsal's barrier, a
     // blocking collective) must not hold back S, which needs nothing from R
@@ -460,17 +525,22 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
     if (rc == PHJ_OK) rc = rx;
     if (rc == PHJ_OK) rc = timer_end(c);
     if (rc == PHJ_OK) rc = mark(c, &x1);
-    if (rc == PHJ_OK) gathered_segments(G, i, L, P, segs.data());
     if (p2) {
         b0 = x1;
-        if (rc == PHJ_OK) rc = timer_begin(c, "build", total(G.n[PHJ_SIDE_BUILD]) * 16);
-        if (rc == PHJ_OK) rc = build_csr(c, pl, G.world, segs.data());
+        const int64_t* codes[kHtSegs];
+        const uint32_t* bnd[kHtSegs];
+        gathered_codes(G, i, L, codes, bnd);
+        const uint64_t nRall = total(G.n[PHJ_SIDE_BUILD]);
+        if (rc == PHJ_OK) rc = timer_begin(c, "build", nRall * 8 * 3);   // codes read, tables written
+        if (rc == PHJ_OK) rc = build_ht(c, pl, G.world, codes, bnd, nRall);
         if (rc == PHJ_OK) rc = timer_end(c);
         if (rc == PHJ_OK) rc = mark(c, &b1);
+    } else if (rc == PHJ_OK) {
+        gathered_segments(G, i, L, P, segs.data());
     }
     c->ks = c->stream;
-    PHJ_TRY(rc);
     if (G.rehearse && i > 0) {   // rehearsal: only member 0 joins (its time = one rank's device work)
+        PHJ_TRY(rc);
         B.rehearsal_packed = true;
         PHJ_HIP(c, hipStreamWaitEvent(c->stream, p2 ? b1 : x1, 0));
         PHJ_HIP(c, hipMemsetAsync(B.cnt.p, 0, 8, c->stream));
@@ -479,21 +549,29 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
         return PHJ_OK;
     }
     // (the S shard's pass 1 went out on the main stream before the exchange)
-    PHJ_HIP(c, hipStreamWaitEvent(c->stream, p2 ? b1 : x1, 0));
-    PHJ_TRY(mark(c, &t1));
-    if (p2) {
-        PHJ_TRY(timer_begin(c, "probe", c->side[PHJ_SIDE_PROBE].n * (c->side[PHJ_SIDE_PROBE].p2.keys_only ? 8 : 16)));
-        PHJ_TRY(probe_p1(c, pl));
-        PHJ_TRY(timer_end(c));
-        PHJ_TRY(mark(c, &p1));
-        c->last_fused = false;
-    } else {
-        PHJ_TRY(build_and_probe(c, pl, G.world, segs.data(), &b0, &b1, &p1));
+    auto join_local = [&]() -> int {
+        PHJ_HIP(c, hipStreamWaitEvent(c->stream, p2 ? b1 : x1, 0));
+        PHJ_TRY(mark(c, &t1));
+        if (p2) {
+            PHJ_TRY(timer_begin(c, "probe", c->side[PHJ_SIDE_PROBE].n * (c->side[PHJ_SIDE_PROBE].p2.keys_only ? 8 : 16)));
+            PHJ_TRY(probe_ht(c, pl));
+            PHJ_TRY(timer_end(c));
+            PHJ_TRY(mark(c, &p1));
+            c->last_fused = false;
+            return PHJ_OK;
+        }
+        return build_and_probe(c, pl, G.world, segs.data(), &b0, &b1, &p1);
+    };
+    if (rc == PHJ_OK) rc = join_local();
+    // RCCL: a member that failed still takes part in the count all-reduce
+    if (rc == PHJ_OK || G.kind == Xchg::kRccl) {
+        const int ra = allreduce_count(G, i, c->count.p, rc != PHJ_OK);
+        if (rc == PHJ_OK) rc = ra;
     }
-    PHJ_TRY(allreduce_count(G, i, c->count.p));
+    PHJ_TRY(rc);
     PHJ_TRY(mark(c, &te));
     uint64_t m = 0;
-    PHJ_TRY(read_count(c, B.cnt, &m));
+    PHJ_TRY(read_count(G, i, &m));
     r->matches = m;
     r->partition_ms = elapsed(c, t0, t1);
     r->build_ms = elapsed(c, b0, b1);
@@ -539,7 +617,7 @@ int member_nopart(Group& G, int i, const phj_join_params* p, phj_join_result* r,
         reset_timers(c);
         rc = ensure(c, B.full, std::max<uint64_t>(1, nRall) * sizeof(phj_tuple));
     }
-    if (rc == PHJ_OK) rc = ensure(c, B.cnt, 16 + static_cast<size_t>(G.world) * 8);
+    if (rc == PHJ_OK) rc = ensure(c, B.cnt, cnt_bytes(G));
     if (rc == PHJ_OK && !B.packed && hipEventCreateWithFlags(&B.packed, hipEventDisableTiming) != hipSuccess)
         rc = set_err(c, PHJ_ERR_HIP, "hipEventCreate");
     auto* full = static_cast<phj_tuple*>(B.full.p);
@@ -557,7 +635,10 @@ int member_nopart(Group& G, int i, const phj_join_params* p, phj_join_result* r,
     if (rc == PHJ_OK) rc = mark(c, &t0);
     if (rc == PHJ_OK) rc = timer_begin(c, "exchange", (nRall - shard_n) * sizeof(phj_tuple));
     if (G.kind == Xchg::kRccl) {
-        PHJ_TRY(rc);
+        // a member that failed still takes part (its peers' broadcasts wait
+        // for it) when it has the receive buffer, else it aborts the communicator
+        if (rc != PHJ_OK && (!full || B.full.bytes < nRall * sizeof(phj_tuple) || !B.cnt.p)) return abort_comm(G, i, rc);
+        if (!G.comm[i]) return set_err(c, PHJ_ERR_STATE, "RCCL communicator aborted by an earlier failure");
         // all-gather-v: one broadcast per root, grouped, straight into the
         // contiguous relation (no padding, no compaction)
         uint64_t off = 0;
@@ -574,16 +655,18 @@ int member_nopart(Group& G, int i, const phj_join_params* p, phj_join_result* r,
         PHJ_NCCL(c, rccl().GroupEnd());
         c->since_ev++;
     } else {
-        // the shards are resident and read-only: after the barrier every member
-        // copies them all (their relations were bound before the join)
+        // the shards are resident and read-only: every member publishes its
+        // shard pointer, then after the barrier copies them all from those
+        // snapshots (a peer may already have rebound its SideState to its own
+        // replicated relation, which is still being filled)
+        B.shard = shard;
         if (rc != PHJ_OK) G.failed.store(1);
         G.barrier->wait();
         if (G.failed.load()) return rc != PHJ_OK ? rc : set_err(c, PHJ_ERR_STATE, "another member failed");
         uint64_t off = 0;
         for (int h = 0; h < G.nlocal(); h++) {
             phj_ctx* ch = G.mem[h];
-            const void* src = h == i ? static_cast<const void*>(shard)
-                                     : static_cast<const void*>(G.mem[h]->side[PHJ_SIDE_BUILD].rel);
+            const void* src = static_cast<const void*>(G.buf[h].shard);
             if (nr[h]) {
                 if (ch->device == c->device)
                     PHJ_HIP(c, hipMemcpyAsync(full + off, src, nr[h] * sizeof(phj_tuple), hipMemcpyDeviceToDevice,
@@ -596,19 +679,26 @@ int member_nopart(Group& G, int i, const phj_join_params* p, phj_join_result* r,
         }
         c->since_ev++;
     }
-    PHJ_TRY(rc);
-    PHJ_TRY(timer_end(c));
-    PHJ_TRY(mark(c, &t1));
-    R.rel = full;
-    R.n = nRall;
-    R.partitioned = false;
-    // join_nopart resets nothing: its timers follow the exchange timer
     phj_join_result jr{};
-    PHJ_TRY(join_nopart(c, p, &jr));
-    PHJ_TRY(allreduce_count(G, i, c->count.p));
+    auto join_local = [&]() -> int {
+        PHJ_TRY(timer_end(c));
+        PHJ_TRY(mark(c, &t1));
+        R.rel = full;
+        R.n = nRall;
+        R.partitioned = false;
+        // join_nopart resets nothing: its timers follow the exchange timer
+        return join_nopart(c, p, &jr);
+    };
+    if (rc == PHJ_OK) rc = join_local();
+    // RCCL: a member that failed still takes part in the count all-reduce
+    if (rc == PHJ_OK || G.kind == Xchg::kRccl) {
+        const int ra = allreduce_count(G, i, c->count.p, rc != PHJ_OK);
+        if (rc == PHJ_OK) rc = ra;
+    }
+    PHJ_TRY(rc);
     PHJ_TRY(mark(c, &te));
     uint64_t m = 0;
-    PHJ_TRY(read_count(c, B.cnt, &m));
+    PHJ_TRY(read_count(G, i, &m));
     *r = jr;
     r->matches = m;
     r->exchange_ms = elapsed(c, t0, t1);
@@ -646,7 +736,9 @@ int group_join(phj_ctx* shell, const phj_join_params* p, phj_join_result* r, boo
     if (p->algo != PHJ_ALGO_RADIX) return set_err(shell, PHJ_ERR_INVALID, "Unrecognized join algorithm");
     if (G.world > kMaxSegs) return set_err(shell, PHJ_ERR_RANGE, "at most 16 ranks");
     Plan pl;
-    PHJ_TRY(make_plan(shell, p, pl));
+    // planned with member 0's tuning (refine_plan below uses it too), so a
+    // group plans exactly as a single-device context would
+    if (const int rc = make_plan(G.mem[0], p, pl); rc != PHJ_OK) return set_err(shell, rc, G.mem[0]->err);
     const uint32_t requested = pl.Ppad;
     // every rank plans for the GLOBAL build side (the gathered segments), so all
     // ranks partition by the same function

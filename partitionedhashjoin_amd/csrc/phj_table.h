@@ -1,0 +1,866 @@
+// phj_table.h — the counting radix join's build side and on-chip probe.
+//
+// The reference joins partition by partition: build a LinearProbing table on
+// R_p, probe it with S_p, count the S tuples whose Get() finds a key
+// (src/RadixCluster/HashJoin.hpp:267-303, Get() = first match,
+// src/HashTables/LinearProbing.hpp:160-180). The count only tests key
+// equality, and both hash functions are bijections of the 64-bit keys
+// (phj_hash.h), so the join runs over hash codes c = h(k): equal codes <=>
+// equal keys.
+//
+//   k_scatter_codes : R's pass 1, keys only, written as codes, contiguous per
+//                     pass-1 digit d1 (k_hist + scan give the offsets)
+//   k_ht_*          : R's pass 2 over every build segment (the shards of all
+//                     ranks after the multi-GPU all-gather) into a scratch in
+//                     final partition order p = d1 * nb2 + d2, then one wave per
+//                     partition builds its table in LDS and writes it out
+//   k_probe_ht      : the probe side's pass 2 on chip: a 4096-key pass-1 tile
+//                     (one d1) is grouped by d2 in LDS and every key probes the
+//                     table of its final partition
+//
+// Table of a final partition p: an open-addressed array of codes in 2-slot
+// (16-B) buckets, cap = the smallest power of two >= 1.5 * |R_p| slots (load
+// <= 2/3), home bucket (c >> 24) & (buckets - 1), linear probing over buckets
+// with wrap-around, a bucket's slots filled in order, duplicates stored once
+// (the count is a semi-join, a set test). There is no occupancy word and no
+// key value is reserved: an empty slot holds E_p, a code of ANOTHER
+// partition, which no code probing p can equal. Every partition function maps
+// code 0 to partition 0 and code 1 elsewhere (q_from_hash: radix bits, h % P
+// and sub-partitions alike), so E_p = (p == 0 ? 1 : 0). A probe reads one
+// 16-B bucket (one cache line) and stops at a match or an empty slot; the CSR
+// form needed a home slot plus, for a quarter to a half of the keys, a second
+// line.
+//
+// Table layout: the region of d1 starts at slot 4 * Σ_g b1_g[d1] + 2 * nb2 * d1
+// (closed form from the segments' pass-1 bounds, no scan: a partition's cap is
+// < 3 |R_p| + 2), its partitions' tables follow in d2 order; desc[p] = {slot
+// base, buckets - 1}.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "phj_hash.h"
+#include "phj_partition.h"
+
+namespace phj {
+
+constexpr int kHtSegs = 16;             // build segments (ranks) per join
+constexpr uint32_t kHtBucketShift = 24; // home bucket = (c >> 24) & (buckets - 1): clear of every partition bit
+
+__host__ __device__ __forceinline__ uint32_t ht_cap(uint32_t m) {
+    // slots: the smallest power of two >= 1.5 m, at least one 2-slot bucket
+    const uint32_t want = m + (m + 1) / 2;
+    uint32_t c = 2;
+    while (c < want) c <<= 1;
+    return c;
+}
+
+__host__ __device__ __forceinline__ uint64_t ht_empty(uint32_t p) { return p == 0 ? 1ull : 0ull; }
+
+// Rank of this lane's digit d among the tile's keys of digit d (counter row C
+// in LDS). The lanes sharing the wave's first active digit take one atomic
+// together (a hot key's digit no longer serialises 64-way), the others one
+// each. Every lane calls it (ballots); d is computed on invalid lanes too.
+__device__ __forceinline__ uint32_t agg_rank(uint32_t* C, uint32_t d, bool valid) {
+    const uint64_t act = __ballot(valid);
+    if (act == 0) return 0;
+    const int leader = __builtin_ctzll(act);
+    const uint32_t ld = __builtin_amdgcn_readlane(d, leader);
+    const bool mine = valid && d == ld;
+    const uint64_t same = __ballot(mine);
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t base = 0;
+    if (lane == static_cast<uint32_t>(leader)) base = atomicAdd(&C[ld], static_cast<uint32_t>(__popcll(same)));
+    base = __builtin_amdgcn_readlane(base, leader);
+    if (mine) return base + static_cast<uint32_t>(__popcll(same & lanemask_lt()));
+    return valid ? atomicAdd(&C[d], 1u) : 0u;
+}
+
+
+// ---------------------------------------------------------------------------
+// R pass 1: hash codes, contiguous per digit. One tile of T = BLOCK * ITEMS
+// tuples per workgroup: keys loaded (8 B of each 16-B tuple), hashed, ranked
+// by one LDS atomic per key (the order inside a partition is free), sorted by
+// digit in LDS and written so consecutive lanes fill consecutive slots of each
+// digit run. Offsets from k_hist's scanned histogram (hist[d * ntiles + t]).
+// ---------------------------------------------------------------------------
+__host__ __device__ constexpr size_t scatter_codes_lds_bytes(int T, uint32_t nb) {
+    return static_cast<size_t>(T) * (8 + (nb <= 256 ? 1 : 2)) + static_cast<size_t>(nb) * 12 + 64 + 16;
+}
+
+template <int BLOCK, int ITEMS, int HK>
+__global__ __launch_bounds__(BLOCK) void k_scatter_codes(PassArgs a) {
+    constexpr int T = BLOCK * ITEMS;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t nb = a.nbins;
+    int64_t* skey = reinterpret_cast<int64_t*>(smem);
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(skey + T);   // [nb] counts, then tile-local starts
+    uint32_t* gofs = cnt + nb;                                 // [nb]
+    uint32_t* dstart = gofs + nb;                              // [nb]
+    uint32_t* tmp = dstart + nb;                               // 16 words
+    const SortedDigits sdig{tmp + 16, nb <= 256};              // [T]
+    TileLoc L;
+    if (!locate_tile<T>(a, tile_id(a), L)) return;
+    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const uint32_t n = L.hi - L.lo;
+    for (uint32_t d = tid; d < nb; d += BLOCK) {
+        cnt[d] = 0;
+        gofs[d] = a.hist[static_cast<size_t>(d) * L.ntiles_s + L.tseg];
+    }
+    const longlong2* rel = reinterpret_cast<const longlong2*>(a.in_keys);
+    int64_t code[ITEMS];
+    uint32_t dig[ITEMS], rank[ITEMS];
+    const uint32_t wbase = wave * 64 * ITEMS;
+#pragma unroll
+    for (int i = 0; i < ITEMS; i++) {
+        const uint32_t e = wbase + i * 64 + lane;
+        code[i] = e < n ? rel[L.lo + e].x : 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < ITEMS; i++) {
+        const uint32_t e = wbase + i * 64 + lane;
+        const uint64_t h = hash64<HK>(static_cast<uint64_t>(code[i]), a.f.seed);
+        code[i] = static_cast<int64_t>(h);
+        dig[i] = static_cast<uint32_t>(q_from_hash(h, a.f) >> a.f.shift) & a.f.dmask;
+        if (e < n) rank[i] = atomicAdd(&cnt[dig[i]], 1u);
+    }
+    __syncthreads();
+    {
+        const uint32_t dpt = (nb + BLOCK - 1) / BLOCK, d0 = tid * dpt;
+        uint32_t local = 0;
+        for (uint32_t j = 0; j < dpt; j++)
+            if (d0 + j < nb) local += cnt[d0 + j];
+        uint32_t tot;
+        uint32_t run = block_exclusive_scan_t<BLOCK / 64>(local, tmp, tot);
+        for (uint32_t j = 0; j < dpt; j++) {
+            const uint32_t d = d0 + j;
+            if (d < nb) {
+                const uint32_t c = cnt[d];
+                cnt[d] = run;
+                dstart[d] = run;
+                run += c;
+            }
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < ITEMS; i++) {
+        const uint32_t e = wbase + i * 64 + lane;
+        if (e < n) {
+            const uint32_t pos = cnt[dig[i]] + rank[i];
+            skey[pos] = code[i];
+            sdig.put(pos, dig[i]);
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < ITEMS; i++) {
+        const uint32_t k = i * BLOCK + tid;
+        if (k < n) {
+            const uint32_t d = sdig.get(k);
+            a.out_keys[gofs[d] + (k - dstart[d])] = skey[k];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// The build side. Every rank groups ITS OWN codes by final partition before
+// the exchange (R pass 2, on the rank's shard only: kHtTpd workgroups per
+// pass-1 digit d1, each a contiguous slice of d1's run, count then scatter by
+// d2; hist[p * kHtTpd + k] scanned = where slice k's codes of partition p
+// start), so a build segment is {codes in partition order, bounds[P + 1]}.
+// After the exchange only the tables are built over all segments:
+//   k_ht_desc: per d1 (one wave) the table offsets of its partitions from the
+//       partition sizes (closed-form region base, prefix of the caps)
+//   k_ht_fill: a workgroup stages the codes of 16 consecutive partitions from
+//       every segment into LDS (coalesced), then each wave builds a
+//       partition's table in its LDS slice (compare-and-swap in LDS) and
+//       writes it out in whole lines
+// ---------------------------------------------------------------------------
+constexpr uint32_t kHtTpd = 16;      // R pass-2 workgroups per pass-1 digit
+constexpr uint32_t kHtLcap = 512;    // k_ht_fill: LDS table slots per wave
+constexpr uint32_t kHtPpw = 16;      // k_ht_fill: partitions per workgroup
+constexpr uint32_t kHtLcodes = 4096; // k_ht_fill: staged codes per workgroup (more: read in place)
+constexpr uint32_t kHtUnr = 8;       // codes per thread in flight
+
+// R pass 2 over one relation's pass-1 output (codes contiguous per d1).
+struct HtPass2Args {
+    const int64_t* codes;      // pass-1 output
+    const uint32_t* b1;        // nb1 + 1
+    uint32_t* hist;            // [P * kHtTpd + 1], scanned in place between the kernels
+    int64_t* out;              // codes in final partition order
+    uint32_t* bounds;          // P + 1 final bounds (written by k_ht_scatter's slice-0 workgroups)
+    uint32_t nb1, nb2;
+    DigitFn f2;                // d2 = q_from_hash(c, f2) & f2.dmask (shift 0)
+};
+
+__global__ __launch_bounds__(256) void k_ht_hist(HtPass2Args a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(smem);   // [nb2]
+    const uint32_t d1 = blockIdx.x / kHtTpd, k = blockIdx.x % kHtTpd, tid = threadIdx.x;
+    const uint32_t nb2 = a.nb2;
+    const uint32_t lo = a.b1[d1], m1 = a.b1[d1 + 1] - lo;
+    const uint32_t f_lo = lo + static_cast<uint32_t>(static_cast<uint64_t>(m1) * k / kHtTpd);
+    const uint32_t f_hi = lo + static_cast<uint32_t>(static_cast<uint64_t>(m1) * (k + 1) / kHtTpd);
+    for (uint32_t d = tid; d < nb2; d += 256) cnt[d] = 0;
+    __syncthreads();
+    for (uint32_t f0 = f_lo; f0 < f_hi; f0 += 256 * kHtUnr) {
+        uint64_t c[kHtUnr];
+#pragma unroll
+        for (uint32_t u = 0; u < kHtUnr; u++) {
+            const uint32_t f = f0 + u * 256 + tid;
+            c[u] = f < f_hi ? static_cast<uint64_t>(a.codes[f]) : 0;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kHtUnr; u++)
+            count_digit(cnt, static_cast<uint32_t>(q_from_hash(c[u], a.f2)) & a.f2.dmask, f0 + u * 256 + tid < f_hi);
+    }
+    __syncthreads();
+    uint32_t* h = a.hist + static_cast<size_t>(d1) * nb2 * kHtTpd + k;
+    for (uint32_t d = tid; d < nb2; d += 256) h[static_cast<size_t>(d) * kHtTpd] = cnt[d];
+    if (blockIdx.x == 0 && tid == 0) a.hist[static_cast<size_t>(a.nb1) * nb2 * kHtTpd] = 0;
+}
+
+__global__ __launch_bounds__(256) void k_ht_scatter(HtPass2Args a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint32_t* cur = reinterpret_cast<uint32_t*>(smem);   // [nb2] output cursors
+    const uint32_t d1 = blockIdx.x / kHtTpd, k = blockIdx.x % kHtTpd, tid = threadIdx.x;
+    const uint32_t nb2 = a.nb2;
+    const uint32_t lo = a.b1[d1], m1 = a.b1[d1 + 1] - lo;
+    const uint32_t f_lo = lo + static_cast<uint32_t>(static_cast<uint64_t>(m1) * k / kHtTpd);
+    const uint32_t f_hi = lo + static_cast<uint32_t>(static_cast<uint64_t>(m1) * (k + 1) / kHtTpd);
+    const uint32_t* h = a.hist + static_cast<size_t>(d1) * nb2 * kHtTpd + k;
+    for (uint32_t d = tid; d < nb2; d += 256) {
+        cur[d] = h[static_cast<size_t>(d) * kHtTpd];
+        if (k == 0) a.bounds[static_cast<size_t>(d1) * nb2 + d] = cur[d];   // partition start = slice 0's
+    }
+    if (blockIdx.x == 0 && tid == 0) a.bounds[static_cast<size_t>(a.nb1) * nb2] = a.hist[static_cast<size_t>(a.nb1) * nb2 * kHtTpd];
+    __syncthreads();
+    for (uint32_t f0 = f_lo; f0 < f_hi; f0 += 256 * kHtUnr) {
+        uint64_t c[kHtUnr];
+#pragma unroll
+        for (uint32_t u = 0; u < kHtUnr; u++) {
+            const uint32_t f = f0 + u * 256 + tid;
+            c[u] = f < f_hi ? static_cast<uint64_t>(a.codes[f]) : 0;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kHtUnr; u++) {
+            const uint32_t f = f0 + u * 256 + tid;
+            const uint32_t d = static_cast<uint32_t>(q_from_hash(c[u], a.f2)) & a.f2.dmask;
+            const uint32_t r = agg_rank(cur, d, f < f_hi);
+            if (f < f_hi) a.out[r] = static_cast<int64_t>(c[u]);
+        }
+    }
+}
+
+// The tables over `nseg` build segments (codes in partition order + bounds).
+struct HtArgs {
+    const int64_t* codes[kHtSegs];
+    const uint32_t* bounds[kHtSegs];   // P + 1 each
+    uint32_t nseg, nb1, nb2, pad;
+    uint64_t* table;                   // slots (4 |R| + 2 P bound)
+    uint2* desc;                       // per final partition: {slot base (even), buckets - 1}
+};
+
+__device__ __forceinline__ uint32_t ht_part_size(const HtArgs& a, uint32_t p) {
+    uint32_t m = 0;
+    for (uint32_t g = 0; g < a.nseg; g++) m += a.bounds[g][p + 1] - a.bounds[g][p];
+    return m;
+}
+
+// One wave per d1: desc[p] for its nb2 partitions.
+__global__ __launch_bounds__(256) void k_ht_desc(HtArgs a) {
+    const uint32_t d1 = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (d1 >= a.nb1) return;
+    const uint32_t nb2 = a.nb2;
+    uint32_t s1 = 0;   // d1's first code over all segments
+    for (uint32_t g = 0; g < a.nseg; g++) s1 += a.bounds[g][static_cast<size_t>(d1) * nb2];
+    const uint64_t rbase = 4ull * s1 + 2ull * nb2 * d1;
+    uint32_t carry = 0;
+    for (uint32_t d0 = 0; d0 < nb2; d0 += 64) {
+        const uint32_t d = d0 + lane;
+        const uint32_t cap = d < nb2 ? ht_cap(ht_part_size(a, d1 * nb2 + d)) : 0u;
+        uint32_t x = cap;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= static_cast<uint32_t>(o)) x += y;
+        }
+        if (d < nb2) a.desc[static_cast<size_t>(d1) * nb2 + d] = make_uint2(static_cast<uint32_t>(rbase + carry + x - cap), cap / 2 - 1u);
+        carry += __shfl(x, 63, 64);
+    }
+}
+
+__device__ __forceinline__ void ht_insert(uint64_t* tab, uint32_t bmask, uint64_t e, uint64_t c) {
+    uint32_t b = static_cast<uint32_t>(c >> kHtBucketShift) & bmask;
+    for (;;) {
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const uint64_t old = atomicCAS(reinterpret_cast<unsigned long long*>(tab + 2 * b + j), e, c);
+            if (old == e || old == c) return;   // placed, or already there (duplicates stored once)
+        }
+        b = (b + 1) & bmask;
+    }
+}
+
+// A workgroup per kHtPpw consecutive partitions: their codes from every
+// segment are staged in LDS (segment g's run at soff[g]), then wave w builds
+// partitions w, w + 4, ... in its LDS table slice and writes each out.
+__global__ __launch_bounds__(256) void k_ht_fill(HtArgs a) {
+    __shared__ __attribute__((aligned(16))) uint64_t wtab[4][kHtLcap];
+    __shared__ __attribute__((aligned(16))) int64_t scode[kHtLcodes];
+    __shared__ uint32_t soff[kHtSegs + 1], slo[kHtSegs];
+    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const uint32_t P = a.nb1 * a.nb2;
+    const uint32_t p0 = blockIdx.x * kHtPpw, p1 = min(P, p0 + kHtPpw);
+    if (wave == 0) {
+        uint32_t lo = 0, n = 0;
+        if (lane < a.nseg) {
+            lo = a.bounds[lane][p0];
+            n = a.bounds[lane][p1] - lo;
+        }
+        uint32_t x = n;
+#pragma unroll
+        for (int o = 1; o < kHtSegs; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= static_cast<uint32_t>(o)) x += y;
+        }
+        if (lane < a.nseg) {
+            slo[lane] = lo;
+            soff[lane] = x - n;
+        }
+        if (lane == kHtSegs - 1) soff[a.nseg] = x;
+    }
+    __syncthreads();
+    const uint32_t ntot = soff[a.nseg];
+    const bool staged = ntot <= kHtLcodes;
+    if (staged) {
+        for (uint32_t g = 0; g < a.nseg; g++) {
+            const uint32_t n = soff[g + 1] - soff[g];
+            const int64_t* src = a.codes[g] + slo[g];
+            for (uint32_t j = tid; j < n; j += 256) scode[soff[g] + j] = src[j];
+        }
+    }
+    __syncthreads();
+    uint64_t* tab = wtab[wave];
+    for (uint32_t p = p0 + wave; p < p1; p += 4) {
+        const uint2 ds = a.desc[p];
+        const uint32_t cap = 2 * (ds.y + 1);
+        const uint64_t e = ht_empty(p);
+        uint64_t* out = a.table + ds.x;
+        const bool lds = cap <= kHtLcap;
+        uint64_t* t = lds ? tab : out;
+        for (uint32_t s = lane; s < cap; s += 64) t[s] = e;
+        if (lds) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        else __threadfence();
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t g = 0; g < a.nseg; g++) {
+            const uint32_t b0 = a.bounds[g][p], b1e = a.bounds[g][p + 1];
+            for (uint32_t j = b0 + lane; j < b1e; j += 64) {
+                const uint64_t c = static_cast<uint64_t>(staged ? scode[soff[g] + (j - slo[g])] : a.codes[g][j]);
+                ht_insert(t, ds.y, e, c);
+            }
+        }
+        if (lds) {
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            ulonglong2* o2 = reinterpret_cast<ulonglong2*>(out);
+            const ulonglong2* t2 = reinterpret_cast<const ulonglong2*>(tab);
+            for (uint32_t b = lane; b < cap / 2; b += 64) o2[b] = t2[b];
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// On-chip probe: the probe side's pass 2 never lands in HBM. Persistent: XCD x
+// walks tiles [x, x + 1) * ntiles / 8 of the pass-1 output (tiles of one d1 are
+// contiguous, so an XCD's L2 holds the few d1 regions it probes), its
+// workgroups round-robin over them, and the next tile's keys load while the
+// current one is probed. A tile is grouped by d2 with one LDS atomic per key
+// (an unstable counting sort: neighbouring lanes then probe the same small
+// table, often the same cache line), the tile's nb2 descriptors are staged in
+// LDS when d1 changes, and every key probes PB slots at a time.
+// HK = kHashed when the pass-1 output holds codes (VAR 13), else the key is
+// hashed here (stable pass 1 of whole tuples).
+// ---------------------------------------------------------------------------
+struct HtProbeArgs {
+    PassArgs a;                  // the pass-2 tile mapping over the pass-1 output
+    const uint2* desc;
+    const uint64_t* table;
+    unsigned long long* count;
+    uint64_t seed;
+    uint32_t nb2;
+    uint32_t pad;
+};
+
+__host__ __device__ constexpr size_t probe_ht_lds_bytes(int T, uint32_t nb) {
+    return static_cast<size_t>(T) * 8 + static_cast<size_t>(nb) * 12 + 64 + 16 + static_cast<size_t>(nb) * 4 * 8;
+}
+
+template <int BLOCK, int ITEMS, int HK, int PBN = 2, int WPE = 6, bool DIAG = false, int GMODE = 0>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void k_probe_ht(HtProbeArgs pa) {
+    constexpr int T = BLOCK * ITEMS;
+    constexpr int PB = PBN;   // probes in flight per lane
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const PassArgs& a = pa.a;
+    const uint32_t nb = a.nbins;
+    int64_t* skey = reinterpret_cast<int64_t*>(smem);
+    uint2* sdesc = reinterpret_cast<uint2*>(skey + T);          // [nb]
+    uint32_t* cnt_d = reinterpret_cast<uint32_t*>(sdesc + nb);   // [nb] counts, then starts
+    uint32_t* tmp = cnt_d + nb;                                  // 16 words
+    __shared__ uint32_t red[BLOCK / 64];
+
+    const uint32_t total = a.tile_base[a.nseg];
+    const uint32_t xcd = blockIdx.x & 7u, g8 = gridDim.x >> 3;
+    const uint32_t t_lo = static_cast<uint32_t>(static_cast<uint64_t>(total) * xcd / 8);
+    const uint32_t t_hi = static_cast<uint32_t>(static_cast<uint64_t>(total) * (xcd + 1) / 8);
+    uint32_t tile = t_lo + (blockIdx.x >> 3);
+    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    uint32_t hits = 0;
+    if (tile < t_hi) {
+        const uint32_t wbase = wave * 64 * ITEMS;
+        const longlong2* rel = reinterpret_cast<const longlong2*>(a.in_keys);
+        const bool soa = a.in_pays != nullptr || a.keys_only;   // key column, or AoS tuples
+        int64_t key[ITEMS];
+        uint32_t vm = 0, d1 = 0;   // vm bit i: item i holds a key
+        auto load = [&](uint32_t t, uint32_t& m, uint32_t& d) {
+            d = a.tile_seg[t];
+            m = 0;
+            TileLoc L;
+            locate_tile<T>(a, t, L);
+            const uint32_t c = L.hi - L.lo;
+#pragma unroll
+            for (int i = 0; i < ITEMS; i++) {
+                const uint32_t e = wbase + i * 64 + lane;
+                key[i] = e < c ? (soa ? a.in_keys[L.lo + e] : rel[L.lo + e].x) : 0;
+                m |= e < c ? (1u << i) : 0u;
+            }
+        };
+        load(tile, vm, d1);
+        uint32_t staged = 0xffffffffu;   // d1 whose descriptors sit in LDS
+        for (;;) {
+            const bool restage = d1 != staged;   // consecutive tiles mostly share d1
+            for (uint32_t d = tid; d < nb; d += BLOCK) {
+                cnt_d[d] = 0;
+                if (restage) sdesc[d] = pa.desc[static_cast<size_t>(d1) * pa.nb2 + d];
+            }
+            staged = d1;
+            __syncthreads();
+            uint32_t cnt;   // codes of the tile, grouped into [0, cnt)
+            if constexpr (GMODE == 1) {
+                // ungrouped (measurement): the codes in load order
+                cnt = 0;
+#pragma unroll
+                for (int i = 0; i < ITEMS; i++) {
+                    const uint32_t e = wbase + i * 64 + lane;
+                    if ((vm >> i) & 1u) skey[e] = static_cast<int64_t>(hash64<HK>(static_cast<uint64_t>(key[i]), pa.seed));
+                }
+                cnt = __syncthreads_count((vm & 1u) != 0) * 0;   // (barrier)
+                TileLoc L;
+                locate_tile<T>(a, tile, L);
+                cnt = L.hi - L.lo;
+            } else if constexpr (GMODE == 2) {
+                // match ranking: lanes of a wave sharing a digit are ranked with
+                // ballots (no LDS atomics: no serialisation on hot digits), one
+                // counter row per wave, then a scan over (digit, wave)
+                uint32_t* wrow = cnt_d + nb + 16;   // [NW][nb]
+                constexpr int NW = BLOCK / 64;
+                uint32_t* my = wrow + wave * nb;
+                for (uint32_t d = lane; d < nb; d += 64) my[d] = 0;
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+                __builtin_amdgcn_wave_barrier();
+                uint32_t dig[ITEMS], rank[ITEMS];
+#pragma unroll
+                for (int i = 0; i < ITEMS; i++) {
+                    const uint64_t h = hash64<HK>(static_cast<uint64_t>(key[i]), pa.seed);
+                    key[i] = static_cast<int64_t>(h);
+                    const bool valid = (vm >> i) & 1u;
+                    const uint32_t d = static_cast<uint32_t>(q_from_hash(h, a.f) >> a.f.shift) & a.f.dmask;
+                    const uint64_t peers = match_digit(d, valid, a.nbits);
+                    dig[i] = d;
+                    rank[i] = 0;
+                    if (valid) {
+                        const uint32_t before = my[d];
+                        const uint64_t lt = peers & lanemask_lt();
+                        rank[i] = before + __popcll(lt);
+                        if (lt == 0) my[d] = before + __popcll(peers);
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+                    __builtin_amdgcn_wave_barrier();
+                }
+                __syncthreads();
+                {
+                    const uint32_t dpt = (nb + BLOCK - 1) / BLOCK, d0 = tid * dpt;
+                    uint32_t local = 0;
+                    for (uint32_t j = 0; j < dpt; j++)
+                        if (d0 + j < nb)
+#pragma unroll
+                            for (int w = 0; w < NW; w++) local += wrow[w * nb + d0 + j];
+                    uint32_t tot;
+                    uint32_t run = block_exclusive_scan_t<BLOCK / 64>(local, tmp, tot);
+                    cnt = tot;
+                    for (uint32_t j = 0; j < dpt; j++) {
+                        const uint32_t d = d0 + j;
+                        if (d < nb) {
+#pragma unroll
+                            for (int w = 0; w < NW; w++) {
+                                const uint32_t c = wrow[w * nb + d];
+                                wrow[w * nb + d] = run;
+                                run += c;
+                            }
+                        }
+                    }
+                }
+                __syncthreads();
+#pragma unroll
+                for (int i = 0; i < ITEMS; i++)
+                    if ((vm >> i) & 1u) skey[my[dig[i]] + rank[i]] = key[i];
+            } else {
+                uint32_t dig[ITEMS], rank[ITEMS];
+#pragma unroll
+                for (int i = 0; i < ITEMS; i++) {
+                    const uint64_t h = hash64<HK>(static_cast<uint64_t>(key[i]), pa.seed);
+                    key[i] = static_cast<int64_t>(h);
+                    dig[i] = static_cast<uint32_t>(q_from_hash(h, a.f) >> a.f.shift) & a.f.dmask;
+                    if ((vm >> i) & 1u) rank[i] = atomicAdd(&cnt_d[dig[i]], 1u);
+                }
+                __syncthreads();
+                {
+                    const uint32_t dpt = (nb + BLOCK - 1) / BLOCK, d0 = tid * dpt;
+                    uint32_t local = 0;
+                    for (uint32_t j = 0; j < dpt; j++)
+                        if (d0 + j < nb) local += cnt_d[d0 + j];
+                    uint32_t tot;
+                    uint32_t run = block_exclusive_scan_t<BLOCK / 64>(local, tmp, tot);
+                    cnt = tot;
+                    for (uint32_t j = 0; j < dpt; j++) {
+                        const uint32_t d = d0 + j;
+                        if (d < nb) {
+                            const uint32_t c = cnt_d[d];
+                            cnt_d[d] = run;
+                            run += c;
+                        }
+                    }
+                }
+                __syncthreads();
+#pragma unroll
+                for (int i = 0; i < ITEMS; i++)
+                    if ((vm >> i) & 1u) skey[cnt_d[dig[i]] + rank[i]] = key[i];
+            }
+            // the next tile's keys go out now, into the same registers
+            const uint32_t next = tile + g8;
+            uint32_t nvm = 0, nd1 = 0;
+            load(next < t_hi ? next : tile, nvm, nd1);
+            __syncthreads();
+            // E of partition (d1, d2): 1 for partition 0 only, else 0
+            const uint32_t e0 = d1 == 0 ? 1u : 0u;
+            const ulonglong2* tab2 = reinterpret_cast<const ulonglong2*>(pa.table);
+#pragma unroll
+            for (int i0 = 0; i0 < ITEMS; i0 += PB) {
+                uint64_t c[PB];
+                ulonglong2 v[PB];
+                uint32_t base[PB], bmask[PB], b[PB], ebits = 0, pend = 0;
+#pragma unroll
+                for (int i = 0; i < PB; i++) {
+                    const uint32_t k = (i0 + i) * BLOCK + tid;
+                    c[i] = 0;
+                    base[i] = 0;
+                    bmask[i] = 0;
+                    b[i] = 0;
+                    if (k < cnt) {
+                        c[i] = static_cast<uint64_t>(skey[k]);
+                        const uint32_t d2 = static_cast<uint32_t>(q_from_hash(c[i], a.f) >> a.f.shift) & a.f.dmask;
+                        const uint2 ds = sdesc[d2];
+                        base[i] = ds.x >> 1;   // bucket index of the table
+                        bmask[i] = ds.y;
+                        ebits |= (d2 == 0 ? e0 : 0u) << i;
+                        b[i] = static_cast<uint32_t>(c[i] >> kHtBucketShift) & bmask[i];
+                        pend |= 1u << i;
+                    }
+                }
+                if constexpr (DIAG) {   // measurement only: no table reads
+                    hits += __popc(pend);
+                    pend = 0;
+                }
+                // every pending probe reads its next bucket, all loads in flight together
+                while (pend) {
+#pragma unroll
+                    for (int i = 0; i < PB; i++)
+                        if ((pend >> i) & 1u) v[i] = tab2[base[i] + b[i]];
+#pragma unroll
+                    for (int i = 0; i < PB; i++) {
+                        if ((pend >> i) & 1u) {
+                            const uint64_t e = (ebits >> i) & 1u;
+                            const bool hit = v[i].x == c[i] || v[i].y == c[i];
+                            if (hit || v[i].y == e) {   // a match, or a bucket with an empty slot
+                                hits += hit ? 1u : 0u;
+                                pend &= ~(1u << i);
+                            } else {
+                                b[i] = (b[i] + 1u) & bmask[i];
+                            }
+                        }
+                    }
+                }
+            }
+            if (next >= t_hi) break;
+            tile = next;
+            vm = nvm;
+            d1 = nd1;
+            __syncthreads();   // LDS reads of this tile before the next tile's counts
+        }
+    }
+    uint32_t x = hits;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_down(x, o, 64);
+    if (lane == 0) red[wave] = x;
+    __syncthreads();
+    if (tid == 0) {
+        unsigned long long t = 0;
+        for (int w = 0; w < BLOCK / 64; w++) t += red[w];
+        if (t) atomicAdd(pa.count, t);
+    }
+}
+
+
+__host__ __device__ constexpr size_t probe_ht2_lds_bytes(int T, uint32_t nb) {
+    return static_cast<size_t>(T) * 8 + static_cast<size_t>(nb) * 2 * 12 + 64;
+}
+
+// The probe loop with three barriers per tile: rank (aggregated LDS atomics)
+// | B1 | wave 0 scans the counts | B2 | scatter into skey, issue the next
+// tile's loads, clear the other counter row and stage the other descriptor
+// buffer for the next tile's d1 | B3 | probe. Counters and descriptors are
+// double-buffered, so the next tile's ranking may start while slower waves
+// still probe this one (its scatter waits behind the next B1 / B2, which every
+// wave reaches only after its probe).
+template <int BLOCK, int ITEMS, int HK, int PBN = 2, int WPE = 6, bool DIAG = false, bool ALL = false>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void k_probe_ht2(HtProbeArgs pa) {
+    constexpr int T = BLOCK * ITEMS;
+    constexpr int PB = PBN;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const PassArgs& a = pa.a;
+    const uint32_t nb = a.nbins;
+    int64_t* skey = reinterpret_cast<int64_t*>(smem);
+    uint2* sdesc = reinterpret_cast<uint2*>(skey + T);             // [2][nb]
+    uint32_t* cntb = reinterpret_cast<uint32_t*>(sdesc + 2 * nb);   // [2][nb]
+    __shared__ uint32_t red[BLOCK / 64];
+    __shared__ uint32_t tot_s;
+
+    const uint32_t total = a.tile_base[a.nseg];
+    const uint32_t xcd = blockIdx.x & 7u, g8 = gridDim.x >> 3;
+    const uint32_t t_lo = static_cast<uint32_t>(static_cast<uint64_t>(total) * xcd / 8);
+    const uint32_t t_hi = static_cast<uint32_t>(static_cast<uint64_t>(total) * (xcd + 1) / 8);
+    uint32_t tile = t_lo + (blockIdx.x >> 3);
+    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    uint32_t hits = 0;
+    if (tile < t_hi) {   // block-uniform
+        const uint32_t wbase = wave * 64 * ITEMS;
+        const longlong2* rel = reinterpret_cast<const longlong2*>(a.in_keys);
+        const bool soa = a.in_pays != nullptr || a.keys_only;
+        int64_t key[ITEMS];
+        uint32_t vm = 0, d1 = 0;
+        auto load = [&](uint32_t t, uint32_t& m, uint32_t& d) {
+            d = a.tile_seg[t];
+            m = 0;
+            TileLoc L;
+            locate_tile<T>(a, t, L);
+            const uint32_t c = L.hi - L.lo;
+#pragma unroll
+            for (int i = 0; i < ITEMS; i++) {
+                const uint32_t e = wbase + i * 64 + lane;
+                key[i] = e < c ? (soa ? a.in_keys[L.lo + e] : rel[L.lo + e].x) : 0;
+                m |= e < c ? (1u << i) : 0u;
+            }
+        };
+        auto stage = [&](uint32_t buf, uint32_t dd) {
+            for (uint32_t d = tid; d < nb; d += BLOCK) sdesc[buf * nb + d] = pa.desc[static_cast<size_t>(dd) * pa.nb2 + d];
+        };
+        load(tile, vm, d1);
+        uint32_t sd[2] = {d1, 0xffffffffu};   // d1 staged in each descriptor buffer
+        stage(0, d1);
+        for (uint32_t d = tid; d < nb; d += BLOCK) cntb[d] = 0;
+        __syncthreads();
+        uint32_t buf = 0;
+        for (;;) {
+            uint32_t* C = cntb + buf * nb;
+            const uint2* D = sdesc + buf * nb;
+            uint32_t dig[ITEMS], rank[ITEMS];
+#pragma unroll
+            for (int i = 0; i < ITEMS; i++) {
+                const uint64_t h = hash64<HK>(static_cast<uint64_t>(key[i]), pa.seed);
+                key[i] = static_cast<int64_t>(h);
+                dig[i] = static_cast<uint32_t>(q_from_hash(h, a.f) >> a.f.shift) & a.f.dmask;
+                rank[i] = agg_rank(C, dig[i], (vm >> i) & 1u);
+            }
+            __syncthreads();   // B1
+            if (wave == 0) {   // exclusive scan of the counts by one wave
+                const uint32_t per = (nb + 63) / 64, d0 = lane * per;
+                uint32_t local = 0;
+                for (uint32_t j = 0; j < per; j++)
+                    if (d0 + j < nb) local += C[d0 + j];
+                uint32_t x = local;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const uint32_t y = __shfl_up(x, o, 64);
+                    if (lane >= static_cast<uint32_t>(o)) x += y;
+                }
+                uint32_t run = x - local;
+                for (uint32_t j = 0; j < per; j++)
+                    if (d0 + j < nb) {
+                        const uint32_t c = C[d0 + j];
+                        C[d0 + j] = run;
+                        run += c;
+                    }
+                if (lane == 63) tot_s = x;
+            }
+            __syncthreads();   // B2
+            const uint32_t cnt = tot_s;
+#pragma unroll
+            for (int i = 0; i < ITEMS; i++)
+                if ((vm >> i) & 1u) skey[C[dig[i]] + rank[i]] = key[i];
+            const uint32_t next = tile + g8;
+            const bool more = next < t_hi;
+            uint32_t nvm = 0, nd1 = d1;
+            if (more) load(next, nvm, nd1);
+            // the next tile's counter row and descriptors
+            const uint32_t ob = buf ^ 1u;
+            for (uint32_t d = tid; d < nb; d += BLOCK) cntb[ob * nb + d] = 0;
+            if (more && sd[ob] != nd1) {
+                stage(ob, nd1);
+                sd[ob] = nd1;
+            }
+            __syncthreads();   // B3
+            const uint32_t e0 = d1 == 0 ? 1u : 0u;   // E of partition (d1, d2): 1 only for partition 0
+            const ulonglong2* tab2 = reinterpret_cast<const ulonglong2*>(pa.table);
+            if constexpr (ALL) {
+                // every item's home bucket requested at once (only the 16-B
+                // buckets stay in registers; codes and descriptors are re-read
+                // from LDS), then the rare items whose home bucket is full
+                // without a match walk on one bucket at a time
+                ulonglong2 v[ITEMS];
+#pragma unroll
+                for (int i = 0; i < ITEMS; i++) {
+                    const uint32_t k = i * BLOCK + tid;
+                    v[i] = make_ulonglong2(0, 0);
+                    if (k < cnt) {
+                        const uint64_t c = static_cast<uint64_t>(skey[k]);
+                        const uint32_t d2 = static_cast<uint32_t>(q_from_hash(c, a.f) >> a.f.shift) & a.f.dmask;
+                        const uint2 ds = D[d2];
+                        v[i] = tab2[(ds.x >> 1) + (static_cast<uint32_t>(c >> kHtBucketShift) & ds.y)];
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < ITEMS; i++) {
+                    const uint32_t k = i * BLOCK + tid;
+                    if (k < cnt) {
+                        const uint64_t c = static_cast<uint64_t>(skey[k]);
+                        bool hit = v[i].x == c || v[i].y == c;
+                        const uint32_t d2 = static_cast<uint32_t>(q_from_hash(c, a.f) >> a.f.shift) & a.f.dmask;
+                        const uint64_t e = d2 == 0 ? e0 : 0u;
+                        if (!hit && v[i].y != e) {   // home bucket full, no match: walk on
+                            const uint2 ds = D[d2];
+                            uint32_t b = static_cast<uint32_t>(c >> kHtBucketShift) & ds.y;
+                            for (;;) {
+                                b = (b + 1) & ds.y;
+                                const ulonglong2 w = tab2[(ds.x >> 1) + b];
+                                hit = w.x == c || w.y == c;
+                                if (hit || w.y == e) break;
+                            }
+                        }
+                        hits += hit ? 1u : 0u;
+                    }
+                }
+            }
+#pragma unroll
+            for (int i0 = 0; i0 < (ALL ? 0 : ITEMS); i0 += PB) {
+                uint64_t c[PB];
+                ulonglong2 v[PB];
+                uint32_t base[PB], bmask[PB], b[PB], ebits = 0, pend = 0;
+#pragma unroll
+                for (int i = 0; i < PB; i++) {
+                    const uint32_t k = (i0 + i) * BLOCK + tid;
+                    c[i] = 0;
+                    base[i] = 0;
+                    bmask[i] = 0;
+                    b[i] = 0;
+                    if (k < cnt) {
+                        c[i] = static_cast<uint64_t>(skey[k]);
+                        const uint32_t d2 = static_cast<uint32_t>(q_from_hash(c[i], a.f) >> a.f.shift) & a.f.dmask;
+                        const uint2 ds = D[d2];
+                        base[i] = ds.x >> 1;
+                        bmask[i] = ds.y;
+                        ebits |= (d2 == 0 ? e0 : 0u) << i;
+                        b[i] = static_cast<uint32_t>(c[i] >> kHtBucketShift) & bmask[i];
+                        pend |= 1u << i;
+                    }
+                }
+                if constexpr (DIAG) {
+                    hits += __popc(pend);
+                    pend = 0;
+                }
+                while (pend) {
+#pragma unroll
+                    for (int i = 0; i < PB; i++)
+                        if ((pend >> i) & 1u) v[i] = tab2[base[i] + b[i]];
+#pragma unroll
+                    for (int i = 0; i < PB; i++) {
+                        if ((pend >> i) & 1u) {
+                            const uint64_t e = (ebits >> i) & 1u;
+                            const bool hit = v[i].x == c[i] || v[i].y == c[i];
+                            if (hit || v[i].y == e) {
+                                hits += hit ? 1u : 0u;
+                                pend &= ~(1u << i);
+                            } else {
+                                b[i] = (b[i] + 1u) & bmask[i];
+                            }
+                        }
+                    }
+                }
+            }
+            if (!more) break;
+            tile = next;
+            vm = nvm;
+            d1 = nd1;
+            buf = ob;
+        }
+    }
+    uint32_t x = hits;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_down(x, o, 64);
+    if (lane == 0) red[wave] = x;
+    __syncthreads();
+    if (tid == 0) {
+        unsigned long long t = 0;
+        for (int w = 0; w < BLOCK / 64; w++) t += red[w];
+        if (t) atomicAdd(pa.count, t);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Test hook (phj_probe_pass1): the pass-1 tiles the probe consumes,
+// concatenated in tile order. cnt[t] = keys of tile t (0 past the last tile);
+// after an exclusive scan, k_gather_pass1 copies tile t to out[off[t], ...).
+// ---------------------------------------------------------------------------
+template <int T>
+__global__ __launch_bounds__(256) void k_tile_counts(PassArgs a, uint32_t nt, uint32_t* cnt) {
+    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+    if (t > nt) return;
+    TileLoc L;
+    cnt[t] = (t < nt && locate_tile<T>(a, t, L)) ? L.hi - L.lo : 0u;
+}
+
+template <int T>
+__global__ __launch_bounds__(256) void k_gather_pass1(PassArgs a, const uint32_t* off, int64_t* out) {
+    TileLoc L;
+    if (!locate_tile<T>(a, blockIdx.x, L)) return;
+    const bool soa = a.in_pays != nullptr || a.keys_only;
+    const longlong2* rel = reinterpret_cast<const longlong2*>(a.in_keys);
+    int64_t* o = out + off[blockIdx.x];
+    for (uint32_t e = threadIdx.x; e < L.hi - L.lo; e += 256) o[e] = soa ? a.in_keys[L.lo + e] : rel[L.lo + e].x;
+}
+
+}  // namespace phj

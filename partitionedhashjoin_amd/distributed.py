@@ -30,13 +30,16 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import Context, comm_unique_id, CTX_EXCHANGE
-from . import shard_range as _lib_shard_range
 
 
 def shard_range(n: int, rank: int, world: int):
-    """Rows [lo, hi) of an n-row relation held by `rank` (phj_shard_range: the
-    range sharding every multi-device context applies)."""
-    return _lib_shard_range(n, rank, world)
+    """Rows [lo, hi) of an n-row relation held by `rank`: the range sharding
+    every multi-device context applies (phj_shard_range, csrc/phj_group.h
+    shard_range; tests/test_distributed.py pins the two together). Pure Python,
+    so the CPU rehearsal needs no HIP runtime."""
+    if not 0 <= rank < world:
+        return (0, 0)
+    return ((n * rank) // world, (n * (rank + 1)) // world)
 
 
 def max_shard(n: int, world: int) -> int:

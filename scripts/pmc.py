@@ -30,7 +30,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 FAMILIES = [
     (re.compile(r"\.hist$"), re.compile(r"phj::k_hist")),
     (re.compile(r"\.scatter$"), re.compile(r"phj::k_scatter")),
-    (re.compile(r"^build$"), re.compile(r"phj::k_(build_small|join_fused)")),
+    (re.compile(r"^build$"), re.compile(r"phj::k_(build_small|build_ht|join_fused)")),
     (re.compile(r"^probe$"), re.compile(r"phj::k_(probe|join_fused)")),
     (re.compile(r"^np\.build$"), re.compile(r"phj::k_np_build(?!_overflow)")),
     (re.compile(r"^np\.probe$"), re.compile(r"phj::k_np_probe")),

@@ -136,6 +136,11 @@ def test_library_shard_range_is_the_documented_split():
             for r in range(w):
                 assert phj.shard_range(n, r, w) == ((n * r) // w, (n * (r + 1)) // w)
     assert phj.shard_range(10, 3, 2) == (0, 0)   # out of range rank: empty
+    # the pure-Python helper of the CPU rehearsal is the same split
+    for n in (0, 1, 7, 10_000_000, 2**40 + 3):
+        for w in (1, 3, 8):
+            for r in range(w + 1):
+                assert shard_range(n, r, w) == phj.shard_range(n, r, w)
 
 
 def test_shard_ranges_cover_exactly():

@@ -21,7 +21,7 @@ CLI = os.path.join(PKG, "phjoin")
 def header_symbols():
     with open(os.path.join(ROOT, "include", "phj.h")) as f:
         text = f.read()
-    return sorted(set(re.findall(r"\b(phj_[a-z_]+)\s*\(", text)))
+    return sorted(set(re.findall(r"\b(phj_[a-z0-9_]+)\s*\(", text)))
 
 
 def test_library_exports_every_declared_symbol():
