@@ -54,7 +54,6 @@ struct Tuning {
     bool nt_store = false; // nontemporal scatter stores
     int nt_load = 1;       // nontemporal tuple loads in the partition passes: 1 pass 1, 2 both
     bool dcol = true;     // 2-pass: pass 1 writes the pass-2 digit column
-    unsigned ev_flags = hipEventDisableSystemFence;  // timer / ordering events
     bool fused = true;    // radix join: fused per-partition LDS build + probe when partitions are small
     int onepass_max = 256; // hash % P: largest P partitioned in one pass
     int ptab = 1;         // partitioned bucket tables: 0 never, 1 very large partitions, 2 always
@@ -63,7 +62,7 @@ struct Tuning {
     int fused_kpl = 4;    // fused join: S keys per lane per probe round (2, 4 or 8)
     bool p1_chunk = true; // 2-pass, unordered partitions: chunked pass 1 without a histogram pass
     int p1_slots = 0;     // chunked pass 1: workgroups per shard (0 = fill the chip once, -1 = one per tile)
-    int p1_wpc2 = 3;      // ... keys-only: workgroups per CU x 2 (0 = fill the chip once)
+    int p1_wpc2 = 2;      // ... keys-only: workgroups per CU x 2 (0 = fill the chip once)
     int p1_tps = static_cast<int>(kTilesPerShard);   // chunked pass 1: tiles per shard (sets the shard count)
     int p1_min_tiles = 32768;  // chunked pass 1: smallest relation (in 4096-tuple tiles, ~134M tuples)
     int p1_ko_tps = 1024;      // ... the keys-only form for the counting probe: tiles per shard
@@ -74,16 +73,10 @@ struct Tuning {
     int np_hot = 1;          // NoPartitioning probe: hot-key LDS cache (0 off, 1 from np_hot_min probes)
     uint64_t np_hot_min = 1u << 20;
     uint32_t np_hot_samples = 65536;
-    int np_diag = 0;         // PHJ_NP_DIAG: diagnostic probe floors (timing only, wrong counts)
-    int np_coop = 0;         // NoPartitioning probe: four lanes per bucket (k_np_probe_coop; measured slower)
-    int p2probe = 1;         // radix join, 2 passes: the probe side's pass 2 on-chip (k_probe_p1)
-    int p1_priv = 0;
-    int p1_bits = 0;
-    int p1_home = 1;         // on-chip probe reads one 16-B home slot per key (k_csr_home)
-    int p1_bshift = 0;       // CSR tables of the on-chip probe: buckets x 2^bshift
-    int p1_ko = 1;           // chunked pass 1 consumed by the counting probe: keys only (k_scatter_chunked VAR 5)
-    int p1_hcode = 1;        // ... written as hash codes; the CSR tables hold codes, the probe never hashes (VAR 13)
-    double np_ratio = kNPDefaultRatio;   // NoPartitioning: slots per build tuple when the params leave it 0         // 2-pass join: pass-1 digit bits (0: the plan's split; rebalance_plan)         // pass 1 consumed on chip: workgroup-private chains (k_scatter_priv)
+    int p2probe = 1;         // radix join, 2 passes: the probe side's pass 2 on-chip (k_probe_ht)
+    int p1_ko = 1;           // chunked pass 1 consumed by the on-chip probe: keys only (k_scatter_chunked VAR 5)
+    int p1_hcode = 1;        // ... written as hash codes, so the probe never hashes (VAR 13)
+    double np_ratio = kNPDefaultRatio;   // NoPartitioning: slots per build tuple when the params leave it 0
     int p1_var = 3;          // chunked pass 1 variant (k_scatter_chunked VAR: 1 atomic rank, 2 tuple LDS)
 };
 
@@ -125,9 +118,6 @@ struct SideState {
     DevBuf hist1, hist2, bounds1, tbase2, tseg2, bounds, partials;
     DevBuf dig;           // pass-2 digit column written by pass 1
     DevBuf ccur, ctab, tstart;   // chunked pass 1: digit cursors + pool counter, chunk table, pass-2 tile starts
-    DevBuf priv;                 // private-chain pass 1: chunk logs, chain states, chunk lists (k_scatter_priv)
-    const uint32_t* p2_ent = nullptr;     // ... the probe's chunk list and its per-digit offsets
-    const uint32_t* p2_ebase = nullptr;
     uint32_t gen = 0;            // chunked pass 1: tag of the current chunk-table entries
     bool hcoded = false;         // the last pass 1 wrote hash codes (keys only, PHJ_P1_HCODE)
     phj_partitioned view{};
@@ -159,11 +149,6 @@ struct phj_ctx {
     int device = 0;
     hipStream_t stream = nullptr;  // the ctx stream (own or borrowed)
     hipStream_t aux = nullptr;     // ctx-owned: R-side partitioning runs here beside S
-    // PHJ_CU_SPLIT=k: CU-masked streams for the single-device on-chip join, k
-    // CUs of every 32 for R's chain (partition + tables), the rest for S's
-    // pass 1, so R is not starved behind S's persistent workgroups
-    hipStream_t r_split = nullptr, s_split = nullptr;
-    int s_split_cus = 0;
     hipStream_t ks = nullptr;      // stream the current launches go to (stream or aux)
     DevBuf* scan_scratch = nullptr; // scan partials of the side being partitioned
     int num_cus = 256;
@@ -226,8 +211,6 @@ int ensure(phj_ctx* c, DevBuf& b, size_t bytes) {
     if (b.p) {
         PHJ_HIP(c, hipStreamSynchronize(c->stream));
         PHJ_HIP(c, hipStreamSynchronize(c->aux));
-        if (c->r_split) PHJ_HIP(c, hipStreamSynchronize(c->r_split));
-        if (c->s_split) PHJ_HIP(c, hipStreamSynchronize(c->s_split));
         PHJ_HIP(c, hipFree(b.p));
         b.p = nullptr;
         b.bytes = 0;
@@ -254,7 +237,7 @@ hipEvent_t next_event(phj_ctx* c) {
         // timing / same-device ordering only: no system-scope fence (a default
         // event's system-scope writeback costs ~10 us per record); the first
         // flag set the runtime accepts is used
-        const unsigned tries[3] = {c->tune.ev_flags, hipEventReleaseToDevice, hipEventDefault};
+        const unsigned tries[3] = {hipEventDisableSystemFence, hipEventReleaseToDevice, hipEventDefault};
         for (unsigned f : tries) {
             if (hipEventCreateWithFlags(&e, f) == hipSuccess) break;
             (void)hipGetLastError();
@@ -445,32 +428,7 @@ void refine_plan_sub(const phj_ctx* c, Plan& pl, uint64_t nR) {
     pl.Ppad = pl.nb1 * pl.nb2;
 }
 
-// Pass split of a 2-pass join plan (PHJ_P1_BITS = b > 0): pass 1 on the top
-// b bits of q, pass 2 on the rest. The final partitions (q) are the same;
-// fewer pass-1 digits give the private-chain pass 1 longer runs per tile
-// (fewer partial 64-B segments) and the on-chip probe more digits to group.
-void rebalance_plan(const phj_ctx* c, Plan& pl) {
-    const int b1 = c->tune.p1_bits;
-    if (b1 <= 0 || pl.npass != 2) return;
-    const uint64_t range = pl.sub_bits == 0 && pl.mode == 0 ? (1ull << (pl.bits1 + pl.bits2))
-                           : (pl.mode == 0 ? (1ull << ceil_log2(pl.P)) : pl.P) << pl.sub_bits;
-    const uint32_t tot = ceil_log2(range);
-    if (static_cast<uint32_t>(b1) >= tot || tot - b1 > static_cast<uint32_t>(kMaxDigitBits)) return;
-    const uint32_t b2 = tot - b1;
-    pl.nb2 = 1u << b2;
-    pl.bits2 = b2;
-    pl.dmask2 = pl.nb2 - 1;
-    pl.shift1 = b2;
-    pl.nb1 = static_cast<uint32_t>((range + pl.nb2 - 1) / pl.nb2);
-    pl.bits1 = ceil_log2(pl.nb1);
-    pl.dmask1 = 0xffffffffu;
-    pl.Ppad = pl.nb1 * pl.nb2;
-}
-
-void refine_plan(const phj_ctx* c, Plan& pl, uint64_t nR) {
-    refine_plan_sub(c, pl, nR);
-    rebalance_plan(c, pl);
-}
+void refine_plan(const phj_ctx* c, Plan& pl, uint64_t nR) { refine_plan_sub(c, pl, nR); }
 
 DigitFn digit_fn(const Plan& pl, int pass) {
     DigitFn f{};
@@ -542,7 +500,7 @@ int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const st
             if (c->tune.p1_slots > 0) slots = std::min<uint32_t>(per, c->tune.p1_slots);
             if (c->tune.p1_slots < 0) slots = per;   // one tile per workgroup
             const void* kfn = nullptr;
-            switch (a.keys_only ? (c->tune.p1_hcode ? 13 : 5) : (c->tune.p1_var & 3)) {
+            switch (a.keys_only ? (c->tune.p1_hcode ? (env_int("PHJ_P1_NOCLAIM", 0) ? 29 : 13) : 5) : (c->tune.p1_var & 3)) {
 #define PHJ_P1_VARIANT(V)                                                                            \
     case V:                                                                                          \
         kfn = hk == kMurmur3 ? reinterpret_cast<const void*>(&k_scatter_chunked<BLOCK, ITEMS, kMurmur3, V>) \
@@ -554,6 +512,7 @@ int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const st
                 PHJ_P1_VARIANT(3)
                 PHJ_P1_VARIANT(5)
                 PHJ_P1_VARIANT(13)
+                PHJ_P1_VARIANT(29)
 #undef PHJ_P1_VARIANT
             }
             PassArgs ak = a;
@@ -728,22 +687,6 @@ int partition_side(phj_ctx* c, int s, const Plan& pl, bool p1_only = false) {
     const bool dcol = pl.npass == 2 && c->tune.dcol && !wc1 && !wc2 && !p1_only;
     const uint32_t dbytes = pl.bits2 > 8 ? 2 : 1;
     const char* tag = s == PHJ_SIDE_BUILD ? "R" : "S";
-    // Pass 1 into workgroup-private chains of 64-slot chunks when the on-chip
-    // probe consumes it (k_scatter_priv): no histogram pass and no claims that
-    // leave the CU; the probe reads a chunk list. Persistent workgroups (two
-    // per CU, what the LDS allows), each a contiguous run of `pper` tiles.
-    const uint32_t pblock = static_cast<uint32_t>(tile_shape(c, pl.nb1).block);
-    uint32_t pG = 0, pper = 0, prch = 0;
-    bool priv = p1_only && pl.npass == 2 && !pl.stable && c->tune.p1_priv && p1_aos && !wc1 && !wc2 && n > 0 &&
-                tile == 4096 && tile2 == 4096 && pblock == 512 && pl.nb1 <= pblock;
-    if (priv) {
-        const uint32_t fit = std::max<uint32_t>(1, static_cast<uint32_t>(160 * 1024 / scatter_priv_lds_bytes(4096, pl.nb1)));
-        pG = std::min<uint32_t>(nt1, fit * c->num_cus);
-        pper = (nt1 + pG - 1) / pG;
-        pG = (nt1 + pper - 1) / pper;   // no workgroup without tiles
-        prch = pper * (tile / kPrivCh) + pl.nb1;
-        priv = static_cast<uint64_t>(pG) * prch * kPrivCh < (1ull << 32) - 64;
-    }
     // Chunked pass 1 (unordered partitions, tile kernels): pass-1 chunks are
     // the pass-2 tiles, every digit's run of a tile fits one workgroup thread
     // (nb1 <= block) and spans at most two chunks (tile1 == tile2).
@@ -754,7 +697,7 @@ int partition_side(phj_ctx* c, int s, const Plan& pl, bool p1_only = false) {
     // form for the on-chip probe (half the bytes, three workgroups per CU)
     // wins at every size measured (25M-200M), with shards of p1_ko_tps tiles.
     const bool ko = p1_only && c->tune.p1_ko;
-    const bool chunked = !priv && pl.npass == 2 && !pl.stable && c->tune.p1_chunk && (dcol || p1_only) && p1_aos && n > 0 &&
+    const bool chunked = pl.npass == 2 && !pl.stable && c->tune.p1_chunk && (dcol || p1_only) && p1_aos && n > 0 &&
                          nt1 >= static_cast<uint32_t>(ko ? c->tune.p1_ko_min_tiles : c->tune.p1_min_tiles) &&
                          tile == tile2 && pl.nb1 <= static_cast<uint32_t>(tile_shape(c, pl.nb1).block) &&
                          tile / tile_shape(c, pl.nb1).block <= 8 &&   // registers: the next tile is prefetched
@@ -771,22 +714,14 @@ int partition_side(phj_ctx* c, int s, const Plan& pl, bool p1_only = false) {
     const uint32_t per = (nt1 + nshards - 1) / nshards;
     const uint32_t pool_stride = 3 * per + pl.nb1;
     const uint32_t maxch = per + 1;   // chunks of one chain (every tuple of a shard in one digit)
-    const size_t slots1 = priv ? static_cast<size_t>(pG) * prch * kPrivCh
-                               : chunked ? static_cast<size_t>(nshards) * pool_stride * tile : n;
-    // pass-2 tiles (bound): one partial tile per segment, or per chain when
-    // chunked; private chains: 64 chunks per tile, one partial tile per digit
-    const uint32_t nt2 = pl.npass != 2 ? 0
-                         : priv ? static_cast<uint32_t>((static_cast<uint64_t>(pG) * prch + 63) / 64) + pl.nb1
-                                : (n + tile2 - 1) / tile2 + pl.nb1 * (chunked ? nshards : 1);
+    const size_t slots1 = chunked ? static_cast<size_t>(nshards) * pool_stride * tile : n;
+    // pass-2 tiles (bound): one partial tile per segment, or per chain when chunked
+    const uint32_t nt2 = pl.npass != 2 ? 0 : (n + tile2 - 1) / tile2 + pl.nb1 * (chunked ? nshards : 1);
     const uint32_t nt2max = nt2 + 8;
     // workspace (grow-only; allocation is outside the timed phases on reuse)
     PHJ_TRY(ensure(c, S.kA, slots1 * (p1_aos ? 16 : 8)));
     if (!p1_aos) PHJ_TRY(ensure(c, S.pA, static_cast<size_t>(n) * 8));
-    if (!chunked && !priv) PHJ_TRY(ensure(c, S.hist1, static_cast<size_t>(nt1) * pl.nb1 * 4));
-    // private chains (u32 words): log, ent [pG * prch]; ccount, clast, cfill,
-    // offw [pG * nb1]; nused [pG]; nch, ntup [nb1]; ebase [nb1 + 1]
-    const size_t pw_ch = static_cast<size_t>(pG) * prch, pw_cw = static_cast<size_t>(pG) * pl.nb1;
-    if (priv) PHJ_TRY(ensure(c, S.priv, (2 * pw_ch + 4 * pw_cw + pG + 3 * static_cast<size_t>(pl.nb1) + 1) * 4));
+    if (!chunked) PHJ_TRY(ensure(c, S.hist1, static_cast<size_t>(nt1) * pl.nb1 * 4));
     PHJ_TRY(ensure(c, S.bounds1, (static_cast<size_t>(pl.nb1) + 1) * 4));
     if (pl.npass == 2) {
         PHJ_TRY(ensure(c, S.kB, static_cast<size_t>(n) * 8));
@@ -810,7 +745,7 @@ int partition_side(phj_ctx* c, int s, const Plan& pl, bool p1_only = false) {
         }
     }
     if (c->dry) {   // scan scratch of both passes, then nothing is launched
-        if (!chunked && !priv) PHJ_TRY(scan_u32(c, nullptr, nt1 * pl.nb1, 1, nt1 * pl.nb1, c->scan_scratch));
+        if (!chunked) PHJ_TRY(scan_u32(c, nullptr, nt1 * pl.nb1, 1, nt1 * pl.nb1, c->scan_scratch));
         if (pl.npass == 2 && n) PHJ_TRY(scan_u32(c, nullptr, nt2 * pl.nb2, 1, nt2 * pl.nb2, c->scan_scratch));
         return PHJ_OK;
     }
@@ -848,51 +783,12 @@ int partition_side(phj_ctx* c, int s, const Plan& pl, bool p1_only = false) {
         a.gen = S.gen;
     }
     uint32_t* tb2 = pl.npass == 2 ? static_cast<uint32_t*>(S.tbase2.p) : nullptr;
-    uint32_t* pw = static_cast<uint32_t*>(S.priv.p);
-    PrivArgs q{};
-    if (priv) {
-        q.log = pw;
-        q.ccount = pw + 2 * pw_ch;
-        q.clast = q.ccount + pw_cw;
-        q.cfill = q.clast + pw_cw;
-        q.nused = q.cfill + 2 * pw_cw;   // after offw
-        q.rchunks = prch;
-        q.per = pper;
-        q.ntiles = nt1;
-        uint32_t* offw = q.cfill + pw_cw;
-        uint32_t* nch = q.nused + pG;
-        uint32_t* ntup = nch + pl.nb1;
-        uint32_t* ebase = ntup + pl.nb1;
-        uint32_t* ent = pw + pw_ch;
-        a.nt_load = c->tune.nt_load ? 1u : 0u;
-        const size_t lds = scatter_priv_lds_bytes(4096, pl.nb1);
-        PHJ_TRY(timer_begin(c, (std::string(tag) + ".p1.scatter").c_str(), static_cast<uint64_t>(n) * 32));
-        const void* kfn = pl.hk == kMurmur3 ? reinterpret_cast<const void*>(&k_scatter_priv<512, 8, kMurmur3>)
-                                            : reinterpret_cast<const void*>(&k_scatter_priv<512, 8, kXXH3>);
-        void* kargs[] = {&a, &q};
-        PHJ_HIP(c, hipLaunchKernel(kfn, dim3(pG), dim3(512), kargs, lds, c->ks));
-        PHJ_LAUNCHED(c, "k_scatter_priv");
-        PHJ_TRY(timer_end(c));
-        hipLaunchKernelGGL(k_priv_offsets, dim3(pl.nb1), dim3(kBlock), 0, c->ks, q.ccount, q.cfill, pG, pl.nb1, offw, nch,
-                           ntup);
-        PHJ_LAUNCHED(c, "k_priv_offsets");
-        hipLaunchKernelGGL(k_priv_finish, dim3(1), dim3(1024), 0, c->ks, nch, ntup, pl.nb1, ebase, tb2,
-                           static_cast<uint32_t*>(S.bounds1.p));
-        PHJ_LAUNCHED(c, "k_priv_finish");
-        hipLaunchKernelGGL(k_priv_list, dim3(static_cast<uint32_t>((pw_ch + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->ks,
-                           q.log, q.nused, q.clast, q.cfill, offw, ebase, pG, pl.nb1, prch, ent);
-        PHJ_LAUNCHED(c, "k_priv_list");
-        S.p2_ent = ent;
-        S.p2_ebase = ebase;
-    } else if (wc1) {
+    if (wc1) {
         PHJ_TRY(launch_pass_wc(c, pl.hk, true, a, nt1, tile, std::string(tag) + ".p1", n, nt1 * pl.nb1));
     } else {
         PHJ_TRY(launch_pass(c, pl.hk, true, p1_aos, a, nt1, std::string(tag) + ".p1", n, nt1 * pl.nb1));
     }
-    if (!priv) S.p2_ent = S.p2_ebase = nullptr;
-    if (priv) {
-        // bounds1 / tile_base2 written by k_priv_finish
-    } else if (chunked) {
+    if (chunked) {
         hipLaunchKernelGGL(k_pass1_finish_sizes, dim3(1), dim3(1024), 0, c->ks, a.chunk_cursor, pl.nb1, nshards, n, tile2,
                            static_cast<uint32_t*>(S.bounds1.p), tb2);
         PHJ_LAUNCHED(c, "k_pass1_finish_sizes");
@@ -928,7 +824,7 @@ int partition_side(phj_ctx* c, int s, const Plan& pl, bool p1_only = false) {
                 PHJ_LAUNCHED(c, "k_tile_chunks");
                 b.tile_start = ts;
                 b.tile_cnt = tc;
-            } else {   // stable layout or private chains: tile -> digit
+            } else {   // stable layout: tile -> digit
                 hipLaunchKernelGGL(k_tile_seg, dim3((pl.nb1 + kWaves - 1) / kWaves), dim3(kBlock), 0, c->ks, tb2,
                                    pl.nb1, static_cast<uint32_t*>(S.tseg2.p));
                 PHJ_LAUNCHED(c, "k_tile_seg");
@@ -1347,7 +1243,7 @@ bool use_p2probe(const phj_ctx* c, const Plan& pl, uint64_t nS, uint64_t nR) {
     bool wc = false;
     return c->tune.p2probe && pl.npass == 2 && tile_shape(c, pl.nb2).tile == 4096 && tile_shape(c, pl.nb2).block == 512 &&
            pass_tile(c, static_cast<uint32_t>(std::min<uint64_t>(nS, 0xffffffffu)), pl.nb1, &wc) == 4096 && !wc &&
-           probe_ht_lds_bytes(4096, pl.nb2) <= 160 * 1024 &&
+           probe_ht_lds_bytes(kProbeBlock * kProbeItems, pl.nb2) <= 160 * 1024 &&
            4 * nR + 2ull * pl.Ppad < (1ull << 32);
 }
 
@@ -1364,41 +1260,21 @@ int probe_ht(phj_ctx* c, const Plan& pl) {
     pa.count = static_cast<unsigned long long*>(c->count.p);
     pa.seed = pl.seed;
     pa.nb2 = pl.nb2;
-    const size_t lds = std::max(probe_ht_lds_bytes(4096, pl.nb2), probe_ht2_lds_bytes(4096, pl.nb2));
+    constexpr int B = kProbeBlock, I = kProbeItems;
+    const size_t lds = probe_ht_lds_bytes(B * I, pl.nb2);
     // a keys-only pass 1 wrote codes (VAR 13); a stable pass 1 left whole tuples
-    const void* kfn = PS.hcoded ? reinterpret_cast<const void*>(&k_probe_ht<512, 8, kHashed>)
-                      : pl.hk == kMurmur3 ? reinterpret_cast<const void*>(&k_probe_ht<512, 8, kMurmur3>)
-                                          : reinterpret_cast<const void*>(&k_probe_ht<512, 8, kXXH3>);
-    if (PS.hcoded) {   // TEMPORARY measurement variants (PHJ_HT_VAR)
-        switch (env_int("PHJ_HT_VAR", 0)) {
-            case 1: kfn = reinterpret_cast<const void*>(&k_probe_ht<512, 8, kHashed, 4, 6>); break;
-            case 2: kfn = reinterpret_cast<const void*>(&k_probe_ht<512, 8, kHashed, 2, 4>); break;
-            case 3: kfn = reinterpret_cast<const void*>(&k_probe_ht<512, 8, kHashed, 4, 4>); break;
-            case 4: kfn = reinterpret_cast<const void*>(&k_probe_ht<512, 8, kHashed, 2, 6, true>); break;
-            case 5: kfn = reinterpret_cast<const void*>(&k_probe_ht<512, 8, kHashed, 2, 8>); break;
-            case 6: kfn = reinterpret_cast<const void*>(&k_probe_ht<512, 8, kHashed, 2, 6, false, 1>); break;
-            case 7: kfn = reinterpret_cast<const void*>(&k_probe_ht<512, 8, kHashed, 2, 6, false, 2>); break;
-            case 8: kfn = reinterpret_cast<const void*>(&k_probe_ht<512, 8, kHashed, 4, 6, false, 1>); break;
-            case 9: kfn = reinterpret_cast<const void*>(&k_probe_ht<512, 8, kHashed, 2, 6, true, 2>); break;
-            case 10: kfn = reinterpret_cast<const void*>(&k_probe_ht2<512, 8, kHashed, 2, 6>); break;
-            case 11: kfn = reinterpret_cast<const void*>(&k_probe_ht2<512, 8, kHashed, 2, 6, true>); break;
-            case 12: kfn = reinterpret_cast<const void*>(&k_probe_ht2<512, 8, kHashed, 4, 4>); break;
-            case 13: kfn = reinterpret_cast<const void*>(&k_probe_ht2<512, 8, kHashed, 2, 8>); break;
-            case 14: kfn = reinterpret_cast<const void*>(&k_probe_ht2<512, 8, kHashed, 2, 6, false, true>); break;
-            case 15: kfn = reinterpret_cast<const void*>(&k_probe_ht2<512, 8, kHashed, 2, 8, false, true>); break;
-            case 16: kfn = reinterpret_cast<const void*>(&k_probe_ht2<512, 8, kHashed, 2, 5, false, true>); break;
-            default: break;
-        }
-    }
+    const void* kfn = PS.hcoded ? reinterpret_cast<const void*>(&k_probe_ht<B, I, kHashed>)
+                      : pl.hk == kMurmur3 ? reinterpret_cast<const void*>(&k_probe_ht<B, I, kMurmur3>)
+                                          : reinterpret_cast<const void*>(&k_probe_ht<B, I, kXXH3>);
     // persistent: as many workgroups as fit the chip at once (a multiple of 8:
     // XCD x owns tiles [x, x + 1) * ntiles / 8), never many more than tiles
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, 512, lds) != hipSuccess || per_cu < 1) per_cu = 2;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, B, lds) != hipSuccess || per_cu < 1) per_cu = 2;
     per_cu = std::min<int>(per_cu, static_cast<int>(160 * 1024 / lds));
     const uint32_t want = (PS.nt2 + 7) & ~7u;
     const uint32_t grid = std::max<uint32_t>(8, std::min<uint32_t>(want, static_cast<uint32_t>(per_cu) * c->num_cus) & ~7u);
     void* kargs[] = {&pa};
-    PHJ_HIP(c, hipLaunchKernel(kfn, dim3(grid), dim3(512), kargs, lds, c->ks));
+    PHJ_HIP(c, hipLaunchKernel(kfn, dim3(grid), dim3(B), kargs, lds, c->ks));
     PHJ_LAUNCHED(c, "k_probe_ht");
     return PHJ_OK;
 }
@@ -1547,31 +1423,7 @@ int join_nopart(phj_ctx* c, const phj_join_params* p, phj_join_result* r, uint32
             if (c->tune.np_nt == 2) PHJ_NP_PROBE(HKV, 4, 2); else if (c->tune.np_nt) PHJ_NP_PROBE(HKV, 4, 1); else PHJ_NP_PROBE(HKV, 4, 0); \
         }                                                                        \
     } while (0)
-        if (c->tune.np_diag == 4 && !marks) {
-            const uint32_t dg = static_cast<uint32_t>(std::min<uint64_t>((S.n + 256ull * kBlock - 1) / (256ull * kBlock), 8192));
-            hipLaunchKernelGGL((k_np_probe_coop<kXXH3, 4, 1, 4>), dim3(dg), dim3(kBlock), 0, c->ks, S_rel, S.n, tab, g, p->hash_seed, cnt);
-        } else if (c->tune.np_coop && !marks) {
-            // one round = 4 keys per lane; a workgroup of 4 waves takes 1024 keys
-            const uint64_t per = 4ull * kBlock;
-            const uint32_t cg = static_cast<uint32_t>(std::min<uint64_t>((S.n + per - 1) / per, 8192));
-            if (p->hash == PHJ_HASH_MURMUR3) {
-                if (c->tune.np_items == 8) hipLaunchKernelGGL((k_np_probe_coop<kMurmur3, 8, 1>), dim3(cg), dim3(kBlock), 0, c->ks, S_rel, S.n, tab, g, p->hash_seed, cnt);
-                else hipLaunchKernelGGL((k_np_probe_coop<kMurmur3, 4, 1>), dim3(cg), dim3(kBlock), 0, c->ks, S_rel, S.n, tab, g, p->hash_seed, cnt);
-            } else {
-                if (c->tune.np_items == 8) hipLaunchKernelGGL((k_np_probe_coop<kXXH3, 8, 1>), dim3(cg), dim3(kBlock), 0, c->ks, S_rel, S.n, tab, g, p->hash_seed, cnt);
-                else hipLaunchKernelGGL((k_np_probe_coop<kXXH3, 4, 1>), dim3(cg), dim3(kBlock), 0, c->ks, S_rel, S.n, tab, g, p->hash_seed, cnt);
-            }
-            if (hot) PHJ_HIP(c, hipStreamWaitEvent(c->ks, es, 0));
-        } else if (c->tune.np_diag >= 1 && c->tune.np_diag <= 3 && !marks) {
-            const uint32_t dg = static_cast<uint32_t>(std::min<uint64_t>((S.n + 4ull * kBlock - 1) / (4ull * kBlock), 8192));
-            if (c->tune.np_diag == 1)
-                hipLaunchKernelGGL((k_np_probe_diag<kXXH3, 1>), dim3(dg), dim3(kBlock), 0, c->ks, S_rel, S.n, tab, g, p->hash_seed, cnt);
-            else if (c->tune.np_diag == 2)
-                hipLaunchKernelGGL((k_np_probe_diag<kXXH3, 2>), dim3(dg), dim3(kBlock), 0, c->ks, S_rel, S.n, tab, g, p->hash_seed, cnt);
-            else
-                hipLaunchKernelGGL((k_np_probe_diag<kXXH3, 3>), dim3(dg), dim3(kBlock), 0, c->ks, S_rel, S.n, tab, g, p->hash_seed, cnt);
-            if (hot) PHJ_HIP(c, hipStreamWaitEvent(c->ks, es, 0));
-        } else if (hot) {
+        if (hot) {
             PHJ_HIP(c, hipStreamWaitEvent(c->ks, es, 0));
             auto* img_keys = static_cast<int64_t*>(c->np_img.p);
             auto* img_st = reinterpret_cast<uint8_t*>(img_keys + kHotSlots);
@@ -1745,13 +1597,7 @@ int ctx_create_device(int device, phj_ctx** out) {
         delete c;
         return PHJ_ERR_HIP;
     }
-    // PHJ_AUX_PRIO=1: the build side's stream (R partition, exchange, tables:
-    // the multi-GPU step's critical chain) at the highest priority, so its
-    // small kernels are dispatched ahead of S's pass-1 workgroups
-    int least = 0, greatest = 0;
-    const bool prio = env_int("PHJ_AUX_PRIO", 0) != 0 && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess;
-    if ((prio ? hipStreamCreateWithPriority(&c->aux, hipStreamNonBlocking, greatest)
-              : hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking)) != hipSuccess) {
+    if (hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess) {
         (void)hipStreamDestroy(c->stream);
         delete c;
         return PHJ_ERR_HIP;
@@ -1788,49 +1634,20 @@ int ctx_create_device(int device, phj_ctx** out) {
     c->tune.np_hot = env_int("PHJ_NP_HOT", 1);
     c->tune.np_hot_min = static_cast<uint64_t>(std::max(0, env_int("PHJ_NP_HOT_MIN", 1 << 20)));
     c->tune.np_hot_samples = static_cast<uint32_t>(std::max(256, env_int("PHJ_NP_HOT_SAMPLES", 65536)));
-    c->tune.np_diag = env_int("PHJ_NP_DIAG", 0);
-    c->tune.np_coop = env_int("PHJ_NP_COOP", 0);
     c->tune.p2probe = env_int("PHJ_P2PROBE", 1);
     c->tune.p1_var = env_int("PHJ_P1_VAR", 3) & 3;
-    // measured: 2.05 vs 1.47 ms at 200M; the private chains'
-    // partial 64-B segments are written separately (WRREQ 61M vs 52M)
-    c->tune.p1_priv = env_int("PHJ_P1_PRIV", 0);
-    c->tune.p1_bits = std::max(0, env_int("PHJ_P1_BITS", 0));
-    c->tune.p1_home = env_int("PHJ_P1_HOME", 1);
-    c->tune.p1_bshift = env_int("PHJ_P1_BSHIFT", 0);
     c->tune.p1_ko = env_int("PHJ_P1_KO", 1);
     c->tune.p1_hcode = env_int("PHJ_P1_HCODE", 1);
     if (const char* r = std::getenv("PHJ_NP_RATIO")) c->tune.np_ratio = std::max(1.0, std::atof(r));
     c->tune.p1_slots = env_int("PHJ_P1_SLOTS", 0);
-    c->tune.p1_wpc2 = std::max(0, env_int("PHJ_P1_WPC2", 3));
+    c->tune.p1_wpc2 = std::max(0, env_int("PHJ_P1_WPC2", 2));
     c->tune.p1_tps = std::max(1, env_int("PHJ_P1_TPS", static_cast<int>(kTilesPerShard)));
     c->tune.p1_min_tiles = std::max(0, env_int("PHJ_P1_MIN_TILES", 32768));
     c->tune.p1_ko_tps = std::max(1, env_int("PHJ_P1_KO_TPS", 1024));
     c->tune.p1_ko_min_tiles = std::max(0, env_int("PHJ_P1_KO_MIN_TILES", 0));
     {
-        const int ev = env_int("PHJ_EVENTS", 1);   // 0 default, 1 no system fence, 2 device release
-        c->tune.ev_flags = ev == 0 ? hipEventDefault : ev == 2 ? hipEventReleaseToDevice : hipEventDisableSystemFence;
-    }
-    {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
-    }
-    {
-        const int k = env_int("PHJ_CU_SPLIT", 0);
-        if (k > 0 && k < 32 && c->num_cus % 32 == 0) {
-            std::vector<uint32_t> rm(static_cast<size_t>(c->num_cus) / 32, 0), sm(rm.size(), 0);
-            for (size_t w = 0; w < rm.size(); w++) {
-                rm[w] = (1u << k) - 1u;
-                sm[w] = ~rm[w];
-            }
-            if (hipExtStreamCreateWithCUMask(&c->r_split, static_cast<uint32_t>(rm.size()), rm.data()) != hipSuccess ||
-                hipExtStreamCreateWithCUMask(&c->s_split, static_cast<uint32_t>(sm.size()), sm.data()) != hipSuccess) {
-                if (c->r_split) (void)hipStreamDestroy(c->r_split);
-                c->r_split = c->s_split = nullptr;
-            } else {
-                c->s_split_cus = c->num_cus - k * (c->num_cus / 32);
-            }
-        }
     }
     c->tune.wc_items = env_int("PHJ_WC_ITEMS", 8) == 4 ? 4 : 8;
     c->tune.wc_lw = env_int("PHJ_WC_LW", 8) == 16 ? 16 : 8;
@@ -1926,11 +1743,9 @@ void phj_ctx_destroy(phj_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     (void)hipStreamSynchronize(c->aux);
-    if (c->r_split) (void)hipStreamSynchronize(c->r_split);
-    if (c->s_split) (void)hipStreamSynchronize(c->s_split);
     for (SideState& S : c->side) {
         for (DevBuf* b : {&S.owned, &S.kA, &S.pA, &S.kB, &S.pB, &S.hist1, &S.hist2, &S.bounds1, &S.tbase2,
-                          &S.bounds, &S.partials, &S.tseg2, &S.dig, &S.ccur, &S.ctab, &S.tstart, &S.priv})
+                          &S.bounds, &S.partials, &S.tseg2, &S.dig, &S.ccur, &S.ctab, &S.tstart})
             free_buf(*b);
     }
     for (DevBuf* b : {&c->ht_tab, &c->ht_desc, &c->r_codes, &c->r_bounds, &c->scan_partials, &c->prep, &c->tkeys, &c->tpays, &c->toffs, &c->gcursor, &c->items, &c->biglist,
@@ -1939,8 +1754,6 @@ void phj_ctx_destroy(phj_ctx* c) {
     for (hipEvent_t e : c->evpool) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->stream);
     (void)hipStreamDestroy(c->aux);
-    if (c->r_split) (void)hipStreamDestroy(c->r_split);
-    if (c->s_split) (void)hipStreamDestroy(c->s_split);
     delete c;
 }
 
@@ -1952,8 +1765,6 @@ int phj_ctx_set_stream(phj_ctx* c, void* stream) {
     PHJ_HIP(c, hipSetDevice(c->device));
     PHJ_HIP(c, hipStreamSynchronize(c->stream));
     PHJ_HIP(c, hipStreamSynchronize(c->aux));
-    if (c->r_split) PHJ_HIP(c, hipStreamSynchronize(c->r_split));
-    if (c->s_split) PHJ_HIP(c, hipStreamSynchronize(c->s_split));
     if (c->own_stream) {
         PHJ_HIP(c, hipStreamDestroy(c->stream));
         c->own_stream = false;
@@ -1978,8 +1789,6 @@ int phj_ctx_synchronize(phj_ctx* c) {
         return PHJ_OK;
     }
     PHJ_HIP(c, hipStreamSynchronize(c->aux));
-    if (c->r_split) PHJ_HIP(c, hipStreamSynchronize(c->r_split));
-    if (c->s_split) PHJ_HIP(c, hipStreamSynchronize(c->s_split));
     PHJ_HIP(c, hipStreamSynchronize(c->stream));
     return PHJ_OK;
 }

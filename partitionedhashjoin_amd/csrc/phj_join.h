@@ -135,7 +135,6 @@ struct BuildArgs {
     uint32_t ocap;         // LDS bucket-counter capacity (per wave in k_build_small)
     uint32_t pad;
     uint64_t seed;
-    longlong2* home;       // non-null: the build also writes the home slots (indexed like toffs)
 };
 
 // LDS ordering between lanes of one wave (stores before loads of other lanes).
@@ -154,7 +153,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 // 64 * KPL tuples or a bucket array beyond the wave's LDS slice are appended to
 // biglist for k_build_big. The order inside a bucket is irrelevant to the
 // semi-join count (set membership).
-template <int HK, int KPL, bool HOUT = false>   // HOUT: store hash codes (phj_hash.h kHashed)
+template <int HK, int KPL>
 __global__ __launch_bounds__(kBlock) void k_build_small(BuildArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -180,8 +179,6 @@ __global__ __launch_bounds__(kBlock) void k_build_small(BuildArgs a) {
         uint32_t* offs = a.toffs + ob;
         if (m == 0) {
             for (uint32_t i = lane; i <= nbk; i += 64) offs[i] = 0;
-            if (a.home)
-                for (uint32_t i = lane; i < nbk; i += 64) a.home[ob + i] = make_longlong2(0, 0);
             continue;
         }
         if (nbk > a.ocap || m > 64u * KPL) {
@@ -219,7 +216,6 @@ __global__ __launch_bounds__(kBlock) void k_build_small(BuildArgs a) {
         for (int j = 0; j < KPL; j++) {
             const uint64_t h = hash64<HK>(static_cast<uint64_t>(key[j]), a.seed);
             bkt[j] = bucket_of(h, nbk);
-            if constexpr (HOUT) key[j] = static_cast<int64_t>(h);
             if (j * 64 + lane < m) atomicAdd(&cnt[bkt[j]], 1u);
         }
         wave_lds_sync();
@@ -236,20 +232,10 @@ __global__ __launch_bounds__(kBlock) void k_build_small(BuildArgs a) {
             if (i < nbk) {
                 cnt[i] = carry + x - v;
                 offs[i] = carry + x - v;
-                // home slot, second half: key count | offset of the bucket's second key
-                if (a.home)
-                    reinterpret_cast<int64_t*>(a.home + ob + i)[1] =
-                        static_cast<int64_t>((static_cast<uint64_t>(carry + x - v + 1) << 32) | v);
             }
             carry += __shfl(x, 63, 64);
         }
         if (lane == 0) offs[nbk] = m;
-        wave_lds_sync();
-        // every bucket's start, read before any placement moves it: the tuple
-        // placed there is the bucket's first key (home slot, first half)
-        uint32_t st[KPL];
-#pragma unroll
-        for (int j = 0; j < KPL; j++) st[j] = a.home ? cnt[bkt[j]] : 0xffffffffu;
         wave_lds_sync();
 #pragma unroll
         for (int j = 0; j < KPL; j++) {
@@ -257,7 +243,6 @@ __global__ __launch_bounds__(kBlock) void k_build_small(BuildArgs a) {
                 const uint32_t pos = atomicAdd(&cnt[bkt[j]], 1u);
                 a.tkeys[kb + pos] = key[j];
                 if (spays_all) a.tpays[kb + pos] = pay[j];
-                if (pos == st[j]) reinterpret_cast<int64_t*>(a.home + ob + bkt[j])[0] = key[j];
             }
         }
         wave_lds_sync();
@@ -281,7 +266,7 @@ __device__ __forceinline__ void block_scan_array(uint32_t len, LoadF ld, StoreF 
 
 // One workgroup per partition of biglist (bucket arrays beyond a wave's LDS
 // slice): LDS counters up to ocap buckets, global atomics beyond.
-template <int HK, bool HOUT = false>
+template <int HK>
 __global__ __launch_bounds__(kBlock) void k_build_big(BuildArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint32_t* tmp = reinterpret_cast<uint32_t*>(smem);        // 16 words
@@ -294,8 +279,6 @@ __global__ __launch_bounds__(kBlock) void k_build_big(BuildArgs a) {
         uint32_t* offs = a.toffs + ob;
         if (m == 0) {
             for (uint32_t i = threadIdx.x; i <= nbk; i += kBlock) offs[i] = 0;
-            if (a.home)
-                for (uint32_t i = threadIdx.x; i < nbk; i += kBlock) a.home[ob + i] = make_longlong2(0, 0);
             continue;
         }
         const bool in_lds = (nbk <= a.ocap);   // (m > 0 here)
@@ -351,19 +334,11 @@ __global__ __launch_bounds__(kBlock) void k_build_big(BuildArgs a) {
                 uint32_t pos;
                 if (in_lds) pos = atomicAdd(&cnt[b], 1u);
                 else pos = __hip_atomic_fetch_add(&cnt[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                a.tkeys[kb + pos] = HOUT ? static_cast<int64_t>(h) : key;
+                a.tkeys[kb + pos] = key;
                 if (S.pays) a.tpays[kb + pos] = pay;
             }
         }
         __syncthreads();
-        if (a.home) {   // home slots from the placed table (written by this workgroup)
-            for (uint32_t i = threadIdx.x; i < nbk; i += kBlock) {
-                const uint32_t o0 = offs[i], o1 = i + 1 < nbk ? offs[i + 1] : m;
-                const int64_t k0 = o1 > o0 ? a.tkeys[kb + o0] : 0;
-                a.home[ob + i] = make_longlong2(k0, static_cast<int64_t>((static_cast<uint64_t>(o0 + 1) << 32) | (o1 - o0)));
-            }
-            __syncthreads();
-        }
     }
 }
 
@@ -1097,345 +1072,6 @@ __global__ __launch_bounds__(kBlock) void k_np_probe(const longlong2* S, uint64_
 }
 
 // ---------------------------------------------------------------------------
-// Probe straight from the pass-1 partitions (PHJ_P2PROBE): the probe side's
-// second partitioning pass runs on-chip instead of through HBM. A pass-2 tile
-// (<= T tuples of one pass-1 partition d1, from the chunked or the stable
-// pass-1 layout) is loaded, sorted by its second digit d2 in LDS exactly as
-// k_scatter sorts it, and then every key probes the prebuilt bucket table of
-// its final partition p = d1 * nb2 + d2 (CSR in HBM, k_build_small over the
-// fully partitioned R) instead of being written out and read back. The
-// per-partition semantics are the reference's (HashJoin.hpp:267-303: build a
-// table per partition, probe it with the partition's S tuples); sorting by d2
-// makes consecutive lanes probe the same small table, so its lines are L1/L2
-// hits. Saved per S tuple: the pass-2 histogram (1 B), the pass-2 write
-// (16 B) and the probe's re-read of the key (8 B).
-// ---------------------------------------------------------------------------
-struct P1ProbeArgs {
-    PassArgs a;               // the pass-2 tile mapping over the pass-1 output (in_keys = AoS tuples)
-    const uint4* desc;        // per final partition: {kb, ob, nbk, m}
-    const uint32_t* toffs;    // bucket offsets (relative to kb), nbk + 1 per partition
-    const int64_t* tkeys;     // keys in bucket order
-    unsigned long long* count;
-    uint64_t seed;
-    uint32_t nb2;             // digits of pass 2 (final partition = d1 * nb2 + d2)
-    uint32_t pad;
-    // pass 1 into workgroup-private chains (k_scatter_priv): tile t of digit d
-    // is entries [ebase[d] + (t - tile_base[d]) * 64, +64) of the chunk list,
-    // one chunk (g << 6 | fill - 1) per wave row. nullptr: tiles from a.tile_start
-    const uint32_t* ent;
-    const uint32_t* ebase;
-    const longlong2* home;    // HOME probe: k_csr_home's slots (indexed like toffs)
-};
-
-// arr: 2 arrays of P+1 entries: m_p and NB_p + 1 (last entries 0), for the
-// CSR tables of k_build_small when no probe work list is needed.
-__global__ __launch_bounds__(kBlock) void k_csr_prep(SegList L, uint32_t* arr, uint32_t bshift) {
-    const uint32_t P = L.P;
-    const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
-    if (p > P) return;
-    const size_t stride = static_cast<size_t>(P) + 1;
-    if (p == P) {
-        arr[P] = 0;
-        arr[stride + P] = 0;
-        return;
-    }
-    uint32_t m = 0;
-    for (uint32_t g = 0; g < L.nseg; g++) m += L.seg[g].bounds[p + 1] - L.seg[g].bounds[p];
-    arr[p] = m;
-    arr[stride + p] = (table_buckets(m) << (m > 1 ? bshift : 0u)) + 1;
-}
-
-// Home slots over a built CSR table (one wave per partition): home[ob + i] =
-// {first key of bucket i, its key count | (offset of its second key) << 32},
-// so a probe reads one 16-B slot and only walks tkeys for a bucket holding
-// more than one key and not matching the first.
-__global__ __launch_bounds__(kBlock) void k_csr_home(const uint4* desc, const uint32_t* toffs, const int64_t* tkeys,
-                                                     uint32_t P, longlong2* home) {
-    const uint32_t p = blockIdx.x * kWaves + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (p >= P) return;
-    const uint4 d = desc[p];   // {kb, ob, nbk, m}
-    for (uint32_t i = lane; i < d.z; i += 64) {
-        const uint32_t o0 = toffs[d.y + i], o1 = toffs[d.y + i + 1];
-        const int64_t k0 = o1 > o0 ? tkeys[d.x + o0] : 0;
-        home[d.y + i] = make_longlong2(k0, static_cast<int64_t>((static_cast<uint64_t>(o0 + 1) << 32) | (o1 - o0)));
-    }
-}
-
-// desc[p] = {kb, ob, nbk, m} from the scanned table bases.
-__global__ __launch_bounds__(kBlock) void k_csr_desc(const uint32_t* tkb, const uint32_t* tob, uint32_t P,
-                                                     uint4* desc) {
-    const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
-    if (p >= P) return;
-    const uint32_t kb = tkb[p], ob = tob[p];
-    desc[p] = make_uint4(kb, ob, tob[p + 1] - ob - 1, tkb[p + 1] - kb);
-}
-
-// Persistent: XCD x walks the contiguous tile range [x, x + 1) * ntiles / 8
-// (tiles of one pass-1 partition are contiguous, so an XCD's L2 holds the
-// few R tables it is probing), its workgroups round-robin over it, and the
-// next tile's keys load while the current one is probed. The tile is grouped
-// by d2 with one LDS atomic per key (an unstable counting sort: the probe only
-// needs neighbours to share a table); the tile's nb2 table descriptors are
-// staged in LDS. The digit and bucket bits are re-hashed after the grouping
-// (the LDS holds keys only: four workgroups per CU). Measured
-// against a one-read table of 64-B buckets (7 keys + fill per bucket, wrapping
-// regions): 1.94 ms against 1.45 for these narrow CSR reads (two 4-B offsets,
-// ~1.2 8-B keys), as in the NoPartitioning probe a lane's four 16-B loads of
-// one bucket cost more than the extra dependent level. DIAG (timing only):
-// 1 = no table reads.
-template <int BLOCK, int ITEMS, int HK, int DIAG = 0, int WPE = 4, bool CHK = false, bool GRP = true, bool HOME = false>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void k_probe_p1(P1ProbeArgs pa) {
-    constexpr int T = BLOCK * ITEMS;
-    constexpr int PB = 4;   // probes in flight per lane per batch
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const PassArgs& a = pa.a;
-    const uint32_t nb = a.nbins;
-    int64_t* skey = reinterpret_cast<int64_t*>(smem);
-    uint4* sdesc = reinterpret_cast<uint4*>(skey + T);            // [nb]
-    uint32_t* cnt_d = reinterpret_cast<uint32_t*>(sdesc + nb);    // [nb] counts, then starts
-    uint32_t* tmp = cnt_d + nb;                                   // 16 words
-    __shared__ uint32_t red[BLOCK / 64];
-    // (measured: carrying the digit and bucket bits beside the key in LDS
-    // instead of re-hashing after the grouping costs registers: 25 VGPRs
-    // spilled at 6 waves/SIMD, probe 1.27 -> 1.44 ms)
-
-    const uint32_t total = a.tile_base[a.nseg];
-    const uint32_t xcd = blockIdx.x & 7u, g8 = gridDim.x >> 3;
-    const uint32_t t_lo = static_cast<uint32_t>(static_cast<uint64_t>(total) * xcd / 8);
-    const uint32_t t_hi = static_cast<uint32_t>(static_cast<uint64_t>(total) * (xcd + 1) / 8);
-    uint32_t tile = t_lo + (blockIdx.x >> 3);
-    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    uint32_t hits = 0;
-    if (tile < t_hi) {
-        const uint32_t wbase = wave * 64 * ITEMS;
-        const longlong2* rel = reinterpret_cast<const longlong2*>(a.in_keys);
-        int64_t key[ITEMS];
-        uint32_t vm = 0, d1 = 0;   // vm bit i: item i holds a key
-        auto load = [&](uint32_t t, uint32_t& m, uint32_t& d) {
-            d = a.tile_seg[t];
-            m = 0;
-            if constexpr (CHK) {   // 64 chunks, wave row r = wave * ITEMS + i holds chunk r
-                const uint32_t e0 = pa.ebase[d] + (t - a.tile_base[d]) * 64;
-                const uint32_t ne = min(64u, pa.ebase[d + 1] - e0);
-                const uint32_t wv = __builtin_amdgcn_readfirstlane(wave);   // rows are wave-uniform: scalar loads
-#pragma unroll
-                for (int i = 0; i < ITEMS; i++) {
-                    const uint32_t r = wv * ITEMS + i;
-                    const uint32_t en = r < ne ? pa.ent[e0 + r] : 0u;
-                    const bool v = r < ne && lane <= (en & 63u);
-                    key[i] = v ? rel[static_cast<size_t>(en >> 6) * 64 + lane].x : 0;
-                    m |= v ? (1u << i) : 0u;
-                }
-                return;
-            }
-            TileLoc L;
-            locate_tile<T>(a, t, L);
-            const uint32_t c = L.hi - L.lo;
-            // pass-1 output as AoS tuples (the default) or as a key column (PHJ_P1_AOS=0)
-            const bool soa = a.in_pays != nullptr || a.keys_only;
-#pragma unroll
-            for (int i = 0; i < ITEMS; i++) {
-                const uint32_t e = wbase + i * 64 + lane;
-                key[i] = e < c ? (soa ? a.in_keys[L.lo + e] : rel[L.lo + e].x) : 0;
-                m |= e < c ? (1u << i) : 0u;
-            }
-        };
-        load(tile, vm, d1);
-        uint32_t staged = 0xffffffffu;   // d1 whose table descriptors sit in LDS
-        for (;;) {
-            const uint32_t pbase = d1 * pa.nb2;
-            const bool restage = d1 != staged;   // consecutive tiles mostly share d1
-            for (uint32_t d = tid; d < nb; d += BLOCK) {
-                cnt_d[d] = 0;
-                if (restage) sdesc[d] = pa.desc[pbase + d];
-            }
-            staged = d1;
-            __syncthreads();
-            if constexpr (!GRP) {
-                // ungrouped: every key probes straight from registers (hashed
-                // once); the next tile's keys load into a second register set
-                int64_t kc[ITEMS];
-#pragma unroll
-                for (int i = 0; i < ITEMS; i++) kc[i] = key[i];
-                const uint32_t vc = vm;
-                const uint32_t next = tile + g8;
-                uint32_t nvm = 0, nd1 = 0;
-                load(next < t_hi ? next : tile, nvm, nd1);
-#pragma unroll
-                for (int i0 = 0; i0 < ITEMS; i0 += PB) {
-                    uint4 ds[PB];
-                    uint32_t hb[PB];
-#pragma unroll
-                    for (int i = 0; i < PB; i++) {
-                        ds[i] = make_uint4(0, 0, 1, 0);
-                        hb[i] = 0;
-                        if ((vc >> (i0 + i)) & 1u) {
-                            const uint64_t h = hash64<HK>(static_cast<uint64_t>(kc[i0 + i]), pa.seed);
-                            hb[i] = static_cast<uint32_t>(h >> 32);
-                            ds[i] = sdesc[static_cast<uint32_t>(q_from_hash(h, a.f) >> a.f.shift) & a.f.dmask];
-                        }
-                    }
-                    uint32_t o0[PB], o1[PB];
-#pragma unroll
-                    for (int i = 0; i < PB; i++) {
-                        o0[i] = o1[i] = 0;
-                        if (ds[i].w) {
-                            typedef uint32_t u32x2 __attribute__((ext_vector_type(2), aligned(4)));
-                            const u32x2 ob = *reinterpret_cast<const u32x2*>(pa.toffs + ds[i].y + (hb[i] & (ds[i].z - 1u)));
-                            o0[i] = ob.x;
-                            o1[i] = ob.y;
-                        }
-                    }
-                    int64_t f[PB][2];
-#pragma unroll
-                    for (int i = 0; i < PB; i++) {
-#pragma unroll
-                        for (int j = 0; j < 2; j++) f[i][j] = o0[i] + j < o1[i] ? pa.tkeys[ds[i].x + o0[i] + j] : 0;
-                    }
-#pragma unroll
-                    for (int i = 0; i < PB; i++) {
-                        const int64_t k2 = kc[i0 + i];
-                        bool hit = (o0[i] < o1[i] && f[i][0] == k2) || (o0[i] + 1 < o1[i] && f[i][1] == k2);
-                        for (uint32_t j = o0[i] + 2; j < o1[i] && !hit; j++) hit = pa.tkeys[ds[i].x + j] == k2;
-                        hits += hit ? 1u : 0u;
-                    }
-                }
-                if (next >= t_hi) break;
-                tile = next;
-                vm = nvm;
-                d1 = nd1;
-                __syncthreads();   // sdesc reads of this tile before a restage
-                continue;
-            }
-            uint32_t dig[ITEMS], rank[ITEMS];
-#pragma unroll
-            for (int i = 0; i < ITEMS; i++) {
-                const uint64_t h = hash64<HK>(static_cast<uint64_t>(key[i]), pa.seed);
-                dig[i] = static_cast<uint32_t>(q_from_hash(h, a.f) >> a.f.shift) & a.f.dmask;
-                if ((vm >> i) & 1u) rank[i] = atomicAdd(&cnt_d[dig[i]], 1u);
-            }
-            __syncthreads();
-            uint32_t cnt;   // keys of the tile, grouped into [0, cnt)
-            {
-                const uint32_t dpt = (nb + BLOCK - 1) / BLOCK;
-                const uint32_t d0 = tid * dpt;
-                uint32_t local = 0;
-                for (uint32_t j = 0; j < dpt; j++)
-                    if (d0 + j < nb) local += cnt_d[d0 + j];
-                uint32_t tot;
-                uint32_t run = block_exclusive_scan_t<BLOCK / 64>(local, tmp, tot);
-                cnt = tot;
-                for (uint32_t j = 0; j < dpt; j++) {
-                    const uint32_t d = d0 + j;
-                    if (d < nb) {
-                        const uint32_t c = cnt_d[d];
-                        cnt_d[d] = run;
-                        run += c;
-                    }
-                }
-            }
-            __syncthreads();
-#pragma unroll
-            for (int i = 0; i < ITEMS; i++) {
-                if ((vm >> i) & 1u) skey[cnt_d[dig[i]] + rank[i]] = key[i];
-            }
-            // the next tile's keys go out now, into the same registers
-            const uint32_t next = tile + g8;
-            uint32_t nvm = 0, nd1 = 0;
-            load(next < t_hi ? next : tile, nvm, nd1);
-            __syncthreads();
-            // probe in grouped order: consecutive lanes mostly share a table
-#pragma unroll
-            for (int i0 = 0; i0 < ITEMS; i0 += PB) {
-                uint4 ds[PB];
-                int64_t k2[PB];
-                uint32_t hb[PB];
-#pragma unroll
-                for (int i = 0; i < PB; i++) {
-                    const uint32_t k = (i0 + i) * BLOCK + tid;
-                    ds[i] = make_uint4(0, 0, 1, 0);
-                    k2[i] = 0;
-                    hb[i] = 0;
-                    if (k < cnt) {
-                        k2[i] = skey[k];
-                        const uint64_t h = hash64<HK>(static_cast<uint64_t>(k2[i]), pa.seed);
-                        hb[i] = static_cast<uint32_t>(h >> 32);
-                        if constexpr (DIAG == 1) ds[i].w = (k2[i] & 1) ? 1u : 0u;
-                        else ds[i] = sdesc[static_cast<uint32_t>(q_from_hash(h, a.f) >> a.f.shift) & a.f.dmask];
-                    }
-                }
-                if constexpr (HOME) {
-                    // one 16-B home slot per probe: first key, count, rest offset
-                    longlong2 hs[PB];
-#pragma unroll
-                    for (int i = 0; i < PB; i++) {
-                        hs[i] = make_longlong2(0, 0);
-                        if (ds[i].w) hs[i] = pa.home[ds[i].y + (hb[i] & (ds[i].z - 1u))];
-                    }
-#pragma unroll
-                    for (int i = 0; i < PB; i++) {
-                        const uint32_t cntb = static_cast<uint32_t>(hs[i].y);
-                        bool hit = cntb != 0 && hs[i].x == k2[i];
-                        const uint32_t r0 = static_cast<uint32_t>(static_cast<uint64_t>(hs[i].y) >> 32);
-                        for (uint32_t j = 1; j < cntb && !hit; j++) hit = pa.tkeys[ds[i].x + r0 + j - 1] == k2[i];
-                        hits += hit ? 1u : 0u;
-                    }
-                    continue;
-                }
-                uint32_t o0[PB], o1[PB];
-#pragma unroll
-                for (int i = 0; i < PB; i++) {
-                    o0[i] = o1[i] = 0;
-                    if (DIAG != 1 && ds[i].w) {   // m > 0
-                        const uint32_t b = hb[i] & (ds[i].z - 1u);
-                        // the bucket's [start, end) offsets in one 8-B load (4-B aligned)
-                        typedef uint32_t u32x2 __attribute__((ext_vector_type(2), aligned(4)));
-                        const u32x2 ob = *reinterpret_cast<const u32x2*>(pa.toffs + ds[i].y + b);
-                        o0[i] = ob.x;
-                        o1[i] = ob.y;
-                    }
-                }
-                // the first two keys of every bucket are requested together (one
-                // L2 round trip for all PB probes; buckets average ~1.5 keys),
-                // the rest walked only when a bucket holds more
-                int64_t f[PB][2];
-#pragma unroll
-                for (int i = 0; i < PB; i++) {
-#pragma unroll
-                    for (int j = 0; j < 2; j++) f[i][j] = o0[i] + j < o1[i] ? pa.tkeys[ds[i].x + o0[i] + j] : 0;
-                }
-#pragma unroll
-                for (int i = 0; i < PB; i++) {
-                    bool hit = (DIAG == 1 && ds[i].w != 0) || (o0[i] < o1[i] && f[i][0] == k2[i]) ||
-                               (o0[i] + 1 < o1[i] && f[i][1] == k2[i]);
-                    for (uint32_t j = o0[i] + 2; j < o1[i] && !hit; j++) hit = pa.tkeys[ds[i].x + j] == k2[i];
-                    hits += hit ? 1u : 0u;
-                }
-            }
-            if (next >= t_hi) break;
-            tile = next;
-            vm = nvm;
-            d1 = nd1;
-            __syncthreads();   // LDS reads of this tile before the next tile's counts
-        }
-    }
-    uint32_t x = hits;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x += __shfl_down(x, o, 64);
-    if (lane == 0) red[wave] = x;
-    __syncthreads();
-    if (tid == 0) {
-        unsigned long long t = 0;
-        for (int w = 0; w < BLOCK / 64; w++) t += red[w];
-        if (t) atomicAdd(pa.count, t);
-    }
-}
-
-__host__ __device__ constexpr size_t probe_p1_lds_bytes(int T, uint32_t nb, int NW) {
-    return static_cast<size_t>(T) * 8 + static_cast<size_t>(nb) * 20 + 64 + 16 + 0 * NW;
-}
-
-// ---------------------------------------------------------------------------
 // NoPartitioning hot-key cache. Under Zipf a few keys
 // take most probes (s = 1.05 over 10M keys: the top key 8.7 %, the top ~1000
 // about half); their buckets are L2 hits, but every probe of one key lands on
@@ -1619,125 +1255,6 @@ __global__ __launch_bounds__(kBlock) void k_np_probe_hot(const longlong2* S, uin
         for (int w = 0; w < kWaves; w++) t += red[w];
         if (t) atomicAdd(count, t);
     }
-}
-
-// Cooperative NoPartitioning probe: four lanes read one 64-B bucket (one
-// 16-B part each), so a wave's bucket load instruction touches 16 cache lines
-// instead of 64. Measured on the probe's own access pattern: with one lane per
-// bucket a wave's 4 x ITEMS load instructions each touch 64 lines and the
-// vector L1 (one tag lookup per line per clock) caps the probe at ~1.3 ms for
-// 200M probes even when every bucket is an L2 hit (PHJ_NP_DIAG=2), against
-// 0.46 ms for streaming and hashing S alone (PHJ_NP_DIAG=1). Each wave stages
-// its ITEMS x 64 keys and home buckets in LDS; in load step t the quad g of
-// lanes serves key t * 16 + g; a quad's hit is OR-reduced and counted once.
-// DIAG = 4: every bucket index is replaced by one of 4096 (the L2-hit floor).
-template <int HK, int ITEMS, int NT, int DIAG = 0>
-__global__ __launch_bounds__(kBlock) void k_np_probe_coop(const longlong2* S, uint64_t nS, const NPBucket* tab,
-                                                          NPHome g, uint64_t seed, unsigned long long* count) {
-    constexpr int NK = ITEMS * 64;   // keys per wave per round
-    __shared__ int64_t wkey[kWaves][NK];
-    __shared__ uint32_t wbkt[kWaves][NK];
-    __shared__ uint32_t red[kWaves];
-    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint32_t quad = lane >> 2, part = lane & 3;
-    const uint32_t nb = g.nb;
-    uint32_t hits = 0;
-    const uint64_t wstride = static_cast<uint64_t>(gridDim.x) * kWaves * NK;
-    for (uint64_t base = (static_cast<uint64_t>(blockIdx.x) * kWaves + wv) * NK; base < nS; base += wstride) {
-        // stage: ITEMS coalesced keys per lane, their home buckets (~0u: past the end)
-#pragma unroll
-        for (int j = 0; j < ITEMS; j++) {
-            const uint64_t idx = base + static_cast<uint64_t>(j) * 64 + lane;
-            int64_t k = 0;
-            if (idx < nS) {
-                if constexpr (NT > 0) k = __builtin_nontemporal_load(&S[idx].x);
-                else k = S[idx].x;
-            }
-            const uint64_t h = hash64<HK>(static_cast<uint64_t>(k), seed);
-            uint32_t b = np_home_r(h, g);
-            if constexpr (DIAG == 4) b = static_cast<uint32_t>(h) & 4095u;
-            wkey[wv][j * 64 + lane] = k;
-            wbkt[wv][j * 64 + lane] = idx < nS ? b : ~0u;
-        }
-        __builtin_amdgcn_wave_barrier();
-        // every part of every bucket of the round requested before any compare
-        longlong2 q[4 * ITEMS];
-        int64_t key[4 * ITEMS];
-        uint32_t bk[4 * ITEMS];
-#pragma unroll
-        for (int t = 0; t < 4 * ITEMS; t++) {
-            const uint32_t slot = t * 16 + quad;
-            key[t] = wkey[wv][slot];
-            bk[t] = wbkt[wv][slot];
-            if (bk[t] != ~0u) q[t] = reinterpret_cast<const longlong2*>(tab + bk[t])[part];
-            else q[t] = make_longlong2(0, 0);
-        }
-#pragma unroll
-        for (int t = 0; t < 4 * ITEMS; t++) {
-            // the fill count sits in part 3's second half
-            const uint32_t fill = static_cast<uint32_t>(__shfl(q[t].y, (lane & ~3u) | 3u, 64));
-            const uint32_t c = fill < kNPSlots ? fill : kNPSlots;
-            const uint32_t s0 = 2 * part;
-            bool m = (s0 < c && q[t].x == key[t]) || (part < 3 && s0 + 1 < c && q[t].y == key[t]);
-            uint32_t any = m ? 1u : 0u;
-            any |= static_cast<uint32_t>(__shfl_xor(static_cast<int>(any), 1, 64));
-            any |= static_cast<uint32_t>(__shfl_xor(static_cast<int>(any), 2, 64));
-            if (part == 0 && bk[t] != ~0u) {
-                if (any) hits++;
-                else if (fill >= kNPSlots)   // full home bucket: continue in the next ones (rare)
-                    hits += np_lookup(tab, nb, bk[t] + 1 == nb ? 0 : bk[t] + 1, key[t]) ? 1u : 0u;
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-    }
-    uint32_t x = hits;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x += __shfl_down(x, o, 64);
-    if (lane == 0) red[wv] = x;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long t = 0;
-        for (int w = 0; w < kWaves; w++) t += red[w];
-        if (t) atomicAdd(count, t);
-    }
-}
-
-// Diagnostic floors of the probe (PHJ_NP_DIAG, timing only; the count is not
-// the join's): 1 = stream and hash S without any bucket read; 2 = every probe
-// reads one of 4096 buckets (L2 hits spread over the channels); 3 = every
-// probe reads bucket 0 (one L2 line).
-template <int HK, int MODE>
-__global__ __launch_bounds__(kBlock) void k_np_probe_diag(const longlong2* S, uint64_t nS, const NPBucket* tab,
-                                                          NPHome g, uint64_t seed, unsigned long long* count) {
-    constexpr int ITEMS = 4;
-    uint32_t hits = 0;
-    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kBlock * ITEMS;
-    for (uint64_t base = static_cast<uint64_t>(blockIdx.x) * kBlock * ITEMS; base < nS; base += stride) {
-        int64_t k[ITEMS];
-#pragma unroll
-        for (int j = 0; j < ITEMS; j++) {
-            const uint64_t idx = base + static_cast<uint64_t>(j) * kBlock + threadIdx.x;
-            k[j] = idx < nS ? __builtin_nontemporal_load(&S[idx].x) : 0;
-        }
-        longlong2 q[ITEMS][4];
-#pragma unroll
-        for (int j = 0; j < ITEMS; j++) {
-            const uint64_t h = hash64<HK>(static_cast<uint64_t>(k[j]), seed);
-            const uint32_t b = MODE == 2 ? static_cast<uint32_t>(h) & 4095u : 0u;
-            if constexpr (MODE == 1) {
-                hits += (h & 1023) == 7;
-            } else {
-                const longlong2* bp = reinterpret_cast<const longlong2*>(tab + b);
-#pragma unroll
-                for (int w = 0; w < 4; w++) q[j][w] = bp[w];
-            }
-        }
-        if constexpr (MODE != 1) {
-#pragma unroll
-            for (int j = 0; j < ITEMS; j++) hits += q[j][0].x == k[j] || q[j][2].y == k[j];
-        }
-    }
-    if (hits == 0xffffffffu) atomicAdd(count, 1ull);
 }
 
 // ---------------------------------------------------------------------------

@@ -205,6 +205,24 @@ __device__ __forceinline__ void count_digit(uint32_t* row, uint32_t d, bool vali
     if (lane == static_cast<uint32_t>(__builtin_ctzll(act))) atomicAdd(&row[first], static_cast<uint32_t>(__popcll(same)));
 }
 
+// A slot from counter row C for this lane's digit d (every lane calls it,
+// d computed on invalid lanes too): the lanes sharing the wave's first active
+// digit take one LDS atomic together, so a hot key's digit does not
+// serialise a wave-instruction 64-way (Zipf input); the others take one each.
+__device__ __forceinline__ uint32_t agg_rank_lds(uint32_t* C, uint32_t d, bool valid) {
+    const uint64_t act = __ballot(valid);
+    if (act == 0) return 0;
+    const int leader = __builtin_ctzll(act);
+    const uint32_t ld = __builtin_amdgcn_readlane(d, leader);
+    const bool mine = valid && d == ld;
+    const uint64_t same = __ballot(mine);
+    uint32_t base = 0;
+    if ((threadIdx.x & 63) == static_cast<uint32_t>(leader)) base = atomicAdd(&C[ld], static_cast<uint32_t>(__popcll(same)));
+    base = __builtin_amdgcn_readlane(base, leader);
+    if (mine) return base + static_cast<uint32_t>(__popcll(same & lanemask_lt()));
+    return valid ? atomicAdd(&C[d], 1u) : 0u;
+}
+
 // Exclusive scan of one value per thread across a block of NW waves.
 template <int NW>
 __device__ __forceinline__ uint32_t block_exclusive_scan_t(uint32_t v, uint32_t* tmp,
@@ -573,6 +591,7 @@ void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
     constexpr int T = BLOCK * ITEMS;
     constexpr bool ARANK = (VAR & 1) != 0, KO = (VAR & 4) != 0, LAOS = (VAR & 2) != 0 && !KO;
     constexpr bool HC = KO && (VAR & 8) != 0;   // keys only, written as hash codes
+    constexpr bool NOCLAIM = (VAR & 16) != 0;   // TEMPORARY measurement: tiles written in place, no chain claims
     // atomic ranking + one 16-B access per element: a digit's three write
     // offsets packed in one 16-B LDS entry (one ds_read_b128 per element in
     // the write loop), placed in the counter rows the atomic ranking leaves unused
@@ -654,7 +673,7 @@ void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
             dig[i] = d;
             rank[i] = 0;
             if constexpr (ARANK) {
-                if (valid) rank[i] = atomicAdd(&my[d], 1u);
+                rank[i] = agg_rank_lds(my, d, valid);
             } else {
                 const uint64_t peers = match_digit(d, valid, a.nbits);
                 if (valid) {
@@ -685,7 +704,7 @@ void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
                     run += v;
                 }
             }
-            if (tid < nb && c) {
+            if (!NOCLAIM && tid < nb && c) {
                 v0 = atomicAdd(cur(tid), c);
                 hint = __hip_atomic_load(hint_of(tid), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
@@ -717,7 +736,8 @@ void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
         // behind the claims, into the same registers
         const uint32_t next = tile + slots;
         load(next < t_end ? next : tile);   // unconditional (a last one goes unused): exact vmcnt waits
-        if (tid < nb && c) {
+        if (NOCLAIM && tid < nb) wdesc[tid] = make_uint4(tile * T, tile * T, T, 0u);
+        if (!NOCLAIM && tid < nb && c) {
             const uint32_t d = tid;
             const uint32_t off = v0 % T, k0 = v0 / T, k1 = (v0 + c - 1) / T;
             unsigned long long* tab = a.chunk_tab + (static_cast<size_t>(x) * nb + d) * a.maxch;
@@ -794,239 +814,6 @@ void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
     }
 }
 
-// ---------------------------------------------------------------------------
-// Pass 1 into workgroup-private chains (unordered partitions, consumed by the
-// on-chip pass-2 probe). Every persistent workgroup w owns a contiguous run
-// of tiles and a private region of 64-slot chunks; digit d of w is a chain of
-// chunks whose state (open chunk, its fill, chunks taken) lives in thread d's
-// registers. A tile's run of digit d fills the open chunk, then as many fresh
-// chunks as it needs, taken consecutively from the region by one block scan
-// of (count | chunks << 16) that also gives the tile-local digit starts. So
-// no atomic leaves the CU, and the partial lines of a chain are only ever
-// written by one CU (one L2). Each fresh chunk's (digit, rank in its chain)
-// goes to a log; k_priv_offsets / k_priv_finish / k_priv_list turn the logs
-// into per-digit chunk lists, which the probe reads 64 chunks (one per wave
-// row) per tile. Reference: the per-worker scatter of HashJoin.hpp:394-412
-// (same partition contents; order inside a partition unspecified).
-// ---------------------------------------------------------------------------
-constexpr uint32_t kPrivCh = 64;         // slots per chunk = lanes of a probe row
-constexpr uint32_t kPrivRankBits = 21;   // log entry: (digit << 21) | rank in chain
-
-__host__ __device__ constexpr size_t scatter_priv_lds_bytes(int T, uint32_t nb) {
-    return static_cast<size_t>(T) * (nb <= 256 ? 17 : 18) + static_cast<size_t>((nb + 3u) & ~3u) * 4 +
-           static_cast<size_t>(nb) * 16 + 64;
-}
-
-struct PrivArgs {
-    uint32_t* log;       // [chunk id] (digit << kPrivRankBits) | rank of the chunk in its chain
-    uint32_t* ccount;    // [wg][nb] chunks of chain (wg, d)
-    uint32_t* clast;     // [wg][nb] its last chunk
-    uint32_t* cfill;     // [wg][nb] tuples in that chunk (1..64; 0 for an empty chain)
-    uint32_t* nused;     // [wg] chunks taken
-    uint32_t rchunks;    // chunks reserved per workgroup (>= per * T / 64 + nb)
-    uint32_t per;        // tiles per workgroup
-    uint32_t ntiles;
-    uint32_t pad;
-};
-
-template <int BLOCK, int ITEMS, int HK>
-__global__ __launch_bounds__(BLOCK)
-__attribute__((amdgpu_waves_per_eu((BLOCK * ITEMS <= 4096 ? 2 : 1) * BLOCK / 256)))   // what the LDS lets share a CU
-void k_scatter_priv(PassArgs a, PrivArgs q) {
-    constexpr int NW = BLOCK / 64;
-    constexpr int T = BLOCK * ITEMS;
-    constexpr uint32_t CH = kPrivCh;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const uint32_t nb = a.nbins;
-    longlong2* stup = reinterpret_cast<longlong2*>(smem);                    // [T] the sorted tile
-    uint32_t* wcnt = reinterpret_cast<uint32_t*>(stup + T);                  // [nb] counts, then starts
-    uint4* wdesc = reinterpret_cast<uint4*>(wcnt + ((nb + 3u) & ~3u));       // [nb] {k < split: slot - k, else, split}
-    uint32_t* tmp = reinterpret_cast<uint32_t*>(wdesc + nb);                 // 16 words
-    const SortedDigits sdig{tmp + 16, nb <= 256};                            // [T]
-
-    const uint32_t w = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const uint32_t rb = w * q.rchunks;
-    uint32_t tile = w * q.per;
-    const uint32_t t_end = min(q.ntiles, tile + q.per);
-    const uint32_t wbase = wave * 64 * ITEMS;
-    uint32_t cur = 0, fill = CH, cc = 0, nxt = 0;   // chain (w, tid); fill == CH: no open chunk
-    int64_t key[ITEMS], pay[ITEMS];
-    const longlong2* rel = reinterpret_cast<const longlong2*>(a.in_keys);
-    auto load = [&](uint32_t t) {
-        const uint32_t lo = t * T;
-#pragma unroll
-        for (int i = 0; i < ITEMS; i++) {
-            const uint32_t ix = min(lo + wbase + i * 64 + lane, a.n - 1);
-            if (a.nt_load) {
-                typedef long long v2i __attribute__((ext_vector_type(2)));
-                const v2i v = __builtin_nontemporal_load(reinterpret_cast<const v2i*>(rel) + ix);
-                key[i] = v.x;
-                pay[i] = v.y;
-            } else {
-                const longlong2 v = rel[ix];
-                key[i] = v.x;
-                pay[i] = v.y;
-            }
-        }
-    };
-    if (tile < t_end) load(tile);
-    while (tile < t_end) {
-        const uint32_t lo = tile * T, cnt = min(static_cast<uint32_t>(T), a.n - lo);
-        for (uint32_t i = tid; i < nb; i += BLOCK) wcnt[i] = 0;
-        __syncthreads();
-        uint32_t dig[ITEMS], rank[ITEMS];
-#pragma unroll
-        for (int i = 0; i < ITEMS; i++) {
-            const uint32_t e = wbase + i * 64 + lane;
-            const bool valid = e < cnt;
-            const uint32_t d = valid ? digit_of<HK>(static_cast<uint64_t>(key[i]), a.f) : 0u;
-            dig[i] = d;
-            rank[i] = valid ? atomicAdd(&wcnt[d], 1u) : 0u;
-        }
-        __syncthreads();
-        const uint32_t c = tid < nb ? wcnt[tid] : 0u;
-        const uint32_t room = CH - fill;
-        const uint32_t m = c > room ? (c - room + CH - 1) / CH : 0u;
-        uint32_t tot;
-        const uint32_t ex = block_exclusive_scan_t<NW>(c | (m << 16), tmp, tot);
-        if (tid < nb && c) {
-            const uint32_t ds = ex & 0xffffu, nbase = rb + nxt + (ex >> 16);
-            wcnt[tid] = ds;
-            wdesc[tid] = make_uint4(cur * CH + fill - ds, nbase * CH - (ds + room), ds + room, 0u);
-            for (uint32_t j = 0; j < m; j++) q.log[nbase + j] = (tid << kPrivRankBits) | (cc + j);
-            if (m) {
-                cur = nbase + m - 1;
-                fill = c - room - (m - 1) * CH;
-                cc += m;
-            } else {
-                fill += c;
-            }
-        }
-        nxt += tot >> 16;
-        __syncthreads();
-#pragma unroll
-        for (int i = 0; i < ITEMS; i++) {
-            const uint32_t e = wbase + i * 64 + lane;
-            if (e < cnt) {
-                const uint32_t pos = wcnt[dig[i]] + rank[i];
-                stup[pos] = make_longlong2(key[i], pay[i]);
-                sdig.put(pos, dig[i]);
-            }
-        }
-        const uint32_t next = tile + 1;
-        load(next < t_end ? next : tile);   // unconditional (a last one goes unused)
-        __syncthreads();
-#pragma unroll
-        for (int i = 0; i < ITEMS; i++) {
-            const uint32_t k = i * BLOCK + tid;
-            if (k < cnt) {
-                const uint4 wd = wdesc[sdig.get(k)];
-                const longlong2 t = stup[k];
-                store_tuple<true>(a, (k < wd.z ? wd.x : wd.y) + k, t.x, t.y);
-            }
-        }
-        tile = next;
-        __syncthreads();   // LDS reads of this tile before the next tile's counts
-    }
-    for (uint32_t d = tid; d < nb; d += BLOCK) {   // d == tid (host: nb <= BLOCK)
-        const size_t i = static_cast<size_t>(w) * nb + d;
-        q.ccount[i] = cc;
-        q.clast[i] = cur;
-        q.cfill[i] = cc ? fill : 0u;
-    }
-    if (tid == 0) q.nused[w] = nxt;
-}
-
-// Per digit d (one workgroup each): offw[d][w] = chunks of chains (w' < w, d),
-// nch[d] = chunks of digit d, ntup[d] = its tuples.
-__global__ __launch_bounds__(kBlock) void k_priv_offsets(const uint32_t* ccount, const uint32_t* cfill, uint32_t G,
-                                                         uint32_t nb, uint32_t* offw, uint32_t* nch, uint32_t* ntup) {
-    __shared__ uint32_t tmp[16];
-    const uint32_t d = blockIdx.x, tid = threadIdx.x;
-    uint32_t carry = 0, tup = 0;
-    for (uint32_t w0 = 0; w0 < G; w0 += kBlock) {
-        const uint32_t w = w0 + tid;
-        const uint32_t v = w < G ? ccount[static_cast<size_t>(w) * nb + d] : 0u;
-        if (v) tup += (v - 1) * kPrivCh + cfill[static_cast<size_t>(w) * nb + d];
-        uint32_t tot;
-        const uint32_t ex = block_exclusive_scan(v, tmp, tot);
-        if (w < G) offw[static_cast<size_t>(d) * G + w] = carry + ex;
-        carry += tot;
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) tup += __shfl_xor(tup, o, 64);
-    if ((tid & 63) == 0) tmp[tid >> 6] = tup;
-    __syncthreads();
-    if (tid == 0) {
-        uint32_t t = 0;
-        for (int i = 0; i < kWaves; i++) t += tmp[i];
-        nch[d] = carry;
-        ntup[d] = t;
-    }
-}
-
-// One workgroup, nb <= 1024: ebase = exclusive scan of nch (entry offsets),
-// tile_base2 = exclusive scan of ceil(nch / 64) (probe tiles of 64 chunks),
-// bounds1 = exclusive scan of ntup (the pass-1 partition bounds).
-__global__ __launch_bounds__(1024) void k_priv_finish(const uint32_t* nch, const uint32_t* ntup, uint32_t nb,
-                                                      uint32_t* ebase, uint32_t* tile_base2, uint32_t* bounds1) {
-    __shared__ uint32_t tmp[3][16];
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    uint32_t v[3] = {0, 0, 0};
-    if (tid < nb) {
-        v[0] = nch[tid];
-        v[1] = (v[0] + 63) / 64;
-        v[2] = ntup[tid];
-    }
-    uint32_t x[3] = {v[0], v[1], v[2]};
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-#pragma unroll
-        for (int j = 0; j < 3; j++) {
-            const uint32_t y = __shfl_up(x[j], o, 64);
-            if (lane >= (uint32_t)o) x[j] += y;
-        }
-    }
-    if (lane == 63) {
-#pragma unroll
-        for (int j = 0; j < 3; j++) tmp[j][wave] = x[j];
-    }
-    __syncthreads();
-    uint32_t b[3] = {0, 0, 0};
-    for (uint32_t w = 0; w < wave; w++) {
-#pragma unroll
-        for (int j = 0; j < 3; j++) b[j] += tmp[j][w];
-    }
-    if (tid < nb) {
-        ebase[tid] = b[0] + x[0] - v[0];
-        tile_base2[tid] = b[1] + x[1] - v[1];
-        bounds1[tid] = b[2] + x[2] - v[2];
-    }
-    if (tid == 1023) {
-        ebase[nb] = b[0] + x[0];
-        tile_base2[nb] = b[1] + x[1];
-        bounds1[nb] = b[2] + x[2];
-    }
-}
-
-// Every taken chunk g of workgroup w lands in its digit's list at
-// ebase[d] + offw[d][w] + rank: entry (g << 6) | (fill - 1).
-__global__ __launch_bounds__(kBlock) void k_priv_list(const uint32_t* log, const uint32_t* nused, const uint32_t* clast,
-                                                      const uint32_t* cfill, const uint32_t* offw, const uint32_t* ebase,
-                                                      uint32_t G, uint32_t nb, uint32_t rchunks, uint32_t* ent) {
-    const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
-    const uint32_t w = g / rchunks;
-    if (w >= G || g - w * rchunks >= nused[w]) return;
-    const uint32_t e = log[g];
-    const uint32_t d = e >> kPrivRankBits, r = e & ((1u << kPrivRankBits) - 1);
-    const size_t cw = static_cast<size_t>(w) * nb + d;
-    const uint32_t fill = g == clast[cw] ? cfill[cw] : kPrivCh;
-    ent[ebase[d] + offw[static_cast<size_t>(d) * G + w] + r] = (g << 6) | (fill - 1);
-}
-
-// ---------------------------------------------------------------------------
-// Flat exclusive scan of uint32 arrays (batched: blockIdx.y selects array).
-// ---------------------------------------------------------------------------
 constexpr int kScanItems = 16;
 constexpr int kScanBlockElems = kBlock * kScanItems;  // 4096
 

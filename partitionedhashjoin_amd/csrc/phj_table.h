@@ -58,24 +58,9 @@ __host__ __device__ __forceinline__ uint32_t ht_cap(uint32_t m) {
 
 __host__ __device__ __forceinline__ uint64_t ht_empty(uint32_t p) { return p == 0 ? 1ull : 0ull; }
 
-// Rank of this lane's digit d among the tile's keys of digit d (counter row C
-// in LDS). The lanes sharing the wave's first active digit take one atomic
-// together (a hot key's digit no longer serialises 64-way), the others one
-// each. Every lane calls it (ballots); d is computed on invalid lanes too.
-__device__ __forceinline__ uint32_t agg_rank(uint32_t* C, uint32_t d, bool valid) {
-    const uint64_t act = __ballot(valid);
-    if (act == 0) return 0;
-    const int leader = __builtin_ctzll(act);
-    const uint32_t ld = __builtin_amdgcn_readlane(d, leader);
-    const bool mine = valid && d == ld;
-    const uint64_t same = __ballot(mine);
-    const uint32_t lane = threadIdx.x & 63;
-    uint32_t base = 0;
-    if (lane == static_cast<uint32_t>(leader)) base = atomicAdd(&C[ld], static_cast<uint32_t>(__popcll(same)));
-    base = __builtin_amdgcn_readlane(base, leader);
-    if (mine) return base + static_cast<uint32_t>(__popcll(same & lanemask_lt()));
-    return valid ? atomicAdd(&C[d], 1u) : 0u;
-}
+// Rank of this lane's digit d among the tile's keys of digit d (counter row
+// C): phj_partition.h agg_rank_lds.
+__device__ __forceinline__ uint32_t agg_rank(uint32_t* C, uint32_t d, bool valid) { return agg_rank_lds(C, d, valid); }
 
 
 // ---------------------------------------------------------------------------
@@ -181,8 +166,7 @@ __global__ __launch_bounds__(BLOCK) void k_scatter_codes(PassArgs a) {
 // ---------------------------------------------------------------------------
 constexpr uint32_t kHtTpd = 16;      // R pass-2 workgroups per pass-1 digit
 constexpr uint32_t kHtLcap = 512;    // k_ht_fill: LDS table slots per wave
-constexpr uint32_t kHtPpw = 16;      // k_ht_fill: partitions per workgroup
-constexpr uint32_t kHtLcodes = 4096; // k_ht_fill: staged codes per workgroup (more: read in place)
+constexpr uint32_t kHtPpw = 8;       // k_ht_fill: partitions per workgroup (two per wave)
 constexpr uint32_t kHtUnr = 8;       // codes per thread in flight
 
 // R pass 2 over one relation's pass-1 output (codes contiguous per d1).
@@ -265,8 +249,15 @@ struct HtArgs {
 };
 
 __device__ __forceinline__ uint32_t ht_part_size(const HtArgs& a, uint32_t p) {
+    uint32_t lo[kHtSegs], hi[kHtSegs];   // every segment's bounds requested together
+#pragma unroll
+    for (uint32_t g = 0; g < kHtSegs; g++) {
+        lo[g] = g < a.nseg ? a.bounds[g][p] : 0u;
+        hi[g] = g < a.nseg ? a.bounds[g][p + 1] : 0u;
+    }
     uint32_t m = 0;
-    for (uint32_t g = 0; g < a.nseg; g++) m += a.bounds[g][p + 1] - a.bounds[g][p];
+#pragma unroll
+    for (uint32_t g = 0; g < kHtSegs; g++) m += hi[g] - lo[g];
     return m;
 }
 
@@ -305,73 +296,106 @@ __device__ __forceinline__ void ht_insert(uint64_t* tab, uint32_t bmask, uint64_
     }
 }
 
-// A workgroup per kHtPpw consecutive partitions: their codes from every
-// segment are staged in LDS (segment g's run at soff[g]), then wave w builds
-// partitions w, w + 4, ... in its LDS table slice and writes each out.
+// A workgroup per kHtPpw consecutive partitions (their bounds in every
+// segment staged in LDS in one round of loads), each wave builds partitions
+// w, w + 4, ... in its LDS table slice: the partition's codes (<= 8 per lane,
+// flattened over the segments) are all requested at once, every code claims a
+// slot of its home bucket with a 32-bit counter (slot 0 before slot 1, as the
+// probe assumes), codes finding their home bucket full (~7 % at load 2/3)
+// probe onwards with compare-and-swap, and the table is written out in 16-B
+// stores. Duplicates may take two slots: harmless to a set test, and the cap
+// counts them.
 __global__ __launch_bounds__(256) void k_ht_fill(HtArgs a) {
+    constexpr uint32_t CPL = kHtLcap * 2 / 3 / 64 + 1;   // codes per lane of a partition that fits the slice
     __shared__ __attribute__((aligned(16))) uint64_t wtab[4][kHtLcap];
-    __shared__ __attribute__((aligned(16))) int64_t scode[kHtLcodes];
-    __shared__ uint32_t soff[kHtSegs + 1], slo[kHtSegs];
+    __shared__ uint32_t wcnt[4][kHtLcap / 2];      // per-wave bucket fill counters
+    __shared__ uint32_t sb[kHtSegs][kHtPpw + 1];   // bounds of the workgroup's partitions, per segment
+    __shared__ uint32_t wpre[4][kHtSegs + 1];      // per wave: prefix of the current partition's runs
     const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const uint32_t nseg = a.nseg;
     const uint32_t P = a.nb1 * a.nb2;
-    const uint32_t p0 = blockIdx.x * kHtPpw, p1 = min(P, p0 + kHtPpw);
-    if (wave == 0) {
-        uint32_t lo = 0, n = 0;
-        if (lane < a.nseg) {
-            lo = a.bounds[lane][p0];
-            n = a.bounds[lane][p1] - lo;
-        }
-        uint32_t x = n;
-#pragma unroll
-        for (int o = 1; o < kHtSegs; o <<= 1) {
-            const uint32_t y = __shfl_up(x, o, 64);
-            if (lane >= static_cast<uint32_t>(o)) x += y;
-        }
-        if (lane < a.nseg) {
-            slo[lane] = lo;
-            soff[lane] = x - n;
-        }
-        if (lane == kHtSegs - 1) soff[a.nseg] = x;
+    const uint32_t p0 = blockIdx.x * kHtPpw, np = min(P - p0, kHtPpw);
+    for (uint32_t t = tid; t < nseg * (kHtPpw + 1); t += 256) {
+        const uint32_t g = t / (kHtPpw + 1), j = t - g * (kHtPpw + 1);
+        sb[g][j] = a.bounds[g][p0 + min(j, np)];
     }
     __syncthreads();
-    const uint32_t ntot = soff[a.nseg];
-    const bool staged = ntot <= kHtLcodes;
-    if (staged) {
-        for (uint32_t g = 0; g < a.nseg; g++) {
-            const uint32_t n = soff[g + 1] - soff[g];
-            const int64_t* src = a.codes[g] + slo[g];
-            for (uint32_t j = tid; j < n; j += 256) scode[soff[g] + j] = src[j];
-        }
-    }
-    __syncthreads();
-    uint64_t* tab = wtab[wave];
-    for (uint32_t p = p0 + wave; p < p1; p += 4) {
+    for (uint32_t j = wave; j < np; j += 4) {
+        const uint32_t p = p0 + j;
         const uint2 ds = a.desc[p];
         const uint32_t cap = 2 * (ds.y + 1);
         const uint64_t e = ht_empty(p);
         uint64_t* out = a.table + ds.x;
-        const bool lds = cap <= kHtLcap;
-        uint64_t* t = lds ? tab : out;
-        for (uint32_t s = lane; s < cap; s += 64) t[s] = e;
-        if (lds) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-        else __threadfence();
-        __builtin_amdgcn_wave_barrier();
-        for (uint32_t g = 0; g < a.nseg; g++) {
-            const uint32_t b0 = a.bounds[g][p], b1e = a.bounds[g][p + 1];
-            for (uint32_t j = b0 + lane; j < b1e; j += 64) {
-                const uint64_t c = static_cast<uint64_t>(staged ? scode[soff[g] + (j - slo[g])] : a.codes[g][j]);
-                ht_insert(t, ds.y, e, c);
+        {
+            const uint32_t len = lane < nseg ? sb[lane][j + 1] - sb[lane][j] : 0u;
+            uint32_t x = len;
+#pragma unroll
+            for (int o = 1; o < kHtSegs; o <<= 1) {
+                const uint32_t y = __shfl_up(x, o, 64);
+                if (lane >= static_cast<uint32_t>(o)) x += y;
             }
+            if (lane < kHtSegs) wpre[wave][lane + 1] = x;
+            if (lane == 0) wpre[wave][0] = 0;
         }
-        if (lds) {
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t m = wpre[wave][nseg];
+        auto src_of = [&](uint32_t r) -> const int64_t* {
+            uint32_t g = 0;
+            while (g + 1 < nseg && r >= wpre[wave][g + 1]) g++;
+            return a.codes[g] + sb[g][j] + (r - wpre[wave][g]);
+        };
+        if (cap <= kHtLcap) {
+            uint64_t c[CPL];
+#pragma unroll
+            for (uint32_t i = 0; i < CPL; i++) {
+                const uint32_t r = i * 64 + lane;
+                c[i] = r < m ? static_cast<uint64_t>(*src_of(r)) : 0ull;
+            }
+            uint32_t* bc = wcnt[wave];
+            for (uint32_t sl = lane; sl < cap; sl += 64) wtab[wave][sl] = e;
+            for (uint32_t b = lane; b < cap / 2; b += 64) bc[b] = 0;
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            uint32_t ovf = 0;   // bit i: c[i] found its home bucket full
+#pragma unroll
+            for (uint32_t i = 0; i < CPL; i++) {
+                if (i * 64 + lane < m) {
+                    const uint32_t b = static_cast<uint32_t>(c[i] >> kHtBucketShift) & ds.y;
+                    const uint32_t k = atomicAdd(&bc[b], 1u);
+                    if (k < 2) wtab[wave][2 * b + k] = c[i];
+                    else ovf |= 1u << i;
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (uint32_t i = 0; i < CPL; i++) {
+                if ((ovf >> i) & 1u) {
+                    uint32_t b = static_cast<uint32_t>(c[i] >> kHtBucketShift) & ds.y;
+                    for (bool placed = false; !placed;) {
+                        b = (b + 1) & ds.y;
+#pragma unroll
+                        for (int k = 0; k < 2 && !placed; k++) {
+                            const uint64_t old = atomicCAS(reinterpret_cast<unsigned long long*>(&wtab[wave][2 * b + k]), e, c[i]);
+                            placed = old == e || old == c[i];
+                        }
+                    }
+                }
+            }
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
             __builtin_amdgcn_wave_barrier();
             ulonglong2* o2 = reinterpret_cast<ulonglong2*>(out);
-            const ulonglong2* t2 = reinterpret_cast<const ulonglong2*>(tab);
+            const ulonglong2* t2 = reinterpret_cast<const ulonglong2*>(wtab[wave]);
             for (uint32_t b = lane; b < cap / 2; b += 64) o2[b] = t2[b];
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        } else {   // a partition beyond the slice (adversarial inputs): device atomics in place
+            for (uint32_t sl = lane; sl < cap; sl += 64) out[sl] = e;
+            __threadfence();
             __builtin_amdgcn_wave_barrier();
+            for (uint32_t r = lane; r < m; r += 64) ht_insert(out, ds.y, e, static_cast<uint64_t>(*src_of(r)));
         }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -379,13 +403,21 @@ __global__ __launch_bounds__(256) void k_ht_fill(HtArgs a) {
 // On-chip probe: the probe side's pass 2 never lands in HBM. Persistent: XCD x
 // walks tiles [x, x + 1) * ntiles / 8 of the pass-1 output (tiles of one d1 are
 // contiguous, so an XCD's L2 holds the few d1 regions it probes), its
-// workgroups round-robin over them, and the next tile's keys load while the
-// current one is probed. A tile is grouped by d2 with one LDS atomic per key
-// (an unstable counting sort: neighbouring lanes then probe the same small
-// table, often the same cache line), the tile's nb2 descriptors are staged in
-// LDS when d1 changes, and every key probes PB slots at a time.
+// workgroups round-robin over them. Per 4096-key tile, three barriers:
+//   rank by d2 (agg_rank: LDS atomics, aggregated over a wave's lanes that
+//   share a digit, so a hot key does not serialise) | B1 | one wave scans the
+//   counts | B2 | scatter into skey (grouped by d2: neighbouring lanes probe
+//   the same small table, mostly the same cache line), issue the next tile's
+//   loads, clear the other counter row, stage the other descriptor buffer for
+//   the next tile's d1 | B3 | probe: every lane requests all its items' home
+//   buckets at once (only the 16-B buckets stay in registers; codes and
+//   descriptors are re-read from LDS), then items whose home bucket is full
+//   without a match walk on.
+// Counters and descriptors are double-buffered, so the next tile's ranking may
+// start while slower waves still probe this one (its scatter waits behind the
+// next B1 / B2, which every wave reaches only after its probe).
 // HK = kHashed when the pass-1 output holds codes (VAR 13), else the key is
-// hashed here (stable pass 1 of whole tuples).
+// hashed here (a stable pass 1 of whole tuples).
 // ---------------------------------------------------------------------------
 struct HtProbeArgs {
     PassArgs a;                  // the pass-2 tile mapping over the pass-1 output
@@ -397,250 +429,15 @@ struct HtProbeArgs {
     uint32_t pad;
 };
 
+constexpr int kProbeBlock = 1024, kProbeItems = 4;   // 16 waves, 4 keys per lane: a 4096-key tile
+
 __host__ __device__ constexpr size_t probe_ht_lds_bytes(int T, uint32_t nb) {
-    return static_cast<size_t>(T) * 8 + static_cast<size_t>(nb) * 12 + 64 + 16 + static_cast<size_t>(nb) * 4 * 8;
-}
-
-template <int BLOCK, int ITEMS, int HK, int PBN = 2, int WPE = 6, bool DIAG = false, int GMODE = 0>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void k_probe_ht(HtProbeArgs pa) {
-    constexpr int T = BLOCK * ITEMS;
-    constexpr int PB = PBN;   // probes in flight per lane
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const PassArgs& a = pa.a;
-    const uint32_t nb = a.nbins;
-    int64_t* skey = reinterpret_cast<int64_t*>(smem);
-    uint2* sdesc = reinterpret_cast<uint2*>(skey + T);          // [nb]
-    uint32_t* cnt_d = reinterpret_cast<uint32_t*>(sdesc + nb);   // [nb] counts, then starts
-    uint32_t* tmp = cnt_d + nb;                                  // 16 words
-    __shared__ uint32_t red[BLOCK / 64];
-
-    const uint32_t total = a.tile_base[a.nseg];
-    const uint32_t xcd = blockIdx.x & 7u, g8 = gridDim.x >> 3;
-    const uint32_t t_lo = static_cast<uint32_t>(static_cast<uint64_t>(total) * xcd / 8);
-    const uint32_t t_hi = static_cast<uint32_t>(static_cast<uint64_t>(total) * (xcd + 1) / 8);
-    uint32_t tile = t_lo + (blockIdx.x >> 3);
-    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    uint32_t hits = 0;
-    if (tile < t_hi) {
-        const uint32_t wbase = wave * 64 * ITEMS;
-        const longlong2* rel = reinterpret_cast<const longlong2*>(a.in_keys);
-        const bool soa = a.in_pays != nullptr || a.keys_only;   // key column, or AoS tuples
-        int64_t key[ITEMS];
-        uint32_t vm = 0, d1 = 0;   // vm bit i: item i holds a key
-        auto load = [&](uint32_t t, uint32_t& m, uint32_t& d) {
-            d = a.tile_seg[t];
-            m = 0;
-            TileLoc L;
-            locate_tile<T>(a, t, L);
-            const uint32_t c = L.hi - L.lo;
-#pragma unroll
-            for (int i = 0; i < ITEMS; i++) {
-                const uint32_t e = wbase + i * 64 + lane;
-                key[i] = e < c ? (soa ? a.in_keys[L.lo + e] : rel[L.lo + e].x) : 0;
-                m |= e < c ? (1u << i) : 0u;
-            }
-        };
-        load(tile, vm, d1);
-        uint32_t staged = 0xffffffffu;   // d1 whose descriptors sit in LDS
-        for (;;) {
-            const bool restage = d1 != staged;   // consecutive tiles mostly share d1
-            for (uint32_t d = tid; d < nb; d += BLOCK) {
-                cnt_d[d] = 0;
-                if (restage) sdesc[d] = pa.desc[static_cast<size_t>(d1) * pa.nb2 + d];
-            }
-            staged = d1;
-            __syncthreads();
-            uint32_t cnt;   // codes of the tile, grouped into [0, cnt)
-            if constexpr (GMODE == 1) {
-                // ungrouped (measurement): the codes in load order
-                cnt = 0;
-#pragma unroll
-                for (int i = 0; i < ITEMS; i++) {
-                    const uint32_t e = wbase + i * 64 + lane;
-                    if ((vm >> i) & 1u) skey[e] = static_cast<int64_t>(hash64<HK>(static_cast<uint64_t>(key[i]), pa.seed));
-                }
-                cnt = __syncthreads_count((vm & 1u) != 0) * 0;   // (barrier)
-                TileLoc L;
-                locate_tile<T>(a, tile, L);
-                cnt = L.hi - L.lo;
-            } else if constexpr (GMODE == 2) {
-                // match ranking: lanes of a wave sharing a digit are ranked with
-                // ballots (no LDS atomics: no serialisation on hot digits), one
-                // counter row per wave, then a scan over (digit, wave)
-                uint32_t* wrow = cnt_d + nb + 16;   // [NW][nb]
-                constexpr int NW = BLOCK / 64;
-                uint32_t* my = wrow + wave * nb;
-                for (uint32_t d = lane; d < nb; d += 64) my[d] = 0;
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-                __builtin_amdgcn_wave_barrier();
-                uint32_t dig[ITEMS], rank[ITEMS];
-#pragma unroll
-                for (int i = 0; i < ITEMS; i++) {
-                    const uint64_t h = hash64<HK>(static_cast<uint64_t>(key[i]), pa.seed);
-                    key[i] = static_cast<int64_t>(h);
-                    const bool valid = (vm >> i) & 1u;
-                    const uint32_t d = static_cast<uint32_t>(q_from_hash(h, a.f) >> a.f.shift) & a.f.dmask;
-                    const uint64_t peers = match_digit(d, valid, a.nbits);
-                    dig[i] = d;
-                    rank[i] = 0;
-                    if (valid) {
-                        const uint32_t before = my[d];
-                        const uint64_t lt = peers & lanemask_lt();
-                        rank[i] = before + __popcll(lt);
-                        if (lt == 0) my[d] = before + __popcll(peers);
-                    }
-                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-                    __builtin_amdgcn_wave_barrier();
-                }
-                __syncthreads();
-                {
-                    const uint32_t dpt = (nb + BLOCK - 1) / BLOCK, d0 = tid * dpt;
-                    uint32_t local = 0;
-                    for (uint32_t j = 0; j < dpt; j++)
-                        if (d0 + j < nb)
-#pragma unroll
-                            for (int w = 0; w < NW; w++) local += wrow[w * nb + d0 + j];
-                    uint32_t tot;
-                    uint32_t run = block_exclusive_scan_t<BLOCK / 64>(local, tmp, tot);
-                    cnt = tot;
-                    for (uint32_t j = 0; j < dpt; j++) {
-                        const uint32_t d = d0 + j;
-                        if (d < nb) {
-#pragma unroll
-                            for (int w = 0; w < NW; w++) {
-                                const uint32_t c = wrow[w * nb + d];
-                                wrow[w * nb + d] = run;
-                                run += c;
-                            }
-                        }
-                    }
-                }
-                __syncthreads();
-#pragma unroll
-                for (int i = 0; i < ITEMS; i++)
-                    if ((vm >> i) & 1u) skey[my[dig[i]] + rank[i]] = key[i];
-            } else {
-                uint32_t dig[ITEMS], rank[ITEMS];
-#pragma unroll
-                for (int i = 0; i < ITEMS; i++) {
-                    const uint64_t h = hash64<HK>(static_cast<uint64_t>(key[i]), pa.seed);
-                    key[i] = static_cast<int64_t>(h);
-                    dig[i] = static_cast<uint32_t>(q_from_hash(h, a.f) >> a.f.shift) & a.f.dmask;
-                    if ((vm >> i) & 1u) rank[i] = atomicAdd(&cnt_d[dig[i]], 1u);
-                }
-                __syncthreads();
-                {
-                    const uint32_t dpt = (nb + BLOCK - 1) / BLOCK, d0 = tid * dpt;
-                    uint32_t local = 0;
-                    for (uint32_t j = 0; j < dpt; j++)
-                        if (d0 + j < nb) local += cnt_d[d0 + j];
-                    uint32_t tot;
-                    uint32_t run = block_exclusive_scan_t<BLOCK / 64>(local, tmp, tot);
-                    cnt = tot;
-                    for (uint32_t j = 0; j < dpt; j++) {
-                        const uint32_t d = d0 + j;
-                        if (d < nb) {
-                            const uint32_t c = cnt_d[d];
-                            cnt_d[d] = run;
-                            run += c;
-                        }
-                    }
-                }
-                __syncthreads();
-#pragma unroll
-                for (int i = 0; i < ITEMS; i++)
-                    if ((vm >> i) & 1u) skey[cnt_d[dig[i]] + rank[i]] = key[i];
-            }
-            // the next tile's keys go out now, into the same registers
-            const uint32_t next = tile + g8;
-            uint32_t nvm = 0, nd1 = 0;
-            load(next < t_hi ? next : tile, nvm, nd1);
-            __syncthreads();
-            // E of partition (d1, d2): 1 for partition 0 only, else 0
-            const uint32_t e0 = d1 == 0 ? 1u : 0u;
-            const ulonglong2* tab2 = reinterpret_cast<const ulonglong2*>(pa.table);
-#pragma unroll
-            for (int i0 = 0; i0 < ITEMS; i0 += PB) {
-                uint64_t c[PB];
-                ulonglong2 v[PB];
-                uint32_t base[PB], bmask[PB], b[PB], ebits = 0, pend = 0;
-#pragma unroll
-                for (int i = 0; i < PB; i++) {
-                    const uint32_t k = (i0 + i) * BLOCK + tid;
-                    c[i] = 0;
-                    base[i] = 0;
-                    bmask[i] = 0;
-                    b[i] = 0;
-                    if (k < cnt) {
-                        c[i] = static_cast<uint64_t>(skey[k]);
-                        const uint32_t d2 = static_cast<uint32_t>(q_from_hash(c[i], a.f) >> a.f.shift) & a.f.dmask;
-                        const uint2 ds = sdesc[d2];
-                        base[i] = ds.x >> 1;   // bucket index of the table
-                        bmask[i] = ds.y;
-                        ebits |= (d2 == 0 ? e0 : 0u) << i;
-                        b[i] = static_cast<uint32_t>(c[i] >> kHtBucketShift) & bmask[i];
-                        pend |= 1u << i;
-                    }
-                }
-                if constexpr (DIAG) {   // measurement only: no table reads
-                    hits += __popc(pend);
-                    pend = 0;
-                }
-                // every pending probe reads its next bucket, all loads in flight together
-                while (pend) {
-#pragma unroll
-                    for (int i = 0; i < PB; i++)
-                        if ((pend >> i) & 1u) v[i] = tab2[base[i] + b[i]];
-#pragma unroll
-                    for (int i = 0; i < PB; i++) {
-                        if ((pend >> i) & 1u) {
-                            const uint64_t e = (ebits >> i) & 1u;
-                            const bool hit = v[i].x == c[i] || v[i].y == c[i];
-                            if (hit || v[i].y == e) {   // a match, or a bucket with an empty slot
-                                hits += hit ? 1u : 0u;
-                                pend &= ~(1u << i);
-                            } else {
-                                b[i] = (b[i] + 1u) & bmask[i];
-                            }
-                        }
-                    }
-                }
-            }
-            if (next >= t_hi) break;
-            tile = next;
-            vm = nvm;
-            d1 = nd1;
-            __syncthreads();   // LDS reads of this tile before the next tile's counts
-        }
-    }
-    uint32_t x = hits;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x += __shfl_down(x, o, 64);
-    if (lane == 0) red[wave] = x;
-    __syncthreads();
-    if (tid == 0) {
-        unsigned long long t = 0;
-        for (int w = 0; w < BLOCK / 64; w++) t += red[w];
-        if (t) atomicAdd(pa.count, t);
-    }
-}
-
-
-__host__ __device__ constexpr size_t probe_ht2_lds_bytes(int T, uint32_t nb) {
     return static_cast<size_t>(T) * 8 + static_cast<size_t>(nb) * 2 * 12 + 64;
 }
 
-// The probe loop with three barriers per tile: rank (aggregated LDS atomics)
-// | B1 | wave 0 scans the counts | B2 | scatter into skey, issue the next
-// tile's loads, clear the other counter row and stage the other descriptor
-// buffer for the next tile's d1 | B3 | probe. Counters and descriptors are
-// double-buffered, so the next tile's ranking may start while slower waves
-// still probe this one (its scatter waits behind the next B1 / B2, which every
-// wave reaches only after its probe).
-template <int BLOCK, int ITEMS, int HK, int PBN = 2, int WPE = 6, bool DIAG = false, bool ALL = false>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void k_probe_ht2(HtProbeArgs pa) {
+template <int BLOCK, int ITEMS, int HK>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void k_probe_ht(HtProbeArgs pa) {
     constexpr int T = BLOCK * ITEMS;
-    constexpr int PB = PBN;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const PassArgs& a = pa.a;
     const uint32_t nb = a.nbins;
@@ -734,91 +531,39 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                 sd[ob] = nd1;
             }
             __syncthreads();   // B3
-            const uint32_t e0 = d1 == 0 ? 1u : 0u;   // E of partition (d1, d2): 1 only for partition 0
+            const uint64_t e0 = d1 == 0 ? 1ull : 0ull;   // E of partition (d1, d2): 1 only for partition 0
             const ulonglong2* tab2 = reinterpret_cast<const ulonglong2*>(pa.table);
-            if constexpr (ALL) {
-                // every item's home bucket requested at once (only the 16-B
-                // buckets stay in registers; codes and descriptors are re-read
-                // from LDS), then the rare items whose home bucket is full
-                // without a match walk on one bucket at a time
-                ulonglong2 v[ITEMS];
+            ulonglong2 v[ITEMS];
 #pragma unroll
-                for (int i = 0; i < ITEMS; i++) {
-                    const uint32_t k = i * BLOCK + tid;
-                    v[i] = make_ulonglong2(0, 0);
-                    if (k < cnt) {
-                        const uint64_t c = static_cast<uint64_t>(skey[k]);
-                        const uint32_t d2 = static_cast<uint32_t>(q_from_hash(c, a.f) >> a.f.shift) & a.f.dmask;
-                        const uint2 ds = D[d2];
-                        v[i] = tab2[(ds.x >> 1) + (static_cast<uint32_t>(c >> kHtBucketShift) & ds.y)];
-                    }
-                }
-#pragma unroll
-                for (int i = 0; i < ITEMS; i++) {
-                    const uint32_t k = i * BLOCK + tid;
-                    if (k < cnt) {
-                        const uint64_t c = static_cast<uint64_t>(skey[k]);
-                        bool hit = v[i].x == c || v[i].y == c;
-                        const uint32_t d2 = static_cast<uint32_t>(q_from_hash(c, a.f) >> a.f.shift) & a.f.dmask;
-                        const uint64_t e = d2 == 0 ? e0 : 0u;
-                        if (!hit && v[i].y != e) {   // home bucket full, no match: walk on
-                            const uint2 ds = D[d2];
-                            uint32_t b = static_cast<uint32_t>(c >> kHtBucketShift) & ds.y;
-                            for (;;) {
-                                b = (b + 1) & ds.y;
-                                const ulonglong2 w = tab2[(ds.x >> 1) + b];
-                                hit = w.x == c || w.y == c;
-                                if (hit || w.y == e) break;
-                            }
-                        }
-                        hits += hit ? 1u : 0u;
-                    }
+            for (int i = 0; i < ITEMS; i++) {
+                const uint32_t k = i * BLOCK + tid;
+                v[i] = make_ulonglong2(0, 0);
+                if (k < cnt) {
+                    const uint64_t c = static_cast<uint64_t>(skey[k]);
+                    const uint32_t d2 = static_cast<uint32_t>(q_from_hash(c, a.f) >> a.f.shift) & a.f.dmask;
+                    const uint2 ds = D[d2];
+                    v[i] = tab2[(ds.x >> 1) + (static_cast<uint32_t>(c >> kHtBucketShift) & ds.y)];
                 }
             }
 #pragma unroll
-            for (int i0 = 0; i0 < (ALL ? 0 : ITEMS); i0 += PB) {
-                uint64_t c[PB];
-                ulonglong2 v[PB];
-                uint32_t base[PB], bmask[PB], b[PB], ebits = 0, pend = 0;
-#pragma unroll
-                for (int i = 0; i < PB; i++) {
-                    const uint32_t k = (i0 + i) * BLOCK + tid;
-                    c[i] = 0;
-                    base[i] = 0;
-                    bmask[i] = 0;
-                    b[i] = 0;
-                    if (k < cnt) {
-                        c[i] = static_cast<uint64_t>(skey[k]);
-                        const uint32_t d2 = static_cast<uint32_t>(q_from_hash(c[i], a.f) >> a.f.shift) & a.f.dmask;
+            for (int i = 0; i < ITEMS; i++) {
+                const uint32_t k = i * BLOCK + tid;
+                if (k < cnt) {
+                    const uint64_t c = static_cast<uint64_t>(skey[k]);
+                    bool hit = v[i].x == c || v[i].y == c;
+                    const uint32_t d2 = static_cast<uint32_t>(q_from_hash(c, a.f) >> a.f.shift) & a.f.dmask;
+                    const uint64_t e = d2 == 0 ? e0 : 0ull;
+                    if (!hit && v[i].y != e) {   // home bucket full, no match: walk on
                         const uint2 ds = D[d2];
-                        base[i] = ds.x >> 1;
-                        bmask[i] = ds.y;
-                        ebits |= (d2 == 0 ? e0 : 0u) << i;
-                        b[i] = static_cast<uint32_t>(c[i] >> kHtBucketShift) & bmask[i];
-                        pend |= 1u << i;
-                    }
-                }
-                if constexpr (DIAG) {
-                    hits += __popc(pend);
-                    pend = 0;
-                }
-                while (pend) {
-#pragma unroll
-                    for (int i = 0; i < PB; i++)
-                        if ((pend >> i) & 1u) v[i] = tab2[base[i] + b[i]];
-#pragma unroll
-                    for (int i = 0; i < PB; i++) {
-                        if ((pend >> i) & 1u) {
-                            const uint64_t e = (ebits >> i) & 1u;
-                            const bool hit = v[i].x == c[i] || v[i].y == c[i];
-                            if (hit || v[i].y == e) {
-                                hits += hit ? 1u : 0u;
-                                pend &= ~(1u << i);
-                            } else {
-                                b[i] = (b[i] + 1u) & bmask[i];
-                            }
+                        uint32_t b = static_cast<uint32_t>(c >> kHtBucketShift) & ds.y;
+                        for (;;) {
+                            b = (b + 1) & ds.y;
+                            const ulonglong2 w = tab2[(ds.x >> 1) + b];
+                            hit = w.x == c || w.y == c;
+                            if (hit || w.y == e) break;
                         }
                     }
+                    hits += hit ? 1u : 0u;
                 }
             }
             if (!more) break;

@@ -28,9 +28,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 # timer name -> kernel family doing its work (first match wins)
 FAMILIES = [
+    (re.compile(r"^R\.p2\.hist$"), re.compile(r"phj::k_ht_hist")),
+    (re.compile(r"^R\.p2\.scatter$"), re.compile(r"phj::k_ht_scatter")),
     (re.compile(r"\.hist$"), re.compile(r"phj::k_hist")),
     (re.compile(r"\.scatter$"), re.compile(r"phj::k_scatter")),
-    (re.compile(r"^build$"), re.compile(r"phj::k_(build_small|build_ht|join_fused)")),
+    (re.compile(r"^build$"), re.compile(r"phj::k_(build_small|ht_fill|join_fused)")),
     (re.compile(r"^probe$"), re.compile(r"phj::k_(probe|join_fused)")),
     (re.compile(r"^np\.build$"), re.compile(r"phj::k_np_build(?!_overflow)")),
     (re.compile(r"^np\.probe$"), re.compile(r"phj::k_np_probe")),
@@ -104,11 +106,28 @@ def collect(groups, config="c2", primary=10_000_000, secondary=200_000_000):
     return per
 
 
+# Memory-side read requests by size (one pass: 3 of the 4 TCC counters) and
+# WRITE_SIZE (its own pass). Calibrated on known byte counts
+# (scripts/pmc_calib.hip, profiles/r03_pmc_calib.json): coalesced 8- and 16-B
+# per lane reads arrive as 128-B requests (FETCH_SIZE reports them at half,
+# the MI355X_MICROARCH.md x2 correction), random L2 misses as 64-B requests
+# (FETCH_SIZE reports those in full, so FETCH_SIZE x 2 double-counts them);
+# WRITE_SIZE reads 8- and 16-B stores exactly.
+READ_COUNTERS = ["TCC_EA0_RDREQ_128B_sum", "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_RDREQ_32B_sum"]
+
+
 def hbm_bytes(per):
-    """FETCH_SIZE x 2 (gfx950 tallies 128-B streaming reads at 64 B) + WRITE_SIZE, KiB -> bytes."""
+    """HBM bytes per launch: 128 / 64 / 32 B per memory-side read request of
+    each size + WRITE_SIZE (KiB). Falls back to FETCH_SIZE x 2 + WRITE_SIZE
+    when the request-size counters were not collected."""
     out = {}
     for t, v in per.items():
-        if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
+        if "WRITE_SIZE" not in v:
+            continue
+        if all(k in v for k in READ_COUNTERS):
+            rd = 128 * v[READ_COUNTERS[0]] + 64 * v[READ_COUNTERS[1]] + 32 * v[READ_COUNTERS[2]]
+            out[t] = rd + v["WRITE_SIZE"] * 1024
+        elif "FETCH_SIZE" in v:
             out[t] = (2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024
     return out
 

@@ -123,3 +123,57 @@ def test_c1_nopartitioning_1m_16m(ctx):
     ctx.upload(phj.SIDE_PROBE, S)
     assert O.join_nopart(R, S, workers=1).matches == expect
     assert ctx.join(params).matches == expect
+
+
+def test_full_size_probe_pass1_codes_match_oracle(ctx):
+    # the keys-only hash-code pass 1 (k_scatter_chunked VAR 13) that the
+    # counting join consumes at full size, compared per pass-1 partition with
+    # the oracle's stable partition of the same relation (the reference's
+    # scatter, src/RadixCluster/HashJoin.hpp:394-412): bounds bit-exact, every
+    # partition the same multiset of codes h(k) (two wrapping checksums, and
+    # exact sorted equality on the hottest and three other partitions)
+    _, S, _ = _workload(ctx, NR, NS, 1.05, shift=0, neg_every=0)
+    p = phj.radix_params((8, 8), hash=phj.HASH_MURMUR3, seed=SEED)
+    out, b1, codes = ctx.probe_pass1(p)
+    assert codes and b1.shape[0] == 257
+    ref, rb = O.partition(S, 1 << 16, True, O.HASH_MURMUR3, SEED, workers=THREADS)
+    del S
+    assert np.array_equal(b1.astype(np.uint64), rb[::256])
+    rc = O.hash_keys(O.HASH_MURMUR3, ref[:, 0], SEED)
+    del ref
+    got = out.view(np.uint64)
+    b = b1.astype(np.int64)
+    with np.errstate(over="ignore"):
+        for mix in (lambda x: x, lambda x: (x ^ (x >> np.uint64(29))) * np.uint64(0xBF58476D1CE4E5B9)):
+            cg = np.zeros(NS + 1, dtype=np.uint64)
+            ce = np.zeros(NS + 1, dtype=np.uint64)
+            np.cumsum(mix(got), dtype=np.uint64, out=cg[1:])
+            np.cumsum(mix(rc), dtype=np.uint64, out=ce[1:])
+            assert np.array_equal(cg[b[1:]] - cg[b[:-1]], ce[b[1:]] - ce[b[:-1]])
+    sizes = np.diff(b)
+    for d in {int(np.argmax(sizes)), 0, 97, 255}:
+        assert np.array_equal(np.sort(got[b[d]:b[d + 1]]), np.sort(rc[b[d]:b[d + 1]])), d
+
+
+def test_full_size_duplicate_heavy_and_extreme_build_side(ctx):
+    # 10M build tuples with every key repeated 4x (2.5M distinct keys from
+    # 1 + SHIFT) and the extreme keys INT64_MIN / MAX, 0, -1 in R; S = the
+    # Zipf workload with every 7th key negated and the extremes planted
+    ext = np.array([np.iinfo(np.int64).min, np.iinfo(np.int64).max, 0, -1], dtype=np.int64)
+    keys = (np.arange(NR, dtype=np.int64) // 4) + 1 + SHIFT
+    keys[-4:] = ext
+    R = np.stack([keys, np.arange(NR, dtype=np.int64)], axis=1)
+    ctx.upload(phj.SIDE_BUILD, R)
+    ctx.generate_zipf(phj.SIDE_PROBE, NS, 1.05, 1, NR, GEN_SEED)
+    S = ctx.download(phj.SIDE_PROBE)
+    S[::NEG_EVERY, 0] = -S[::NEG_EVERY, 0]
+    S[5::1_000_003, 0] = np.resize(ext, S[5::1_000_003, 0].shape[0])
+    ctx.upload(phj.SIDE_PROBE, S)
+    sk = S[:, 0]
+    distinct_hi = (NR - 4 - 1) // 4 + 1 + SHIFT
+    expect = int(np.count_nonzero((sk > SHIFT) & (sk <= distinct_hi)) + np.count_nonzero(np.isin(sk, ext)))
+    assert O.semijoin_count(R, S, threads=THREADS) == expect
+    for params in (phj.radix_params((8, 8), hash=phj.HASH_MURMUR3, seed=SEED),
+                   phj.radix_params(num_partitions=1024, hash=phj.HASH_XXH3, seed=SEED),
+                   phj.nopart_params(hash=phj.HASH_XXH3, seed=SEED)):
+        assert ctx.join(params).matches == expect

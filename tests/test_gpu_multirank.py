@@ -108,3 +108,21 @@ def test_rccl_rank_context_world_of_one():
         # a one-device rank context also takes the building blocks
         v = ctx.partition(phj.SIDE_PROBE, phj.radix_params((8, 8)))
         assert v.n == nS
+
+
+def test_rehearsal_member_zero_joins_its_shard(monkeypatch):
+    # PHJ_REHEARSE (scripts/rehearse_world.py): members > 0 only feed the
+    # exchange, so the reported count is member 0's S shard against all of R
+    monkeypatch.setenv("PHJ_REHEARSE", "1")
+    R, S = O.generate_tables(50_000, 600_001, 1.05, 5, threads=4)
+    R[:, 0] += 7
+    S[::5, 0] = -S[::5, 0]
+    world = 3
+    lo, hi = shard_range(S.shape[0], 0, world)
+    expect = O.semijoin_count(R, S[lo:hi])
+    with phj.Context(devices=[0] * world, flags=phj.CTX_LOCAL) as g:
+        g.upload(phj.SIDE_BUILD, R)
+        g.upload(phj.SIDE_PROBE, S)
+        p = phj.radix_params((8, 8), hash=phj.HASH_MURMUR3, seed=SEED)
+        for _ in range(3):   # members > 0 pack once, then only take part in the exchange
+            assert g.join(p).matches == expect

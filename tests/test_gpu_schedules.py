@@ -5,12 +5,17 @@ between kernel schedules that must produce the same bytes: tile size
 (PHJ_TILE) and workgroup size (PHJ_BLOCK) of the histogram/scatter kernels,
 nontemporal stores (PHJ_NT), pass-1 output layout (PHJ_P1_AOS), the pass-2
 digit column (PHJ_DCOL), tile order
-(PHJ_XCD_REMAP), write-combining scatter (PHJ_WC), the one-pass limit of
-hash % P (PHJ_ONEPASS_MAX), the join's sub-partitioning of large partitions
-(PHJ_SUBPART), the chunked pass 1 of unordered partitions (PHJ_P1_CHUNK) and its
-persistent workgroups per shard (PHJ_P1_SLOTS), shard count (PHJ_P1_TPS) and tile ranking / LDS layout (PHJ_P1_VAR), the workgroup-private chains of the on-chip probe's pass 1 (PHJ_P1_PRIV), fused LDS join vs HBM tables (PHJ_FUSED), the
-partitioned bucket tables vs CSR tables (PHJ_PTAB) and the CSR probe
-schedule (PHJ_PROBE_WAVE, PHJ_PROBE_ITEMS). Each is
+(PHJ_XCD_REMAP), write-combining scatter (PHJ_WC, PHJ_WC_ITEMS, PHJ_WC_LW,
+PHJ_WC_WGS), the one-pass limit of hash % P (PHJ_ONEPASS_MAX), the join's
+sub-partitioning of large partitions (PHJ_SUBPART), the chunked pass 1 of
+unordered partitions (PHJ_P1_CHUNK) and its persistent workgroups per shard
+(PHJ_P1_SLOTS, PHJ_P1_WPC2), shard count (PHJ_P1_TPS, PHJ_P1_KO_TPS), size
+thresholds (PHJ_P1_MIN_TILES, PHJ_P1_KO_MIN_TILES) and tile ranking / LDS
+layout (PHJ_P1_VAR), the on-chip probe's input (PHJ_P2PROBE, PHJ_P1_KO,
+PHJ_P1_HCODE), fused LDS join vs HBM tables (PHJ_FUSED), the partitioned bucket
+tables vs CSR tables (PHJ_PTAB), the CSR probe schedule (PHJ_PROBE_WAVE,
+PHJ_PROBE_ITEMS) and the NoPartitioning probe (PHJ_NP_*). Every knob the
+context reads appears here (tests/test_tooling.py checks that). Each is
 checked against the oracle's stable partition (or, for the unordered layout,
 the same tuples in every partition) and semi-join count.
 """
@@ -38,7 +43,9 @@ SCHEDULES = [
     {"PHJ_DCOL": "0"},
     {"PHJ_XCD_REMAP": "0"},
     {"PHJ_NT": "1"},
-    {"PHJ_WC": "1"},
+    {"PHJ_WC": "1"},                                            # software write-combining scatter
+    {"PHJ_WC": "1", "PHJ_WC_ITEMS": "4", "PHJ_WC_LW": "16"},    # ... 4-item sub-tiles, 128-B lines
+    {"PHJ_WC": "1", "PHJ_WC_WGS": "64"},                        # ... few large super-tiles
     {"PHJ_PROBE_ITEMS": "16", "PHJ_PROBE_WAVE": "0", "PHJ_FUSED": "0", "PHJ_PTAB": "0"},
     {"PHJ_FUSED": "0", "PHJ_PTAB": "0", "PHJ_PROBE_WAVE": "0"},
     {"PHJ_FUSED": "0", "PHJ_PTAB": "0", "PHJ_PROBE_WAVE": "2"},
@@ -50,7 +57,7 @@ SCHEDULES = [
     {"PHJ_R_AUX": "0"},
     {"PHJ_TIMERS": "0"},
     {"PHJ_FUSED_KPL": "8"},
-    {"PHJ_P1_CHUNK": "0"},
+    {"PHJ_P1_CHUNK": "0"},                                      # on-chip probe over a stable pass 1 (raw keys)
     {"PHJ_P1_MIN_TILES": "0"},                                  # chunked pass 1 at every size
     {"PHJ_P1_MIN_TILES": "0", "PHJ_P1_SLOTS": "-1"},            # one tile per workgroup
     {"PHJ_P1_MIN_TILES": "0", "PHJ_P1_SLOTS": "3"},             # long persistent walks
@@ -65,24 +72,14 @@ SCHEDULES = [
     {"PHJ_NP_REGION": "0"},                                     # ... device-atomic build
     {"PHJ_NP_HOT": "0"},                                        # ... no hot-key LDS cache
     {"PHJ_NP_HOT_MIN": "0", "PHJ_NP_HOT_SAMPLES": "4096"},      # ... hot-key cache at every size
-    {"PHJ_NP_COOP": "1"},                                       # ... four lanes per bucket
     {"PHJ_P2PROBE": "0"},                                       # radix: probe side's pass 2 through HBM
     {"PHJ_P2PROBE": "0", "PHJ_P1_MIN_TILES": "0"},              # ... after the chunked pass 1
-    {"PHJ_P1_PRIV": "1"},                                       # on-chip probe after workgroup-private chains
-    {"PHJ_P1_PRIV": "1", "PHJ_P1_BITS": "5"},                   # ... pass split 5 + rest
-    {"PHJ_P1_BITS": "6"},
-    {"PHJ_P1_GRP": "0"},
-    {"PHJ_P1_HOME": "0"},                                       # on-chip probe: CSR offset pair + keys
-    {"PHJ_P1_WPC2": "0"},                                       # keys-only pass 1 on every LDS slot (3 per CU)
+    {"PHJ_P1_WPC2": "0"},                                       # keys-only pass 1 on every LDS slot
     {"PHJ_P1_WPC2": "1"},                                       # ... on half a workgroup per CU
-    {"PHJ_CU_SPLIT": "4"},                                      # R chain and S pass 1 on CU-masked streams
-    {"PHJ_P1_HOME": "2"},                                       # home slots from a separate pass (k_csr_home)
     {"PHJ_P1_HCODE": "0"},                                      # keys-only pass 1 writes raw keys (the probe hashes)
-    {"PHJ_P1_HCODE": "0", "PHJ_P1_HOME": "0"},                  # ... with the CSR offset-pair probe
-    {"PHJ_P1_GRP": "0"},                                        # ungrouped probe over hash codes
-    {"PHJ_P1_HOME": "0", "PHJ_P1_BSHIFT": "2"},                 # ... 4x the buckets
-    {"PHJ_P1_BSHIFT": "1"},                                     # home slots over 2x the buckets                                        # on-chip probe without the d2 grouping
-    {"PHJ_P1_KO": "0", "PHJ_P1_MIN_TILES": "0"},                # chunked pass 1 writes whole tuples for the probe                                       # shared chains, pass split 6 + rest
+    {"PHJ_P1_KO": "0", "PHJ_P1_MIN_TILES": "0"},                # chunked pass 1 writes whole tuples for the probe
+    {"PHJ_P1_KO_TPS": "4"},                                     # keys-only pass 1: 16 shards on small relations
+    {"PHJ_P1_KO_MIN_TILES": "1000000"},                         # ... never chunked: stable pass 1 of tuples
     {"PHJ_NP_RATIO": "1.25"},                                   # NoPartitioning default table ratio
     {"PHJ_P1_MIN_TILES": "0", "PHJ_P1_VAR": "0"},               # chunked pass 1: stable ballot ranking
     {"PHJ_P1_MIN_TILES": "0", "PHJ_P1_VAR": "1"},               # ... LDS-atomic ranking

@@ -35,6 +35,24 @@ def test_attribution_takes_the_last_join_in_order():
 def test_hbm_bytes_gfx950_correction():
     per = {"probe": {"FETCH_SIZE": 100.0, "WRITE_SIZE": 10.0}, "build": {"FETCH_SIZE": 1.0}}
     assert pmc.hbm_bytes(per) == {"probe": (200 + 10) * 1024}
+    # request-size counters (calibrated: 128-B streaming requests, 64-B random misses) win when present
+    per = {"probe": {"FETCH_SIZE": 100.0, "WRITE_SIZE": 10.0, "TCC_EA0_RDREQ_128B_sum": 5.0,
+                     "TCC_EA0_RDREQ_64B_sum": 3.0, "TCC_EA0_RDREQ_32B_sum": 1.0}}
+    assert pmc.hbm_bytes(per) == {"probe": 5 * 128 + 3 * 64 + 32 + 10 * 1024}
+
+
+def test_every_tuning_knob_has_a_schedule_test():
+    # every PHJ_* variable the library reads selects a schedule that
+    # tests/test_gpu_schedules.py runs (PHJ_REHEARSE: tests/test_gpu_multirank.py)
+    import glob
+    import re
+    src = "".join(open(f).read() for f in glob.glob(os.path.join(ROOT, "partitionedhashjoin_amd", "csrc", "*")))
+    knobs = set(re.findall(r'(?:env_int|getenv)\("(PHJ_[A-Z0-9_]+)"', src))
+    tested = open(os.path.join(ROOT, "tests", "test_gpu_schedules.py")).read() + \
+        open(os.path.join(ROOT, "tests", "test_gpu_multirank.py")).read()
+    assert knobs, "no knobs found"
+    missing = sorted(k for k in knobs if f'"{k}"' not in tested)
+    assert not missing, missing
 
 
 def test_fused_join_is_one_dispatch_for_build_and_probe():
