@@ -500,7 +500,7 @@ int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const st
             if (c->tune.p1_slots > 0) slots = std::min<uint32_t>(per, c->tune.p1_slots);
             if (c->tune.p1_slots < 0) slots = per;   // one tile per workgroup
             const void* kfn = nullptr;
-            switch (a.keys_only ? (c->tune.p1_hcode ? (env_int("PHJ_P1_NOCLAIM", 0) ? 29 : 13) : 5) : (c->tune.p1_var & 3)) {
+            switch (a.keys_only ? (c->tune.p1_hcode ? 13 : 5) : (c->tune.p1_var & 3)) {
 #define PHJ_P1_VARIANT(V)                                                                            \
     case V:                                                                                          \
         kfn = hk == kMurmur3 ? reinterpret_cast<const void*>(&k_scatter_chunked<BLOCK, ITEMS, kMurmur3, V>) \
@@ -512,7 +512,6 @@ int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const st
                 PHJ_P1_VARIANT(3)
                 PHJ_P1_VARIANT(5)
                 PHJ_P1_VARIANT(13)
-                PHJ_P1_VARIANT(29)
 #undef PHJ_P1_VARIANT
             }
             PassArgs ak = a;

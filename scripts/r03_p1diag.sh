@@ -5,7 +5,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 9
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-for env in "PHJ_P1_WPC2=2" "PHJ_P1_WPC2=2 PHJ_P1_NOCLAIM=1" "PHJ_P1_WPC2=0" "PHJ_P1_WPC2=0 PHJ_P1_NOCLAIM=1"; do
+for env in "PHJ_P1_WPC2=2" "PHJ_P1_WPC2=2 PHJ_P1_PLAINRANK=1" "PHJ_P1_WPC2=2 PHJ_P1_NOCLAIM=1" "PHJ_P1_WPC2=3" "PHJ_P1_WPC2=3 PHJ_P1_PLAINRANK=1" "PHJ_P1_WPC2=0" "PHJ_P1_WPC2=0 PHJ_P1_NOCLAIM=1"; do
   tag=$(echo $env | tr ' =' '_-')
   env $env timeout -k 10 300 python bench.py --config c2 --no-cpu-baseline --no-traffic --steps 10 > gpurun_out/p1d_$tag.json 2> gpurun_out/p1d_$tag.err || { echo "bench $env failed"; tail -5 gpurun_out/p1d_$tag.err; exit 2; }
   python -c "import json; d=json.load(open('gpurun_out/p1d_$tag.json')); print('$env', round(d['ms_per_step'],3), d['correct'], d['kernels_ms'])"
