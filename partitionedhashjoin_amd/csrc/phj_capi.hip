@@ -1262,7 +1262,10 @@ int probe_ht(phj_ctx* c, const Plan& pl) {
     constexpr int B = kProbeBlock, I = kProbeItems;
     const size_t lds = probe_ht_lds_bytes(B * I, pl.nb2);
     // a keys-only pass 1 wrote codes (VAR 13); a stable pass 1 left whole tuples
-    const void* kfn = PS.hcoded ? reinterpret_cast<const void*>(&k_probe_ht<B, I, kHashed>)
+    // (the chunked pass-1 output is always codes; a radix plan's d2 is a bit field)
+    const bool radix = pl.mode == 0 && pl.sub_bits == 0;
+    const void* kfn = PS.hcoded ? (radix ? reinterpret_cast<const void*>(&k_probe_ht<B, I, kHashed, kProbeRadix | kProbeChunked>)
+                                         : reinterpret_cast<const void*>(&k_probe_ht<B, I, kHashed, kProbeChunked>))
                       : pl.hk == kMurmur3 ? reinterpret_cast<const void*>(&k_probe_ht<B, I, kMurmur3>)
                                           : reinterpret_cast<const void*>(&k_probe_ht<B, I, kXXH3>);
     // persistent: as many workgroups as fit the chip at once (a multiple of 8:

@@ -432,17 +432,25 @@ struct HtProbeArgs {
 constexpr int kProbeBlock = 1024, kProbeItems = 4;   // 16 waves, 4 keys per lane: a 4096-key tile
 
 __host__ __device__ constexpr size_t probe_ht_lds_bytes(int T, uint32_t nb) {
-    return static_cast<size_t>(T) * 8 + static_cast<size_t>(nb) * 2 * 12 + 64;
+    return static_cast<size_t>(T + 2) * 8 + static_cast<size_t>(nb) * 2 * 12 + 64;
 }
 
-template <int BLOCK, int ITEMS, int HK>
+// FORM bit 0 (kProbeRadix): the radix digit of a code is a plain bit field,
+// d2 = (c >> shift) & dmask (no h % P, no sub-partition bits); bit 1
+// (kProbeChunked): the input is the chunked keys-only pass 1 (a code column,
+// tile t = chunk [tile_start[t], + tile_cnt[t])). Both drop the run-time mode
+// branches and the kernel-argument state they keep live.
+constexpr int kProbeRadix = 1, kProbeChunked = 2;
+
+template <int BLOCK, int ITEMS, int HK, int FORM = 0>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void k_probe_ht(HtProbeArgs pa) {
     constexpr int T = BLOCK * ITEMS;
+    constexpr bool RADIX = (FORM & kProbeRadix) != 0, CHUNKED = (FORM & kProbeChunked) != 0;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const PassArgs& a = pa.a;
     const uint32_t nb = a.nbins;
-    int64_t* skey = reinterpret_cast<int64_t*>(smem);
-    uint2* sdesc = reinterpret_cast<uint2*>(skey + T);             // [2][nb]
+    int64_t* skey = reinterpret_cast<int64_t*>(smem);              // [T + 2]: slot T takes invalid lanes' writes
+    uint2* sdesc = reinterpret_cast<uint2*>(skey + T + 2);         // [2][nb]
     uint32_t* cntb = reinterpret_cast<uint32_t*>(sdesc + 2 * nb);   // [2][nb]
     __shared__ uint32_t red[BLOCK / 64];
     __shared__ uint32_t tot_s;
@@ -457,19 +465,30 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
     if (tile < t_hi) {   // block-uniform
         const uint32_t wbase = wave * 64 * ITEMS;
         const longlong2* rel = reinterpret_cast<const longlong2*>(a.in_keys);
-        const bool soa = a.in_pays != nullptr || a.keys_only;
+        const bool soa = CHUNKED || a.in_pays != nullptr || a.keys_only;
+        auto d2_of = [&](uint64_t c) -> uint32_t {
+            if constexpr (RADIX) return static_cast<uint32_t>(c >> a.f.shift) & a.f.dmask;
+            return static_cast<uint32_t>(q_from_hash(c, a.f) >> a.f.shift) & a.f.dmask;
+        };
         int64_t key[ITEMS];
         uint32_t vm = 0, d1 = 0;
         auto load = [&](uint32_t t, uint32_t& m, uint32_t& d) {
             d = a.tile_seg[t];
             m = 0;
-            TileLoc L;
-            locate_tile<T>(a, t, L);
-            const uint32_t c = L.hi - L.lo;
+            uint32_t lo, c;
+            if constexpr (CHUNKED) {
+                lo = a.tile_start[t];
+                c = a.tile_cnt[t];
+            } else {
+                TileLoc L;
+                locate_tile<T>(a, t, L);
+                lo = L.lo;
+                c = L.hi - L.lo;
+            }
 #pragma unroll
             for (int i = 0; i < ITEMS; i++) {
                 const uint32_t e = wbase + i * 64 + lane;
-                key[i] = e < c ? (soa ? a.in_keys[L.lo + e] : rel[L.lo + e].x) : 0;
+                key[i] = e < c ? (soa ? a.in_keys[lo + e] : rel[lo + e].x) : 0;
                 m |= e < c ? (1u << i) : 0u;
             }
         };
@@ -490,35 +509,53 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
             for (int i = 0; i < ITEMS; i++) {
                 const uint64_t h = hash64<HK>(static_cast<uint64_t>(key[i]), pa.seed);
                 key[i] = static_cast<int64_t>(h);
-                dig[i] = static_cast<uint32_t>(q_from_hash(h, a.f) >> a.f.shift) & a.f.dmask;
+                dig[i] = d2_of(h);
                 rank[i] = agg_rank(C, dig[i], (vm >> i) & 1u);
             }
             __syncthreads();   // B1
             if (wave == 0) {   // exclusive scan of the counts by one wave
-                const uint32_t per = (nb + 63) / 64, d0 = lane * per;
-                uint32_t local = 0;
-                for (uint32_t j = 0; j < per; j++)
-                    if (d0 + j < nb) local += C[d0 + j];
-                uint32_t x = local;
+                if (nb == 256) {   // the common 8-bit d2: one 16-B LDS read per lane
+                    uint4 q = reinterpret_cast<uint4*>(C)[lane];
+                    const uint32_t local = q.x + q.y + q.z + q.w;
+                    uint32_t x = local;
 #pragma unroll
-                for (int o = 1; o < 64; o <<= 1) {
-                    const uint32_t y = __shfl_up(x, o, 64);
-                    if (lane >= static_cast<uint32_t>(o)) x += y;
-                }
-                uint32_t run = x - local;
-                for (uint32_t j = 0; j < per; j++)
-                    if (d0 + j < nb) {
-                        const uint32_t c = C[d0 + j];
-                        C[d0 + j] = run;
-                        run += c;
+                    for (int o = 1; o < 64; o <<= 1) {
+                        const uint32_t y = __shfl_up(x, o, 64);
+                        if (lane >= static_cast<uint32_t>(o)) x += y;
                     }
-                if (lane == 63) tot_s = x;
+                    const uint32_t r0 = x - local;
+                    reinterpret_cast<uint4*>(C)[lane] = make_uint4(r0, r0 + q.x, r0 + q.x + q.y, r0 + q.x + q.y + q.z);
+                    if (lane == 63) tot_s = x;
+                } else {
+                    const uint32_t per = (nb + 63) / 64, d0 = lane * per;
+                    uint32_t local = 0;
+                    for (uint32_t j = 0; j < per; j++)
+                        if (d0 + j < nb) local += C[d0 + j];
+                    uint32_t x = local;
+#pragma unroll
+                    for (int o = 1; o < 64; o <<= 1) {
+                        const uint32_t y = __shfl_up(x, o, 64);
+                        if (lane >= static_cast<uint32_t>(o)) x += y;
+                    }
+                    uint32_t run = x - local;
+                    for (uint32_t j = 0; j < per; j++)
+                        if (d0 + j < nb) {
+                            const uint32_t c = C[d0 + j];
+                            C[d0 + j] = run;
+                            run += c;
+                        }
+                    if (lane == 63) tot_s = x;
+                }
             }
             __syncthreads();   // B2
             const uint32_t cnt = tot_s;
+            {   // branch-free: the counter reads all go out before the writes
+                uint32_t pos[ITEMS];
 #pragma unroll
-            for (int i = 0; i < ITEMS; i++)
-                if ((vm >> i) & 1u) skey[C[dig[i]] + rank[i]] = key[i];
+                for (int i = 0; i < ITEMS; i++) pos[i] = C[dig[i]];
+#pragma unroll
+                for (int i = 0; i < ITEMS; i++) skey[((vm >> i) & 1u) ? pos[i] + rank[i] : static_cast<uint32_t>(T)] = key[i];   // slot T: a sink
+            }
             const uint32_t next = tile + g8;
             const bool more = next < t_hi;
             uint32_t nvm = 0, nd1 = d1;
@@ -531,6 +568,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
                 sd[ob] = nd1;
             }
             __syncthreads();   // B3
+            // probe: all items' home buckets in flight at once, then the walks
+            // of every item still pending advance together, one bucket a round
             const uint64_t e0 = d1 == 0 ? 1ull : 0ull;   // E of partition (d1, d2): 1 only for partition 0
             const ulonglong2* tab2 = reinterpret_cast<const ulonglong2*>(pa.table);
             ulonglong2 v[ITEMS];
@@ -540,8 +579,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
                 v[i] = make_ulonglong2(0, 0);
                 if (k < cnt) {
                     const uint64_t c = static_cast<uint64_t>(skey[k]);
-                    const uint32_t d2 = static_cast<uint32_t>(q_from_hash(c, a.f) >> a.f.shift) & a.f.dmask;
-                    const uint2 ds = D[d2];
+                    const uint2 ds = D[d2_of(c)];
                     v[i] = tab2[(ds.x >> 1) + (static_cast<uint32_t>(c >> kHtBucketShift) & ds.y)];
                 }
             }
@@ -551,7 +589,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
                 if (k < cnt) {
                     const uint64_t c = static_cast<uint64_t>(skey[k]);
                     bool hit = v[i].x == c || v[i].y == c;
-                    const uint32_t d2 = static_cast<uint32_t>(q_from_hash(c, a.f) >> a.f.shift) & a.f.dmask;
+                    const uint32_t d2 = d2_of(c);
                     const uint64_t e = d2 == 0 ? e0 : 0ull;
                     if (!hit && v[i].y != e) {   // home bucket full, no match: walk on
                         const uint2 ds = D[d2];
