@@ -178,7 +178,10 @@ int phj_relation_download(phj_ctx *ctx, int side, phj_tuple *host, uint64_t n);
  * per 4096-tuple batch. Rows [first_index, first_index + n) of the full
  * relation are generated (a range shard on multi-GPU; 0 = the whole table),
  * so shards concatenate to exactly the single-device relation. The Zipf
- * kernel uses the device libm pow; the host generator is the parity source. */
+ * kernel draws with phj_pow.h, a restatement of glibc's pow (the one the
+ * reference's std::pow calls) evaluated in glibc's FMA-build operation order,
+ * so its samples equal the host generator's and the reference's bit for bit
+ * (tests/test_gpu_generators.py). */
 int phj_relation_generate_sequential(phj_ctx *ctx, int side, uint64_t n, int64_t start,
                                      uint64_t first_index);
 int phj_relation_generate_zipf(phj_ctx *ctx, int side, uint64_t n, double alpha, int64_t lo,

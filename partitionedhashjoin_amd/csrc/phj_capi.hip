@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/phj.h"
@@ -488,17 +489,6 @@ int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const st
             const uint32_t ntiles = static_cast<uint32_t>((n + T - 1) / T);
             const uint32_t per = (ntiles + a.nshards - 1) / a.nshards;
             const size_t lds = a.keys_only ? sc_lds - static_cast<size_t>(T) * 8 : sc_lds;   // no payload rows
-            const uint32_t fit = std::max<uint32_t>(1, static_cast<uint32_t>(160 * 1024 / lds));
-            uint32_t slots = std::max<uint32_t>(1, std::min<uint32_t>(per, fit * c->num_cus / a.nshards));
-            // keys-only (the on-chip join): PHJ_P1_WPC2 half-workgroups per CU, not
-            // every slot the LDS allows, so R's partition and tables on the aux
-            // stream get CUs beside S's persistent pass 1 instead of queueing behind it
-            if (a.keys_only && c->tune.p1_wpc2 > 0)
-                slots = std::max<uint32_t>(
-                    1, std::min<uint32_t>(per, std::min<uint32_t>(fit * 2, static_cast<uint32_t>(c->tune.p1_wpc2)) *
-                                                   c->num_cus / (2 * a.nshards)));
-            if (c->tune.p1_slots > 0) slots = std::min<uint32_t>(per, c->tune.p1_slots);
-            if (c->tune.p1_slots < 0) slots = per;   // one tile per workgroup
             const void* kfn = nullptr;
             switch (a.keys_only ? (c->tune.p1_hcode ? 13 : 5) : (c->tune.p1_var & 3)) {
 #define PHJ_P1_VARIANT(V)                                                                            \
@@ -514,6 +504,28 @@ int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const st
                 PHJ_P1_VARIANT(13)
 #undef PHJ_P1_VARIANT
             }
+            // workgroups per CU: what the LDS and the kernel's registers allow
+            // (cached per kernel and LDS size; one cache per worker thread)
+            thread_local std::unordered_map<const void*, std::pair<size_t, int>> occ_cache;
+            int occ = 0;
+            auto hit = occ_cache.find(kfn);
+            if (hit != occ_cache.end() && hit->second.first == lds) {
+                occ = hit->second.second;
+            } else {
+                if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kfn, BLOCK, lds) != hipSuccess || occ < 1) occ = 1;
+                occ_cache[kfn] = {lds, occ};
+            }
+            const uint32_t fit = std::max<uint32_t>(1, std::min<uint32_t>(static_cast<uint32_t>(occ), static_cast<uint32_t>(160 * 1024 / lds)));
+            uint32_t slots = std::max<uint32_t>(1, std::min<uint32_t>(per, fit * c->num_cus / a.nshards));
+            // keys-only (the on-chip join): PHJ_P1_WPC2 half-workgroups per CU, not
+            // every slot the LDS allows, so R's partition and tables on the aux
+            // stream get CUs beside S's persistent pass 1 instead of queueing behind it
+            if (a.keys_only && c->tune.p1_wpc2 > 0)
+                slots = std::max<uint32_t>(
+                    1, std::min<uint32_t>(per, std::min<uint32_t>(fit * 2, static_cast<uint32_t>(c->tune.p1_wpc2)) *
+                                                   c->num_cus / (2 * a.nshards)));
+            if (c->tune.p1_slots > 0) slots = std::min<uint32_t>(per, c->tune.p1_slots);
+            if (c->tune.p1_slots < 0) slots = per;   // one tile per workgroup
             PassArgs ak = a;
             void* kargs[] = {&ak, const_cast<uint32_t*>(&ntiles), const_cast<uint32_t*>(&per)};
             PHJ_HIP(c, hipLaunchKernel(kfn, dim3(slots * a.nshards), dim3(BLOCK), kargs, lds, c->ks));
@@ -2019,7 +2031,9 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
     hipEvent_t t0, t1, tr, b0, b1, p1;
     if (use_p2probe(c, pl, S.n, R.n)) {
         // S: pass 1 only (its pass 2 runs inside the probe); R: pass 1 as codes
-        // and its tables on the aux stream, beside S
+        // and its tables on the aux stream, beside S (measured: R's chain
+        // issued first, or run before S with S's pass 1 on every LDS slot, is
+        // 0.05-0.1 ms slower)
         PHJ_TRY(mark(c, &t0));
         PHJ_HIP(c, hipStreamWaitEvent(c->aux, t0, 0));
         PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, pl, true));
