@@ -800,11 +800,11 @@ int partition_side(phj_ctx* c, int s, const Plan& pl, bool p1_only = false) {
         PHJ_TRY(launch_pass(c, pl.hk, true, p1_aos, a, nt1, std::string(tag) + ".p1", n, nt1 * pl.nb1));
     }
     if (chunked) {
-        hipLaunchKernelGGL(k_pass1_finish_sizes, dim3(1), dim3(1024), 0, c->ks, a.chunk_cursor, pl.nb1, nshards, n, tile2,
+        hipLaunchKernelGGL(k_pass1_finish_sizes, dim3(1), dim3(kFinBlock), 0, c->ks, a.chunk_cursor, pl.nb1, nshards, n, tile2,
                            static_cast<uint32_t*>(S.bounds1.p), tb2);
         PHJ_LAUNCHED(c, "k_pass1_finish_sizes");
     } else {
-        hipLaunchKernelGGL(k_pass1_finish, dim3(1), dim3(1024), 0, c->ks, a.hist, nt1, pl.nb1, n,
+        hipLaunchKernelGGL(k_pass1_finish, dim3(1), dim3(kFinBlock), 0, c->ks, a.hist, nt1, pl.nb1, n,
                            pl.npass == 2 ? tile2 : tile, static_cast<uint32_t*>(S.bounds1.p), tb2);
         PHJ_LAUNCHED(c, "k_pass1_finish");
     }
@@ -1182,7 +1182,7 @@ int partition_build(phj_ctx* c, const Plan& pl, int64_t* out, uint32_t* bounds) 
     PHJ_TRY(timer_end(c));
     PHJ_TRY(timer_begin(c, "R.p1.scan", static_cast<uint64_t>(hlen) * 12));
     PHJ_TRY(scan_u32(c, a.hist, hlen, 1, hlen, c->scan_scratch));
-    hipLaunchKernelGGL(k_pass1_finish, dim3(1), dim3(1024), 0, c->ks, a.hist, nt, nb, n, static_cast<uint32_t>(T), b1,
+    hipLaunchKernelGGL(k_pass1_finish, dim3(1), dim3(kFinBlock), 0, c->ks, a.hist, nt, nb, n, static_cast<uint32_t>(T), b1,
                        static_cast<uint32_t*>(nullptr));
     PHJ_LAUNCHED(c, "k_pass1_finish");
     PHJ_TRY(timer_end(c));

@@ -919,43 +919,54 @@ __global__ __launch_bounds__(kBlock) void k_scan_apply(ScanArgs s) {
 // ---------------------------------------------------------------------------
 // Pass bookkeeping.
 // ---------------------------------------------------------------------------
-// After pass 1 (single segment): bounds1[d] for d <= nb1 and, for a second
-// pass, the per-segment cumulative tile counts.
-__global__ __launch_bounds__(1024) void k_pass1_finish(const uint32_t* hist, uint32_t ntiles,
-                                                       uint32_t nb, uint32_t n, uint32_t T,
-                                                       uint32_t* bounds1, uint32_t* tile_base2) {
-    __shared__ uint32_t wsum[16];
-    __shared__ uint32_t carry;
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    for (uint32_t d = tid; d < nb; d += 1024) bounds1[d] = ntiles ? hist[static_cast<size_t>(d) * ntiles] : 0u;
-    if (tid == 0) {
-        bounds1[nb] = n;
-        carry = 0;
+// The single-workgroup bookkeeping kernels below use kFinBlock threads and
+// loop over the digits: a 1024-thread workgroup needs 16 wave slots on ONE CU,
+// which a persistent pass beside it (S's pass 1, two workgroups per CU) may not
+// leave free anywhere, so R's chain would stall behind it (measured 0.75 ms).
+constexpr uint32_t kFinBlock = 256;
+
+// Exclusive scan over the block with a running carry (kFinBlock threads).
+__device__ __forceinline__ uint32_t fin_block_scan(uint32_t v, uint32_t* wsum, uint32_t& total) {
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    uint32_t before = 0, all = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kFinBlock / 64; w++) {
+        const uint32_t t = wsum[w];
+        if (w < wave) before += t;
+        all += t;
     }
     __syncthreads();
+    total = all;
+    return before + x - v;
+}
+
+// After pass 1 (single segment): bounds1[d] for d <= nb1 and, for a second
+// pass, the per-segment cumulative tile counts.
+__global__ __launch_bounds__(kFinBlock) void k_pass1_finish(const uint32_t* hist, uint32_t ntiles,
+                                                            uint32_t nb, uint32_t n, uint32_t T,
+                                                            uint32_t* bounds1, uint32_t* tile_base2) {
+    __shared__ uint32_t wsum[kFinBlock / 64];
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t d = tid; d < nb; d += kFinBlock) bounds1[d] = ntiles ? hist[static_cast<size_t>(d) * ntiles] : 0u;
+    if (tid == 0) bounds1[nb] = n;
+    __syncthreads();
     if (tile_base2 == nullptr) return;
-    for (uint32_t base = 0; base < nb; base += 1024) {
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < nb; base += kFinBlock) {
         const uint32_t d = base + tid;
         const uint32_t v = d < nb ? (bounds1[d + 1] - bounds1[d] + T - 1) / T : 0u;
-        uint32_t x = v;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(x, o, 64);
-            if (lane >= (uint32_t)o) x += y;
-        }
-        if (lane == 63) wsum[wave] = x;
-        __syncthreads();
-        uint32_t before = 0, all = 0;
-        for (int w = 0; w < 16; w++) {
-            const uint32_t t = wsum[w];
-            if (w < (int)wave) before += t;
-            all += t;
-        }
-        const uint32_t c = carry;
-        if (d < nb) tile_base2[d] = c + before + x - v;
-        __syncthreads();
-        if (tid == 0) carry = c + all;
-        __syncthreads();
+        uint32_t all;
+        const uint32_t ex = fin_block_scan(v, wsum, all);
+        if (d < nb) tile_base2[d] = carry + ex;
+        carry += all;
     }
     if (tid == 0) tile_base2[nb] = carry;
 }
@@ -998,46 +1009,36 @@ __global__ __launch_bounds__(kBlock) void k_tile_chunks(const uint32_t* tile_bas
 
 // After a chunked pass 1: bounds1 = exclusive scan of the digit sizes (summed
 // over the shards: the segments' offsets in the pass-2 output) and
-// tile_base2 = exclusive scan of their chunk counts. One workgroup; nb <= 1024.
-__global__ __launch_bounds__(1024) void k_pass1_finish_sizes(const uint32_t* sizes, uint32_t nb, uint32_t nshards,
-                                                             uint32_t n, uint32_t T, uint32_t* bounds1,
-                                                             uint32_t* tile_base2) {
-    __shared__ uint32_t tmp[2][16];
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    uint32_t v = 0, t = 0;
-    if (tid < nb) {
-        for (uint32_t x = 0; x < nshards; x++) {
-            const uint32_t z = sizes[x * nb + tid];
-            v += z;
-            t += (z + T - 1) / T;
+// tile_base2 = exclusive scan of their chunk counts. One workgroup.
+__global__ __launch_bounds__(kFinBlock) void k_pass1_finish_sizes(const uint32_t* sizes, uint32_t nb, uint32_t nshards,
+                                                                  uint32_t n, uint32_t T, uint32_t* bounds1,
+                                                                  uint32_t* tile_base2) {
+    __shared__ uint32_t wsum[2][kFinBlock / 64];
+    const uint32_t tid = threadIdx.x;
+    uint32_t cx = 0, cy = 0;
+    for (uint32_t base = 0; base < nb; base += kFinBlock) {
+        const uint32_t d = base + tid;
+        uint32_t v = 0, t = 0;
+        if (d < nb) {
+            for (uint32_t x = 0; x < nshards; x++) {
+                const uint32_t z = sizes[x * nb + d];
+                v += z;
+                t += (z + T - 1) / T;
+            }
         }
-    }
-    uint32_t xs = v, ys = t;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t xv = __shfl_up(xs, o, 64), yv = __shfl_up(ys, o, 64);
-        if (lane >= (uint32_t)o) {
-            xs += xv;
-            ys += yv;
+        uint32_t ax, ay;
+        const uint32_t ex = fin_block_scan(v, wsum[0], ax);
+        const uint32_t ey = fin_block_scan(t, wsum[1], ay);
+        if (d < nb) {
+            bounds1[d] = cx + ex;
+            tile_base2[d] = cy + ey;
         }
+        cx += ax;
+        cy += ay;
     }
-    if (lane == 63) {
-        tmp[0][wave] = xs;
-        tmp[1][wave] = ys;
-    }
-    __syncthreads();
-    uint32_t bx = 0, by = 0;
-    for (uint32_t w = 0; w < wave; w++) {
-        bx += tmp[0][w];
-        by += tmp[1][w];
-    }
-    if (tid < nb) {
-        bounds1[tid] = bx + xs - v;
-        tile_base2[tid] = by + ys - t;
-    }
-    if (tid == 1023) {
+    if (tid == 0) {
         bounds1[nb] = n;
-        tile_base2[nb] = by + ys;
+        tile_base2[nb] = cy;
     }
 }
 
