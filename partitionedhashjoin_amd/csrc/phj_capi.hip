@@ -72,6 +72,7 @@ struct Tuning {
     int np_items = 4;     // NoPartitioning probe: S keys per thread per round (4 or 8)
     bool np_region = true;   // NoPartitioning build: partition R into table regions, build each in LDS
     int np_hot = 1;          // NoPartitioning probe: hot-key LDS cache (0 off, 1 from np_hot_min probes)
+    int np_ct = 1;           // NoPartitioning count: region code tables (k_np_probe_ct) instead of 64-B buckets
     uint64_t np_hot_min = 1u << 20;
     uint32_t np_hot_samples = 65536;
     int p2probe = 1;         // radix join, 2 passes: the probe side's pass 2 on-chip (k_probe_ht)
@@ -161,6 +162,7 @@ struct phj_ctx {
     DevBuf np_tab, np_pays;
     DevBuf np_ovf, np_ovfb, np_ovfn;   // region build: overflow tuples, their start buckets, count
     DevBuf np_hot, np_img;             // hot-key cache: sampled keys + count, LDS image (keys, states)
+    DevBuf np_uni;                     // code-table NoPartitioning: {uniform?, cap} (k_np_ct_plan)
     DevBuf fitems, split;
     DevBuf mat_mark, mat_cnt, mat_rows;   // materialised join: per-probe match, block offsets, rows
     uint64_t mat_n = 0;   // fused join: item slots; wave clocks {build, probe} since the last timer reset
@@ -1222,7 +1224,7 @@ int partition_build(phj_ctx* c, const Plan& pl, int64_t* out, uint32_t* bounds) 
 // partition order + P + 1 bounds each, e.g. the all-gathered shards), plus
 // the descriptors k_probe_ht stages. nR = the codes of all segments.
 int build_ht(phj_ctx* c, const Plan& pl, int nseg, const int64_t* const* codes, const uint32_t* const* bounds,
-             uint64_t nR) {
+             uint64_t nR, const uint32_t* uni = nullptr) {
     if (nseg < 1 || nseg > kHtSegs) return set_err(c, PHJ_ERR_INVALID, "build segments must be in [1,16]");
     const uint32_t P = pl.Ppad;
     const uint64_t slots = 4 * nR + 2ull * P;
@@ -1241,6 +1243,7 @@ int build_ht(phj_ctx* c, const Plan& pl, int nseg, const int64_t* const* codes, 
     a.nb2 = pl.nb2;
     a.table = static_cast<uint64_t*>(c->ht_tab.p);
     a.desc = static_cast<uint2*>(c->ht_desc.p);
+    a.uni = uni;
     hipLaunchKernelGGL(k_ht_desc, dim3((pl.nb1 + 3) / 4), dim3(256), 0, c->ks, a);
     PHJ_LAUNCHED(c, "k_ht_desc");
     hipLaunchKernelGGL(k_ht_fill, dim3((P + kHtPpw - 1) / kHtPpw), dim3(256), 0, c->ks, a);
@@ -1301,6 +1304,83 @@ int get_count(phj_ctx* c, uint64_t* out) {
     return PHJ_OK;
 }
 
+// The NoPartitioning count over region code tables (phj_table.h, k_np_probe_ct):
+// R partitioned into 2^k regions of ~300 codes by two radix passes of its hash
+// codes (the build), one code table per region; S probed unpartitioned.
+int join_nopart_ct(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
+    SideState& R = c->side[PHJ_SIDE_BUILD];
+    SideState& S = c->side[PHJ_SIDE_PROBE];
+    uint32_t k = 2;
+    while (k < 22 && (R.n >> k) > 300) k++;
+    phj_join_params pp = *p;
+    pp.algo = PHJ_ALGO_RADIX;
+    pp.num_partitions = 0;
+    pp.flags = 0;
+    pp.radix_bits[1] = static_cast<uint8_t>(k / 2);
+    pp.radix_bits[0] = static_cast<uint8_t>(k - k / 2);
+    Plan pl;
+    PHJ_TRY(make_plan(c, &pp, pl));
+    const uint32_t P = pl.Ppad;
+    const uint64_t slot_bound = 4 * R.n + 2ull * P;
+    PHJ_TRY(ensure(c, c->r_codes, std::max<uint64_t>(1, R.n) * 8));
+    PHJ_TRY(ensure(c, c->r_bounds, (static_cast<size_t>(P) + 1) * 4));
+    PHJ_TRY(ensure(c, c->np_uni, 16));
+    PHJ_TRY(ensure(c, c->count, 16));
+    const int64_t* rcodes = static_cast<const int64_t*>(c->r_codes.p);
+    const uint32_t* rbnd = static_cast<const uint32_t*>(c->r_bounds.p);
+    auto* uni = static_cast<uint32_t*>(c->np_uni.p);
+    if (c->dry) {
+        PHJ_TRY(partition_build(c, pl, static_cast<int64_t*>(c->r_codes.p), static_cast<uint32_t*>(c->r_bounds.p)));
+        return build_ht(c, pl, 1, &rcodes, &rbnd, R.n, uni);
+    }
+    hipEvent_t e0, e1, e2;
+    PHJ_TRY(mark(c, &e0));
+    // the partition is part of the build (its R.* timers show it)
+    PHJ_TRY(partition_build(c, pl, static_cast<int64_t*>(c->r_codes.p), static_cast<uint32_t*>(c->r_bounds.p)));
+    // algorithmic bytes: the codes read, the tables written (~1.7 slots per code)
+    PHJ_TRY(timer_begin(c, "np.build", R.n * 8 * 3));
+    hipLaunchKernelGGL(k_np_ct_plan, dim3(1), dim3(256), 0, c->ks, rbnd, P, slot_bound, uni);
+    PHJ_LAUNCHED(c, "k_np_ct_plan");
+    PHJ_TRY(build_ht(c, pl, 1, &rcodes, &rbnd, R.n, uni));
+    PHJ_TRY(timer_end(c));
+    PHJ_TRY(mark(c, &e1));
+    PHJ_HIP(c, hipMemsetAsync(c->count.p, 0, 8, c->ks));
+    if (S.n > 0) {
+        // algorithmic bytes: S's tuples read once (16 B), R's tables (~2 slots per code) once
+        PHJ_TRY(timer_begin(c, "np.probe", S.n * 16 + R.n * 16));
+        constexpr int IT = 4;
+        const void* kfn = p->hash == PHJ_HASH_MURMUR3 ? reinterpret_cast<const void*>(&k_np_probe_ct<kMurmur3, IT>)
+                                                      : reinterpret_cast<const void*>(&k_np_probe_ct<kXXH3, IT>);
+        int per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, 256, 0) != hipSuccess || per_cu < 1) per_cu = 8;
+        const uint64_t want = (S.n + 256ull * IT - 1) / (256ull * IT);
+        const uint32_t grid = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(want, static_cast<uint64_t>(per_cu) * c->num_cus)));
+        const auto* S_rel = reinterpret_cast<const longlong2*>(S.rel);
+        const auto* tab = static_cast<const uint64_t*>(c->ht_tab.p);
+        const auto* dsc = static_cast<const uint2*>(c->ht_desc.p);
+        const uint32_t* un = uni;
+        auto* cnt = static_cast<unsigned long long*>(c->count.p);
+        uint64_t nS64 = S.n, seed = p->hash_seed;
+        uint32_t Pv = P;
+        void* kargs[] = {const_cast<longlong2**>(&S_rel), &nS64, const_cast<uint64_t**>(&tab), const_cast<uint2**>(&dsc),
+                         const_cast<uint32_t**>(&un), &Pv, &seed, &cnt};
+        PHJ_HIP(c, hipLaunchKernel(kfn, dim3(grid), dim3(256), kargs, 0, c->ks));
+        PHJ_LAUNCHED(c, "k_np_probe_ct");
+        PHJ_TRY(timer_end(c));
+    }
+    PHJ_TRY(mark(c, &e2));
+    uint64_t m = 0;
+    PHJ_TRY(get_count(c, &m));
+    r->matches = m;
+    r->partition_ms = 0;
+    r->build_ms = elapsed(c, e0, e1);
+    r->probe_ms = elapsed(c, e1, e2);
+    r->total_ms = elapsed(c, e0, e2);
+    r->num_partitions = 0;
+    r->algorithmic_bytes = R.n * (16 + 8 + 8 + 8) + R.n * 24 + S.n * 16 + R.n * 16;
+    return fill_timers(c, r);
+}
+
 // marks != nullptr: the probe also writes, per probe tuple, its match's payload
 // slot (phj_join_materialize)
 int join_nopart(phj_ctx* c, const phj_join_params* p, phj_join_result* r, uint32_t* marks = nullptr) {
@@ -1312,6 +1392,7 @@ int join_nopart(phj_ctx* c, const phj_join_params* p, phj_join_result* r, uint32
         return set_err(c, PHJ_ERR_INVALID,
                        "LinearProbingHashTable::LinearProbingHashTable: numberOfObjects must be greater than zero.");
     if (R.n >= (1ull << 32)) return set_err(c, PHJ_ERR_RANGE, "build side above 2^32 tuples");
+    if (!marks && c->tune.np_ct && R.n < (1ull << 30)) return join_nopart_ct(c, p, r);
     const double ratio = p->table_ratio > 0 ? p->table_ratio : c->tune.np_ratio;
     if (ratio < 1.0) return set_err(c, PHJ_ERR_INVALID, "table_ratio must be >= 1");
     const double nbd = std::ceil(static_cast<double>(R.n) * ratio / kNPSlots);
@@ -1645,6 +1726,7 @@ int ctx_create_device(int device, phj_ctx** out) {
     c->tune.np_nt = std::min(2, std::max(0, env_int("PHJ_NP_NT", 1)));
     c->tune.np_items = env_int("PHJ_NP_ITEMS", 4) == 8 ? 8 : 4;
     c->tune.np_region = env_int("PHJ_NP_REGION", 1) != 0;
+    c->tune.np_ct = env_int("PHJ_NP_CT", 1);
     c->tune.np_hot = env_int("PHJ_NP_HOT", 1);
     c->tune.np_hot_min = static_cast<uint64_t>(std::max(0, env_int("PHJ_NP_HOT_MIN", 1 << 20)));
     c->tune.np_hot_samples = static_cast<uint32_t>(std::max(256, env_int("PHJ_NP_HOT_SAMPLES", 65536)));

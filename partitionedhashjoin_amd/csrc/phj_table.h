@@ -246,6 +246,7 @@ struct HtArgs {
     uint32_t nseg, nb1, nb2, pad;
     uint64_t* table;                   // slots (4 |R| + 2 P bound)
     uint2* desc;                       // per final partition: {slot base (even), buckets - 1}
+    const uint32_t* uni;               // nullptr, or {1, cap}: every partition gets cap slots at p * cap (k_np_ct_plan)
 };
 
 __device__ __forceinline__ uint32_t ht_part_size(const HtArgs& a, uint32_t p) {
@@ -266,6 +267,14 @@ __global__ __launch_bounds__(256) void k_ht_desc(HtArgs a) {
     const uint32_t d1 = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (d1 >= a.nb1) return;
     const uint32_t nb2 = a.nb2;
+    if (a.uni && a.uni[0]) {   // uniform layout: partition p at slot p * cap
+        const uint32_t cap = a.uni[1];
+        for (uint32_t d = lane; d < nb2; d += 64) {
+            const uint32_t p = d1 * nb2 + d;
+            a.desc[p] = make_uint2(p * cap, cap / 2 - 1u);
+        }
+        return;
+    }
     uint32_t s1 = 0;   // d1's first code over all segments
     for (uint32_t g = 0; g < a.nseg; g++) s1 += a.bounds[g][static_cast<size_t>(d1) * nb2];
     const uint64_t rbase = 4ull * s1 + 2ull * nb2 * d1;
@@ -306,7 +315,9 @@ __device__ __forceinline__ void ht_insert(uint64_t* tab, uint32_t bmask, uint64_
 // stores. Duplicates may take two slots: harmless to a set test, and the cap
 // counts them.
 __global__ __launch_bounds__(256) void k_ht_fill(HtArgs a) {
-    constexpr uint32_t CPL = kHtLcap * 2 / 3 / 64 + 1;   // codes per lane of a partition that fits the slice
+    // codes per lane: a partition that fits the slice at load <= 0.8 (the
+    // uniform layout's bound; the radix layout's caps keep it <= 2/3)
+    constexpr uint32_t CPL = kHtLcap * 4 / 5 / 64 + 1;
     __shared__ __attribute__((aligned(16))) uint64_t wtab[4][kHtLcap];
     __shared__ uint32_t wcnt[4][kHtLcap / 2];      // per-wave bucket fill counters
     __shared__ uint32_t sb[kHtSegs][kHtPpw + 1];   // bounds of the workgroup's partitions, per segment
@@ -345,7 +356,7 @@ __global__ __launch_bounds__(256) void k_ht_fill(HtArgs a) {
             while (g + 1 < nseg && r >= wpre[wave][g + 1]) g++;
             return a.codes[g] + sb[g][j] + (r - wpre[wave][g]);
         };
-        if (cap <= kHtLcap) {
+        if (cap <= kHtLcap && m <= CPL * 64) {
             uint64_t c[CPL];
 #pragma unroll
             for (uint32_t i = 0; i < CPL; i++) {
@@ -620,6 +631,103 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
         unsigned long long t = 0;
         for (int w = 0; w < BLOCK / 64; w++) t += red[w];
         if (t) atomicAdd(pa.count, t);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// NoPartitioning over code tables (the count probe of join_nopart, PHJ_NP_CT):
+// the reference's one global table (src/NoPartitioning/HashJoin.hpp:76-126)
+// is realised as 2^k small code tables, region p = the low k bits of the code
+// (the layout k_np_build_region already used), built by R's two-pass code
+// partition and k_ht_fill. S is NOT partitioned: every S key hashes, picks its
+// region's table and reads one 16-B bucket, as the reference's Probe()
+// (:128-187) reads its table. With every region at most 0.8 full at a common
+// power-of-two cap (k_np_ct_plan decides on the device), region p sits at
+// slot p * cap and the probe computes its bucket with no descriptor read;
+// otherwise (skewed build keys) it reads desc[p] like k_probe_ht.
+// ---------------------------------------------------------------------------
+
+// One workgroup: the largest region, then {uniform?, cap}.
+__global__ __launch_bounds__(256) void k_np_ct_plan(const uint32_t* bounds, uint32_t P, uint64_t slot_bound,
+                                                    uint32_t* uni) {
+    __shared__ uint32_t red[4];
+    uint32_t mx = 0;
+    for (uint32_t p = threadIdx.x; p < P; p += 256) mx = max(mx, bounds[p + 1] - bounds[p]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = max(mx, static_cast<uint32_t>(__shfl_xor(mx, o, 64)));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        mx = max(max(red[0], red[1]), max(red[2], red[3]));
+        uint32_t cap = 2;
+        while (cap < mx + (mx + 3) / 4) cap <<= 1;   // load <= 0.8 in every region
+        const bool ok = static_cast<uint64_t>(cap) * P <= slot_bound && cap <= kHtLcap;
+        uni[0] = ok ? 1u : 0u;
+        uni[1] = cap;
+    }
+}
+
+template <int HK, int ITEMS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_np_probe_ct(
+    const longlong2* S, uint64_t nS, const uint64_t* table, const uint2* desc, const uint32_t* uni, uint32_t P,
+    uint64_t seed, unsigned long long* count) {
+    const bool uniform = __builtin_amdgcn_readfirstlane(uni[0]) != 0;
+    const uint32_t nbk = __builtin_amdgcn_readfirstlane(uni[1]) / 2;   // buckets per region (uniform)
+    const ulonglong2* tab2 = reinterpret_cast<const ulonglong2*>(table);
+    const uint32_t tid = threadIdx.x;
+    uint32_t hits = 0;
+    const uint64_t step = static_cast<uint64_t>(gridDim.x) * 256 * ITEMS;
+    for (uint64_t base = static_cast<uint64_t>(blockIdx.x) * 256 * ITEMS; base < nS; base += step) {
+        uint64_t c[ITEMS];
+#pragma unroll
+        for (int i = 0; i < ITEMS; i++) {   // S streams past the caches' allocate (it is read once)
+            const uint64_t ix = min(base + i * 256 + tid, nS - 1);
+            c[i] = static_cast<uint64_t>(__builtin_nontemporal_load(&S[ix].x));
+        }
+        uint32_t bb[ITEMS], bm[ITEMS], bk[ITEMS];
+        ulonglong2 v[ITEMS];
+#pragma unroll
+        for (int i = 0; i < ITEMS; i++) {
+            c[i] = hash64<HK>(c[i], seed);
+            const uint32_t p = static_cast<uint32_t>(c[i]) & (P - 1);
+            if (uniform) {
+                bb[i] = p * nbk;
+                bm[i] = nbk - 1;
+            } else {
+                const uint2 ds = desc[p];
+                bb[i] = ds.x >> 1;
+                bm[i] = ds.y;
+            }
+            bk[i] = static_cast<uint32_t>(c[i] >> kHtBucketShift) & bm[i];
+            v[i] = tab2[bb[i] + bk[i]];
+        }
+#pragma unroll
+        for (int i = 0; i < ITEMS; i++) {
+            if (base + i * 256 + tid < nS) {
+                const uint64_t e = (static_cast<uint32_t>(c[i]) & (P - 1)) == 0 ? 1ull : 0ull;
+                bool hit = v[i].x == c[i] || v[i].y == c[i];
+                if (!hit && v[i].y != e) {   // home bucket full, no match: walk on
+                    uint32_t b = bk[i];
+                    for (;;) {
+                        b = (b + 1) & bm[i];
+                        const ulonglong2 w = tab2[bb[i] + b];
+                        hit = w.x == c[i] || w.y == c[i];
+                        if (hit || w.y == e) break;
+                    }
+                }
+                hits += hit ? 1u : 0u;
+            }
+        }
+    }
+    __shared__ uint32_t red[4];
+    uint32_t x = hits;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_down(x, o, 64);
+    if ((tid & 63) == 0) red[tid >> 6] = x;
+    __syncthreads();
+    if (tid == 0) {
+        const unsigned long long t = static_cast<unsigned long long>(red[0]) + red[1] + red[2] + red[3];
+        if (t) atomicAdd(count, t);
     }
 }
 

@@ -34,7 +34,7 @@ FAMILIES = [
     (re.compile(r"\.scatter$"), re.compile(r"phj::k_scatter")),
     (re.compile(r"^build$"), re.compile(r"phj::k_(build_small|ht_fill|join_fused)")),
     (re.compile(r"^probe$"), re.compile(r"phj::k_(probe|join_fused)")),
-    (re.compile(r"^np\.build$"), re.compile(r"phj::k_np_build(?!_overflow)")),
+    (re.compile(r"^np\.build$"), re.compile(r"phj::k_(np_build(?!_overflow)|ht_fill)")),
     (re.compile(r"^np\.probe$"), re.compile(r"phj::k_np_probe")),
 ]
 

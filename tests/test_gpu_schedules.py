@@ -66,12 +66,16 @@ SCHEDULES = [
     {"PHJ_FUSED_KPL": "2"},                                     # 2 S keys per lane, 6 waves/SIMD
     {"PHJ_NT_LOAD": "0"},                                       # no nontemporal tuple loads
     {"PHJ_NT_LOAD": "2", "PHJ_P1_MIN_TILES": "0"},              # nontemporal loads in both passes
-    {"PHJ_NP_NT": "0"},                                         # NoPartitioning probe: cached S loads
-    {"PHJ_NP_NT": "2"},                                         # ... nontemporal bucket loads too
-    {"PHJ_NP_ITEMS": "8"},                                      # ... 8 S keys per thread per round
-    {"PHJ_NP_REGION": "0"},                                     # ... device-atomic build
-    {"PHJ_NP_HOT": "0"},                                        # ... no hot-key LDS cache
-    {"PHJ_NP_HOT_MIN": "0", "PHJ_NP_HOT_SAMPLES": "4096"},      # ... hot-key cache at every size
+    # NoPartitioning: the count runs over region code tables by default
+    # (PHJ_NP_CT); PHJ_NP_CT=0 selects the 64-B key-bucket table, which the
+    # materialising join always uses, and its knobs
+    {"PHJ_NP_CT": "0"},                                         # NoPartitioning count over 64-B key buckets
+    {"PHJ_NP_CT": "0", "PHJ_NP_NT": "0"},                       # ... cached S loads
+    {"PHJ_NP_CT": "0", "PHJ_NP_NT": "2"},                       # ... nontemporal bucket loads too
+    {"PHJ_NP_CT": "0", "PHJ_NP_ITEMS": "8"},                    # ... 8 S keys per thread per round
+    {"PHJ_NP_CT": "0", "PHJ_NP_REGION": "0"},                   # ... device-atomic build
+    {"PHJ_NP_CT": "0", "PHJ_NP_HOT": "0"},                      # ... no hot-key LDS cache
+    {"PHJ_NP_CT": "0", "PHJ_NP_HOT_MIN": "0", "PHJ_NP_HOT_SAMPLES": "4096"},   # ... hot-key cache at every size
     {"PHJ_P2PROBE": "0"},                                       # radix: probe side's pass 2 through HBM
     {"PHJ_P2PROBE": "0", "PHJ_P1_MIN_TILES": "0"},              # ... after the chunked pass 1
     {"PHJ_P1_WPC2": "0"},                                       # keys-only pass 1 on every LDS slot
@@ -80,7 +84,7 @@ SCHEDULES = [
     {"PHJ_P1_KO": "0", "PHJ_P1_MIN_TILES": "0"},                # chunked pass 1 writes whole tuples for the probe
     {"PHJ_P1_KO_TPS": "4"},                                     # keys-only pass 1: 16 shards on small relations
     {"PHJ_P1_KO_MIN_TILES": "1000000"},                         # ... never chunked: stable pass 1 of tuples
-    {"PHJ_NP_RATIO": "1.25"},                                   # NoPartitioning default table ratio
+    {"PHJ_NP_CT": "0", "PHJ_NP_RATIO": "1.25"},                 # NoPartitioning 64-B bucket table ratio
     {"PHJ_P1_MIN_TILES": "0", "PHJ_P1_VAR": "0"},               # chunked pass 1: stable ballot ranking
     {"PHJ_P1_MIN_TILES": "0", "PHJ_P1_VAR": "1"},               # ... LDS-atomic ranking
     {"PHJ_P1_MIN_TILES": "0", "PHJ_P1_VAR": "2"},               # ... tuple-wide LDS tile
