@@ -683,8 +683,7 @@ uint32_t pass_tile(const phj_ctx* c, uint32_t n, uint32_t nb, bool* wc) {
     return static_cast<uint32_t>(sub * k);
 }
 
-int partition_side(phj_ctx* c, int s, const Plan& pl, bool p1_only = false) {
-    SideState& S = c->side[s];
+int partition_state(phj_ctx* c, SideState& S, const char* tag, const Plan& pl, bool p1_only) {
     c->scan_scratch = &S.partials;
     if (!S.rel && S.n > 0) return set_err(c, PHJ_ERR_STATE, "relation not bound");
     const uint64_t n64 = S.n;
@@ -699,7 +698,6 @@ int partition_side(phj_ctx* c, int s, const Plan& pl, bool p1_only = false) {
     // (p1_only: the probe re-hashes the keys itself, nothing reads the column)
     const bool dcol = pl.npass == 2 && c->tune.dcol && !wc1 && !wc2 && !p1_only;
     const uint32_t dbytes = pl.bits2 > 8 ? 2 : 1;
-    const char* tag = s == PHJ_SIDE_BUILD ? "R" : "S";
     // Chunked pass 1 (unordered partitions, tile kernels): pass-1 chunks are
     // the pass-2 tiles, every digit's run of a tile fits one workgroup thread
     // (nb1 <= block) and spans at most two chunks (tile1 == tile2).
@@ -878,6 +876,10 @@ int partition_side(phj_ctx* c, int s, const Plan& pl, bool p1_only = false) {
     S.partitioned = true;
     S.plan = pl;
     return PHJ_OK;
+}
+
+int partition_side(phj_ctx* c, int s, const Plan& pl, bool p1_only = false) {
+    return partition_state(c, c->side[s], s == PHJ_SIDE_BUILD ? "R" : "S", pl, p1_only);
 }
 
 // Build over `nseg` partitioned build segments and probe the ctx's partitioned
@@ -1138,8 +1140,8 @@ int build_and_probe(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned*
 
 // The build side of the on-chip join on this device's relation: pass 1 as
 // hash codes, contiguous per pass-1 digit (k_hist + scan + k_scatter_codes,
-// 512 x 4096 tiles), then pass 2 into final partition order (k_ht_hist + scan
-// + k_ht_scatter). `out` receives |R| codes, `bounds` the P + 1 partition
+// 512 x 4096 tiles), then pass 2 into final partition order (k_ht_p2, one
+// workgroup per pass-1 digit). `out` receives |R| codes, `bounds` the P + 1 partition
 // bounds: one build segment of build_ht (they may point into an exchange block).
 int partition_build(phj_ctx* c, const Plan& pl, int64_t* out, uint32_t* bounds) {
     SideState& S = c->side[PHJ_SIDE_BUILD];
@@ -1149,15 +1151,9 @@ int partition_build(phj_ctx* c, const Plan& pl, int64_t* out, uint32_t* bounds) 
     constexpr int BLOCK = 512, ITEMS = 8, T = BLOCK * ITEMS;
     const uint32_t n = static_cast<uint32_t>(S.n), nb = pl.nb1, P = pl.Ppad;
     const uint32_t nt = (n + T - 1) / T, hlen = nt * nb;
-    const uint32_t h2len = P * kHtTpd + 1;
     PHJ_TRY(ensure(c, S.hist1, std::max<size_t>(1, hlen) * 4));
-    PHJ_TRY(ensure(c, S.bounds1, (static_cast<size_t>(nb) + 1) * 4));
     PHJ_TRY(ensure(c, S.kA, std::max<size_t>(1, n) * 8));
-    PHJ_TRY(ensure(c, S.hist2, static_cast<size_t>(h2len) * 4));
-    if (c->dry) {
-        if (hlen) PHJ_TRY(scan_u32(c, nullptr, hlen, 1, hlen, c->scan_scratch));
-        return scan_u32(c, nullptr, h2len, 1, h2len, c->scan_scratch);
-    }
+    if (c->dry) return hlen ? scan_u32(c, nullptr, hlen, 1, hlen, c->scan_scratch) : PHJ_OK;
     if (n == 0) {
         PHJ_HIP(c, hipMemsetAsync(bounds, 0, (static_cast<size_t>(P) + 1) * 4, c->ks));
         c->since_ev++;
@@ -1176,17 +1172,13 @@ int partition_build(phj_ctx* c, const Plan& pl, int64_t* out, uint32_t* bounds) 
     a.xcd_remap = c->tune.xcd_remap ? 1u : 0u;
     const uint32_t grid = a.xcd_remap ? (nt + 7) & ~7u : nt;
     const size_t hlds = static_cast<size_t>(BLOCK / 64) * nb * 4;
-    auto* b1 = static_cast<uint32_t*>(S.bounds1.p);
     PHJ_TRY(timer_begin(c, "R.p1.hist", static_cast<uint64_t>(n) * 16));
     if (pl.hk == kMurmur3) hipLaunchKernelGGL((k_hist<BLOCK, ITEMS, true, kMurmur3>), dim3(grid), dim3(BLOCK), hlds, c->ks, a);
     else hipLaunchKernelGGL((k_hist<BLOCK, ITEMS, true, kXXH3>), dim3(grid), dim3(BLOCK), hlds, c->ks, a);
     PHJ_LAUNCHED(c, "k_hist");
     PHJ_TRY(timer_end(c));
     PHJ_TRY(timer_begin(c, "R.p1.scan", static_cast<uint64_t>(hlen) * 12));
-    PHJ_TRY(scan_u32(c, a.hist, hlen, 1, hlen, c->scan_scratch));
-    hipLaunchKernelGGL(k_pass1_finish, dim3(1), dim3(kFinBlock), 0, c->ks, a.hist, nt, nb, n, static_cast<uint32_t>(T), b1,
-                       static_cast<uint32_t*>(nullptr));
-    PHJ_LAUNCHED(c, "k_pass1_finish");
+    PHJ_TRY(scan_u32(c, a.hist, hlen, 1, hlen, c->scan_scratch));   // k_ht_p2 reads d1's run from it
     PHJ_TRY(timer_end(c));
     // algorithmic bytes: the 16-B tuple read, the 8-B code written
     PHJ_TRY(timer_begin(c, "R.p1.scatter", static_cast<uint64_t>(n) * 24));
@@ -1199,24 +1191,21 @@ int partition_build(phj_ctx* c, const Plan& pl, int64_t* out, uint32_t* bounds) 
     PHJ_TRY(timer_end(c));
     HtPass2Args b{};
     b.codes = static_cast<const int64_t*>(S.kA.p);
-    b.b1 = b1;
-    b.hist = static_cast<uint32_t*>(S.hist2.p);
+    b.hist1 = a.hist;
     b.out = out;
     b.bounds = bounds;
+    b.nt1 = nt;
+    b.n = n;
     b.nb1 = nb;
     b.nb2 = pl.nb2;
     b.f2 = digit_fn(pl, 2);
-    const size_t lds2 = static_cast<size_t>(pl.nb2) * 4;
-    PHJ_TRY(timer_begin(c, "R.p2.hist", static_cast<uint64_t>(n) * 8));
-    hipLaunchKernelGGL(k_ht_hist, dim3(nb * kHtTpd), dim3(256), lds2, c->ks, b);
-    PHJ_LAUNCHED(c, "k_ht_hist");
-    PHJ_TRY(timer_end(c));
-    PHJ_TRY(timer_begin(c, "R.p2.scan", static_cast<uint64_t>(h2len) * 12));
-    PHJ_TRY(scan_u32(c, b.hist, h2len, 1, h2len, c->scan_scratch));
-    PHJ_TRY(timer_end(c));
+    // algorithmic bytes: the codes read, written in partition order
     PHJ_TRY(timer_begin(c, "R.p2.scatter", static_cast<uint64_t>(n) * 16));
-    hipLaunchKernelGGL(k_ht_scatter, dim3(nb * kHtTpd), dim3(256), lds2, c->ks, b);
-    PHJ_LAUNCHED(c, "k_ht_scatter");
+    // runs kept in registers when d1's runs average well inside kHtP2Keep
+    const bool keep = static_cast<uint64_t>(n) / nb * 5 / 4 <= kHtP2Keep;
+    if (keep) hipLaunchKernelGGL(k_ht_p2<true>, dim3(nb), dim3(kHtP2Block), ht_p2_lds_bytes(pl.nb2, true), c->ks, b);
+    else hipLaunchKernelGGL(k_ht_p2<false>, dim3(nb), dim3(kHtP2Block), ht_p2_lds_bytes(pl.nb2, false), c->ks, b);
+    PHJ_LAUNCHED(c, "k_ht_p2");
     return timer_end(c);
 }
 
@@ -1244,8 +1233,6 @@ int build_ht(phj_ctx* c, const Plan& pl, int nseg, const int64_t* const* codes, 
     a.table = static_cast<uint64_t*>(c->ht_tab.p);
     a.desc = static_cast<uint2*>(c->ht_desc.p);
     a.uni = uni;
-    hipLaunchKernelGGL(k_ht_desc, dim3((pl.nb1 + 3) / 4), dim3(256), 0, c->ks, a);
-    PHJ_LAUNCHED(c, "k_ht_desc");
     hipLaunchKernelGGL(k_ht_fill, dim3((P + kHtPpw - 1) / kHtPpw), dim3(256), 0, c->ks, a);
     PHJ_LAUNCHED(c, "k_ht_fill");
     return PHJ_OK;
@@ -1261,11 +1248,10 @@ bool use_p2probe(const phj_ctx* c, const Plan& pl, uint64_t nS, uint64_t nR) {
            4 * nR + 2ull * pl.Ppad < (1ull << 32);
 }
 
-// Probe the probe side's pass-1 output (partition_side p1_only) against the
-// tables of build_ht; the count lands in c->count.
-int probe_ht(phj_ctx* c, const Plan& pl) {
-    SideState& PS = c->side[PHJ_SIDE_PROBE];
-    PHJ_HIP(c, hipMemsetAsync(c->count.p, 0, 8, c->ks));
+// Probe a probe-side pass-1 output (partition_state p1_only) against the
+// tables of build_ht; the count lands in (clear) or is added to c->count.
+int probe_ht(phj_ctx* c, const Plan& pl, SideState& PS, bool clear = true) {
+    if (clear) PHJ_HIP(c, hipMemsetAsync(c->count.p, 0, 8, c->ks));
     if (PS.nt2 == 0) return PHJ_OK;
     HtProbeArgs pa{};
     pa.a = PS.p2;
@@ -2115,7 +2101,8 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
         // S: pass 1 only (its pass 2 runs inside the probe); R: pass 1 as codes
         // and its tables on the aux stream, beside S (measured: R's chain
         // issued first, or run before S with S's pass 1 on every LDS slot, is
-        // 0.05-0.1 ms slower)
+        // 0.05-0.1 ms slower; probing S in row ranges, each beside the next
+        // range's pass 1, is 0.3 ms slower: DESIGN.md section 3)
         PHJ_TRY(mark(c, &t0));
         PHJ_HIP(c, hipStreamWaitEvent(c->aux, t0, 0));
         PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, pl, true));
@@ -2138,7 +2125,7 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
         // algorithmic bytes: the pass-1 output read once (16-B tuples, or 8-B
         // codes after a keys-only pass 1); the tables are re-read from L2
         PHJ_TRY(timer_begin(c, "probe", S.n * (S.p2.keys_only ? 8 : 16)));
-        PHJ_TRY(probe_ht(c, pl));
+        PHJ_TRY(probe_ht(c, pl, S));
         PHJ_TRY(timer_end(c));
         PHJ_TRY(mark(c, &p1));
         uint64_t m = 0;

@@ -364,13 +364,13 @@ int allreduce_count(Group& G, int i, const void* local_count, bool failed = fals
         if (!G.comm[i]) return set_err(c, PHJ_ERR_STATE, "RCCL communicator aborted by an earlier failure");
         auto* d = static_cast<uint64_t*>(B.cnt.p);
         if (!d) return abort_comm(G, i, set_err(c, PHJ_ERR_STATE, "count buffer missing"));
-        PHJ_HIP(c, hipMemsetAsync(d + 2, 0, 16, c->stream));
-        if (failed) PHJ_HIP(c, hipMemsetAsync(d + 3, 1, 1, c->stream));
-        else PHJ_HIP(c, hipMemcpyAsync(d + 2, local_count, 8, hipMemcpyDeviceToDevice, c->stream));
-        PHJ_NCCL(c, rccl().AllReduce(d + 2, d, 2, ncclUint64, ncclSum, G.comm[i], c->stream));
+        PHJ_HIP(c, hipMemsetAsync(d + 2, 0, 16, c->ks));
+        if (failed) PHJ_HIP(c, hipMemsetAsync(d + 3, 1, 1, c->ks));
+        else PHJ_HIP(c, hipMemcpyAsync(d + 2, local_count, 8, hipMemcpyDeviceToDevice, c->ks));
+        PHJ_NCCL(c, rccl().AllReduce(d + 2, d, 2, ncclUint64, ncclSum, G.comm[i], c->ks));
     } else {
         if (failed) return PHJ_OK;
-        PHJ_HIP(c, hipMemcpyAsync(B.cnt.p, local_count, 8, hipMemcpyDeviceToDevice, c->stream));
+        PHJ_HIP(c, hipMemcpyAsync(B.cnt.p, local_count, 8, hipMemcpyDeviceToDevice, c->ks));
     }
     c->since_ev++;
     return PHJ_OK;
@@ -379,8 +379,8 @@ int allreduce_count(Group& G, int i, const void* local_count, bool failed = fals
 int read_count(Group& G, int i, uint64_t* out) {
     phj_ctx* c = G.mem[i];
     unsigned long long h[2] = {0, 0};
-    PHJ_HIP(c, hipMemcpyAsync(h, G.buf[i].cnt.p, 16, hipMemcpyDeviceToHost, c->stream));
-    PHJ_HIP(c, hipStreamSynchronize(c->stream));
+    PHJ_HIP(c, hipMemcpyAsync(h, G.buf[i].cnt.p, 16, hipMemcpyDeviceToHost, c->ks));
+    PHJ_HIP(c, hipStreamSynchronize(c->ks));
     if (G.kind == Xchg::kRccl && h[1] != 0)
         return set_err(c, PHJ_ERR_STATE, std::to_string(h[1]) + " rank(s) failed during the join");
     *out = h[0];
@@ -471,7 +471,7 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
     const bool p2 = member_p2(G, c, pl);
     const PackLayout L = member_layout(G, pl, p2);
     std::vector<phj_partitioned> segs(G.world);   // filled once the exchange buffers exist
-    hipEvent_t t0 = nullptr, x0 = nullptr, x1 = nullptr, t1, b0 = nullptr, b1 = nullptr, p1, te;
+    hipEvent_t t0 = nullptr, x0 = nullptr, x1 = nullptr, t1, b0 = nullptr, b1 = nullptr, p1, te, sdone = nullptr;
     // up to the exchange every step runs even after an error (no early
     // return): the local exchange's barrier must see every member
     int rc = hipSetDevice(c->device) == hipSuccess ? PHJ_OK : set_err(c, PHJ_ERR_HIP, "hipSetDevice");
@@ -494,6 +494,24 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
         r->total_ms = 0;
         return PHJ_OK;
     }
+    // the S shard's pass 1 goes out first, on the main stream (it needs nothing
+    // from R): neither the exchange's host-side wait (the local rehearsal's
+    // barrier, a blocking collective) nor the host time of issuing R's chain
+    // may hold it back (measured W=8 rehearsal: S.p1 started after R's
+    // partition, 0.3 ms in, when it was issued after it)
+    // The on-chip join then probes on the aux stream right after the tables
+    // (one cross-stream wait fewer on the critical path: S's pass 1, and the
+    // count reset behind it, are long done by then)
+    const bool s_early = !(G.rehearse && i > 0);
+    if (rc == PHJ_OK && s_early) {
+        c->ks = c->stream;
+        rc = partition_side(c, PHJ_SIDE_PROBE, pl, p2);
+        if (rc == PHJ_OK && p2) rc = ensure(c, c->count, 16);
+        if (rc == PHJ_OK && p2 && hipMemsetAsync(c->count.p, 0, 8, c->stream) != hipSuccess)
+            rc = set_err(c, PHJ_ERR_HIP, "count reset");
+        if (rc == PHJ_OK && p2) rc = mark(c, &sdone);
+        c->ks = c->aux;
+    }
     if (p2) {   // the R shard as codes in partition order, straight into the exchange block
         if (rc == PHJ_OK)
             rc = partition_build(c, pl, static_cast<int64_t*>(B.send.p),
@@ -508,16 +526,6 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
                            hipMemcpyDeviceToDevice, c->ks) != hipSuccess)
             rc = set_err(c, PHJ_ERR_HIP, "pack bounds");
         c->since_ev += 2;
-    }
-    // the S shard's pass 1 is issued on the main stream BEFORE the exchange:
-    // an exchange with a host-side wait (the local rehearsal's barrier, a
-    // blocking collective) must not hold back S, which needs nothing from R
-    // (measured W=8 rehearsal: S.p1 started only after the exchange, 0.47 ms in)
-    const bool s_early = !(G.rehearse && i > 0);
-    if (rc == PHJ_OK && s_early) {
-        c->ks = c->stream;
-        rc = partition_side(c, PHJ_SIDE_PROBE, pl, p2);
-        c->ks = c->aux;
     }
     if (rc == PHJ_OK) rc = mark(c, &x0);
     if (rc == PHJ_OK) rc = timer_begin(c, "exchange", static_cast<uint64_t>(G.world - 1) * L.elems * 8);
@@ -550,16 +558,19 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
     }
     // (the S shard's pass 1 went out on the main stream before the exchange)
     auto join_local = [&]() -> int {
-        PHJ_HIP(c, hipStreamWaitEvent(c->stream, p2 ? b1 : x1, 0));
-        PHJ_TRY(mark(c, &t1));
-        if (p2) {
+        if (p2) {   // on the aux stream, behind the tables
+            c->ks = c->aux;
+            PHJ_HIP(c, hipStreamWaitEvent(c->aux, sdone, 0));
+            PHJ_TRY(mark(c, &t1));
             PHJ_TRY(timer_begin(c, "probe", c->side[PHJ_SIDE_PROBE].n * (c->side[PHJ_SIDE_PROBE].p2.keys_only ? 8 : 16)));
-            PHJ_TRY(probe_ht(c, pl));
+            PHJ_TRY(probe_ht(c, pl, c->side[PHJ_SIDE_PROBE], false));
             PHJ_TRY(timer_end(c));
             PHJ_TRY(mark(c, &p1));
             c->last_fused = false;
             return PHJ_OK;
         }
+        PHJ_HIP(c, hipStreamWaitEvent(c->stream, x1, 0));
+        PHJ_TRY(mark(c, &t1));
         return build_and_probe(c, pl, G.world, segs.data(), &b0, &b1, &p1);
     };
     if (rc == PHJ_OK) rc = join_local();
@@ -568,10 +579,15 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
         const int ra = allreduce_count(G, i, c->count.p, rc != PHJ_OK);
         if (rc == PHJ_OK) rc = ra;
     }
-    PHJ_TRY(rc);
+    if (rc != PHJ_OK) {
+        c->ks = c->stream;
+        return rc;
+    }
     PHJ_TRY(mark(c, &te));
     uint64_t m = 0;
-    PHJ_TRY(read_count(G, i, &m));
+    rc = read_count(G, i, &m);
+    c->ks = c->stream;
+    PHJ_TRY(rc);
     r->matches = m;
     r->partition_ms = elapsed(c, t0, t1);
     r->build_ms = elapsed(c, b0, b1);
@@ -695,10 +711,15 @@ int member_nopart(Group& G, int i, const phj_join_params* p, phj_join_result* r,
         const int ra = allreduce_count(G, i, c->count.p, rc != PHJ_OK);
         if (rc == PHJ_OK) rc = ra;
     }
-    PHJ_TRY(rc);
+    if (rc != PHJ_OK) {
+        c->ks = c->stream;
+        return rc;
+    }
     PHJ_TRY(mark(c, &te));
     uint64_t m = 0;
-    PHJ_TRY(read_count(G, i, &m));
+    rc = read_count(G, i, &m);
+    c->ks = c->stream;
+    PHJ_TRY(rc);
     *r = jr;
     r->matches = m;
     r->exchange_ms = elapsed(c, t0, t1);

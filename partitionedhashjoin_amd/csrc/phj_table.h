@@ -152,89 +152,102 @@ __global__ __launch_bounds__(BLOCK) void k_scatter_codes(PassArgs a) {
 
 // ---------------------------------------------------------------------------
 // The build side. Every rank groups ITS OWN codes by final partition before
-// the exchange (R pass 2, on the rank's shard only: kHtTpd workgroups per
-// pass-1 digit d1, each a contiguous slice of d1's run, count then scatter by
-// d2; hist[p * kHtTpd + k] scanned = where slice k's codes of partition p
-// start), so a build segment is {codes in partition order, bounds[P + 1]}.
-// After the exchange only the tables are built over all segments:
-//   k_ht_desc: per d1 (one wave) the table offsets of its partitions from the
-//       partition sizes (closed-form region base, prefix of the caps)
-//   k_ht_fill: a workgroup stages the codes of 16 consecutive partitions from
-//       every segment into LDS (coalesced), then each wave builds a
-//       partition's table in its LDS slice (compare-and-swap in LDS) and
-//       writes it out in whole lines
+// the exchange (R pass 2 on the rank's shard only, k_ht_p2), so a build
+// segment is {codes in partition order, bounds[P + 1]}. After the exchange
+// only the tables are built over all segments (k_ht_fill: a workgroup stages
+// the codes of kHtPpw consecutive partitions from every segment, each wave
+// builds a partition's table in its LDS slice and writes it out).
 // ---------------------------------------------------------------------------
-constexpr uint32_t kHtTpd = 16;      // R pass-2 workgroups per pass-1 digit
 constexpr uint32_t kHtLcap = 512;    // k_ht_fill: LDS table slots per wave
 constexpr uint32_t kHtPpw = 8;       // k_ht_fill: partitions per workgroup (two per wave)
-constexpr uint32_t kHtUnr = 8;       // codes per thread in flight
 
 // R pass 2 over one relation's pass-1 output (codes contiguous per d1).
 struct HtPass2Args {
     const int64_t* codes;      // pass-1 output
-    const uint32_t* b1;        // nb1 + 1
-    uint32_t* hist;            // [P * kHtTpd + 1], scanned in place between the kernels
+    const uint32_t* hist1;     // pass 1's scanned histogram, hist1[d1 * nt1 + t]: d1's run starts at hist1[d1 * nt1]
     int64_t* out;              // codes in final partition order
-    uint32_t* bounds;          // P + 1 final bounds (written by k_ht_scatter's slice-0 workgroups)
+    uint32_t* bounds;          // P + 1 final bounds
+    uint32_t nt1, n;           // pass-1 tiles, codes
     uint32_t nb1, nb2;
     DigitFn f2;                // d2 = q_from_hash(c, f2) & f2.dmask (shift 0)
 };
 
-__global__ __launch_bounds__(256) void k_ht_hist(HtPass2Args a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    uint32_t* cnt = reinterpret_cast<uint32_t*>(smem);   // [nb2]
-    const uint32_t d1 = blockIdx.x / kHtTpd, k = blockIdx.x % kHtTpd, tid = threadIdx.x;
-    const uint32_t nb2 = a.nb2;
-    const uint32_t lo = a.b1[d1], m1 = a.b1[d1 + 1] - lo;
-    const uint32_t f_lo = lo + static_cast<uint32_t>(static_cast<uint64_t>(m1) * k / kHtTpd);
-    const uint32_t f_hi = lo + static_cast<uint32_t>(static_cast<uint64_t>(m1) * (k + 1) / kHtTpd);
-    for (uint32_t d = tid; d < nb2; d += 256) cnt[d] = 0;
-    __syncthreads();
-    for (uint32_t f0 = f_lo; f0 < f_hi; f0 += 256 * kHtUnr) {
-        uint64_t c[kHtUnr];
-#pragma unroll
-        for (uint32_t u = 0; u < kHtUnr; u++) {
-            const uint32_t f = f0 + u * 256 + tid;
-            c[u] = f < f_hi ? static_cast<uint64_t>(a.codes[f]) : 0;
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < kHtUnr; u++)
-            count_digit(cnt, static_cast<uint32_t>(q_from_hash(c[u], a.f2)) & a.f2.dmask, f0 + u * 256 + tid < f_hi);
-    }
-    __syncthreads();
-    uint32_t* h = a.hist + static_cast<size_t>(d1) * nb2 * kHtTpd + k;
-    for (uint32_t d = tid; d < nb2; d += 256) h[static_cast<size_t>(d) * kHtTpd] = cnt[d];
-    if (blockIdx.x == 0 && tid == 0) a.hist[static_cast<size_t>(a.nb1) * nb2 * kHtTpd] = 0;
+// R pass 2 in one launch: one workgroup per pass-1 digit d1 counts d1's codes by d2 in LDS, scans the
+// counts itself (a digit's codes stay inside d1's run, so no other workgroup
+// is involved) and scatters. A run of up to kHtP2Keep codes (the shard of a
+// multi-GPU rank) is read once into registers, grouped in LDS and written out
+// in order (whole lines); a longer run is counted, then read again and
+// scattered through LDS cursors.
+constexpr uint32_t kHtP2Block = 1024, kHtP2Items = 6;
+constexpr uint32_t kHtP2Keep = kHtP2Block * kHtP2Items;
+
+__host__ __device__ constexpr size_t ht_p2_lds_bytes(uint32_t nb2, bool keep) {
+    return (keep ? static_cast<size_t>(kHtP2Keep) * 8 : 0) + static_cast<size_t>(nb2) * 8;
 }
 
-__global__ __launch_bounds__(256) void k_ht_scatter(HtPass2Args a) {
+template <bool KEEP>
+__global__ __launch_bounds__(kHtP2Block) void k_ht_p2(HtPass2Args a) {
+    constexpr uint32_t B = kHtP2Block, U = kHtP2Items;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    uint32_t* cur = reinterpret_cast<uint32_t*>(smem);   // [nb2] output cursors
-    const uint32_t d1 = blockIdx.x / kHtTpd, k = blockIdx.x % kHtTpd, tid = threadIdx.x;
-    const uint32_t nb2 = a.nb2;
-    const uint32_t lo = a.b1[d1], m1 = a.b1[d1 + 1] - lo;
-    const uint32_t f_lo = lo + static_cast<uint32_t>(static_cast<uint64_t>(m1) * k / kHtTpd);
-    const uint32_t f_hi = lo + static_cast<uint32_t>(static_cast<uint64_t>(m1) * (k + 1) / kHtTpd);
-    const uint32_t* h = a.hist + static_cast<size_t>(d1) * nb2 * kHtTpd + k;
-    for (uint32_t d = tid; d < nb2; d += 256) {
-        cur[d] = h[static_cast<size_t>(d) * kHtTpd];
-        if (k == 0) a.bounds[static_cast<size_t>(d1) * nb2 + d] = cur[d];   // partition start = slice 0's
-    }
-    if (blockIdx.x == 0 && tid == 0) a.bounds[static_cast<size_t>(a.nb1) * nb2] = a.hist[static_cast<size_t>(a.nb1) * nb2 * kHtTpd];
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(smem);                 // [nb2] counts
+    uint32_t* cur = cnt + a.nb2;                                        // [nb2] cursors
+    uint64_t* sorted = reinterpret_cast<uint64_t*>(cur + a.nb2);        // [kHtP2Keep] d2 order (KEEP)
+    __shared__ uint32_t tmp[B / 64];
+    const uint32_t d1 = blockIdx.x, tid = threadIdx.x, nb2 = a.nb2;
+    const uint32_t lo = a.hist1[static_cast<size_t>(d1) * a.nt1];
+    const uint32_t hi = d1 + 1 < a.nb1 ? a.hist1[static_cast<size_t>(d1 + 1) * a.nt1] : a.n, m = hi - lo;
+    const bool keep = KEEP && m <= kHtP2Keep;   // workgroup-uniform
+    auto d2_of = [&](uint64_t c) { return static_cast<uint32_t>(q_from_hash(c, a.f2)) & a.f2.dmask; };
+    for (uint32_t d = tid; d < nb2; d += B) cnt[d] = 0;
     __syncthreads();
-    for (uint32_t f0 = f_lo; f0 < f_hi; f0 += 256 * kHtUnr) {
-        uint64_t c[kHtUnr];
+    uint64_t c[U];
+    for (uint32_t f0 = lo; f0 < hi; f0 += B * U) {
 #pragma unroll
-        for (uint32_t u = 0; u < kHtUnr; u++) {
-            const uint32_t f = f0 + u * 256 + tid;
-            c[u] = f < f_hi ? static_cast<uint64_t>(a.codes[f]) : 0;
+        for (uint32_t u = 0; u < U; u++) {
+            const uint32_t f = f0 + u * B + tid;
+            c[u] = f < hi ? static_cast<uint64_t>(a.codes[f]) : 0;
         }
 #pragma unroll
-        for (uint32_t u = 0; u < kHtUnr; u++) {
-            const uint32_t f = f0 + u * 256 + tid;
-            const uint32_t d = static_cast<uint32_t>(q_from_hash(c[u], a.f2)) & a.f2.dmask;
-            const uint32_t r = agg_rank(cur, d, f < f_hi);
-            if (f < f_hi) a.out[r] = static_cast<int64_t>(c[u]);
+        for (uint32_t u = 0; u < U; u++) count_digit(cnt, d2_of(c[u]), f0 + u * B + tid < hi);
+    }
+    __syncthreads();
+    {   // exclusive scan of the counts: nb2 / B consecutive digits per thread
+        const uint32_t per = (nb2 + B - 1) / B, d0 = tid * per;
+        uint32_t local = 0;
+        for (uint32_t j = 0; j < per; j++)
+            if (d0 + j < nb2) local += cnt[d0 + j];
+        uint32_t tot;
+        uint32_t run = block_exclusive_scan_t<B / 64>(local, tmp, tot);
+        for (uint32_t j = 0; j < per; j++) {
+            const uint32_t d = d0 + j;
+            if (d < nb2) {
+                a.bounds[static_cast<size_t>(d1) * nb2 + d] = lo + run;
+                cur[d] = keep ? run : lo + run;
+                run += cnt[d];
+            }
+        }
+        if (d1 + 1 == a.nb1 && tid == 0) a.bounds[static_cast<size_t>(a.nb1) * nb2] = hi;
+    }
+    __syncthreads();
+    if (keep) {   // the run is in c[] (one round of the loop above)
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++)
+            if (u * B + tid < m) sorted[atomicAdd(&cur[d2_of(c[u])], 1u)] = c[u];
+        __syncthreads();
+        for (uint32_t i = tid; i < m; i += B) a.out[lo + i] = static_cast<int64_t>(sorted[i]);
+        return;
+    }
+    for (uint32_t f0 = lo; f0 < hi; f0 += B * U) {
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+            const uint32_t f = f0 + u * B + tid;
+            c[u] = f < hi ? static_cast<uint64_t>(a.codes[f]) : 0;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+            const uint32_t f = f0 + u * B + tid;
+            const uint32_t r = agg_rank(cur, d2_of(c[u]), f < hi);
+            if (f < hi) a.out[r] = static_cast<int64_t>(c[u]);
         }
     }
 }
@@ -245,7 +258,7 @@ struct HtArgs {
     const uint32_t* bounds[kHtSegs];   // P + 1 each
     uint32_t nseg, nb1, nb2, pad;
     uint64_t* table;                   // slots (4 |R| + 2 P bound)
-    uint2* desc;                       // per final partition: {slot base (even), buckets - 1}
+    uint2* desc;                       // per final partition: {slot base (even), buckets - 1}, written by k_ht_fill
     const uint32_t* uni;               // nullptr, or {1, cap}: every partition gets cap slots at p * cap (k_np_ct_plan)
 };
 
@@ -260,37 +273,6 @@ __device__ __forceinline__ uint32_t ht_part_size(const HtArgs& a, uint32_t p) {
 #pragma unroll
     for (uint32_t g = 0; g < kHtSegs; g++) m += hi[g] - lo[g];
     return m;
-}
-
-// One wave per d1: desc[p] for its nb2 partitions.
-__global__ __launch_bounds__(256) void k_ht_desc(HtArgs a) {
-    const uint32_t d1 = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (d1 >= a.nb1) return;
-    const uint32_t nb2 = a.nb2;
-    if (a.uni && a.uni[0]) {   // uniform layout: partition p at slot p * cap
-        const uint32_t cap = a.uni[1];
-        for (uint32_t d = lane; d < nb2; d += 64) {
-            const uint32_t p = d1 * nb2 + d;
-            a.desc[p] = make_uint2(p * cap, cap / 2 - 1u);
-        }
-        return;
-    }
-    uint32_t s1 = 0;   // d1's first code over all segments
-    for (uint32_t g = 0; g < a.nseg; g++) s1 += a.bounds[g][static_cast<size_t>(d1) * nb2];
-    const uint64_t rbase = 4ull * s1 + 2ull * nb2 * d1;
-    uint32_t carry = 0;
-    for (uint32_t d0 = 0; d0 < nb2; d0 += 64) {
-        const uint32_t d = d0 + lane;
-        const uint32_t cap = d < nb2 ? ht_cap(ht_part_size(a, d1 * nb2 + d)) : 0u;
-        uint32_t x = cap;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(x, o, 64);
-            if (lane >= static_cast<uint32_t>(o)) x += y;
-        }
-        if (d < nb2) a.desc[static_cast<size_t>(d1) * nb2 + d] = make_uint2(static_cast<uint32_t>(rbase + carry + x - cap), cap / 2 - 1u);
-        carry += __shfl(x, 63, 64);
-    }
 }
 
 __device__ __forceinline__ void ht_insert(uint64_t* tab, uint32_t bmask, uint64_t e, uint64_t c) {
@@ -333,12 +315,14 @@ __global__ __launch_bounds__(256) void k_ht_fill(HtArgs a) {
     __syncthreads();
     for (uint32_t j = wave; j < np; j += 4) {
         const uint32_t p = p0 + j;
-        const uint2 ds = a.desc[p];
-        const uint32_t cap = 2 * (ds.y + 1);
         const uint64_t e = ht_empty(p);
-        uint64_t* out = a.table + ds.x;
+        uint32_t bstart = 0;   // the partition's first code over all segments
         {
             const uint32_t len = lane < nseg ? sb[lane][j + 1] - sb[lane][j] : 0u;
+            uint32_t b0 = lane < nseg ? sb[lane][j] : 0u;
+#pragma unroll
+            for (int o = 1; o < kHtSegs; o <<= 1) b0 += __shfl_xor(b0, o, 64);
+            bstart = __shfl(b0, 0, 64);   // lanes 0-15 hold the sum
             uint32_t x = len;
 #pragma unroll
             for (int o = 1; o < kHtSegs; o <<= 1) {
@@ -351,6 +335,14 @@ __global__ __launch_bounds__(256) void k_ht_fill(HtArgs a) {
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
         __builtin_amdgcn_wave_barrier();
         const uint32_t m = wpre[wave][nseg];
+        // the table's slots: closed form from the partition's start (a cap is
+        // at most 4 m + 2 slots), or p * cap in the uniform layout
+        uint2 ds;
+        if (a.uni && a.uni[0]) ds = make_uint2(p * a.uni[1], a.uni[1] / 2 - 1u);
+        else ds = make_uint2(4 * bstart + 2 * p, ht_cap(m) / 2 - 1u);
+        if (lane == 0) a.desc[p] = ds;
+        const uint32_t cap = 2 * (ds.y + 1);
+        uint64_t* out = a.table + ds.x;
         auto src_of = [&](uint32_t r) -> const int64_t* {
             uint32_t g = 0;
             while (g + 1 < nseg && r >= wpre[wave][g + 1]) g++;

@@ -28,8 +28,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 # timer name -> kernel family doing its work (first match wins)
 FAMILIES = [
-    (re.compile(r"^R\.p2\.hist$"), re.compile(r"phj::k_ht_hist")),
-    (re.compile(r"^R\.p2\.scatter$"), re.compile(r"phj::k_ht_scatter")),
+    (re.compile(r"^R\.p2\.scatter$"), re.compile(r"phj::k_ht_p2")),
     (re.compile(r"\.hist$"), re.compile(r"phj::k_hist")),
     (re.compile(r"\.scatter$"), re.compile(r"phj::k_scatter")),
     (re.compile(r"^build$"), re.compile(r"phj::k_(build_small|ht_fill|join_fused)")),

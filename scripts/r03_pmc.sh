@@ -1,6 +1,6 @@
 #!/bin/bash
 # Counter calibration on known byte counts (scripts/pmc_calib.hip) and the
-# on-chip probe's L2 / memory-side counters at s=1.05 (C2) and s=1.25 (C5).
+# on-chip probe's and NoPartitioning probe's L2 / memory-side counters at s=1.05 (C2, C4) and s=1.25 (C5).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 9
 mkdir -p gpurun_out/calib
@@ -23,8 +23,8 @@ for f in sorted(glob.glob("gpurun_out/calib/p*/**/*counter_collection.csv", recu
 for k in sorted(out): print(k, json.dumps(out[k]))
 json.dump(out, open("gpurun_out/calib.json", "w"), indent=1)
 PY
-for cfg in c2 c5; do
-timeout -k 10 400 python scripts/pmc_kernel.py --config $cfg --kernel "k_probe_p1|k_scatter_chunked" \
+for cfg in c2 c5 c4; do
+timeout -k 10 400 python scripts/pmc_kernel.py --config $cfg --kernel "k_probe_ht|k_scatter_chunked|k_np_probe_ct" \
   --group FETCH_SIZE --group WRITE_SIZE \
   --group TCC_HIT_sum,TCC_MISS_sum,TCC_EA0_RDREQ_sum \
   --group TCC_EA0_RDREQ_32B_sum,TCC_REQ_sum \
