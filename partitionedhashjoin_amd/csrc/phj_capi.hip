@@ -851,7 +851,7 @@ int partition_state(phj_ctx* c, SideState& S, const char* tag, const Plan& pl, b
             b.dig_wide = dbytes == 2 ? 1u : 0u;
         }
         const uint32_t grid2 = n ? nt2 : 0;
-        if (p1_only) {   // the caller consumes the pass-2 tiles itself (k_probe_p1)
+        if (p1_only) {   // the caller consumes the pass-2 tiles itself (k_probe_ht)
             S.p2 = b;
             S.nt2 = grid2;
             S.view = phj_partitioned{};

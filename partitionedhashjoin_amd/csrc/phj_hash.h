@@ -19,7 +19,7 @@
 namespace phj {
 
 // kHashed: the column already holds hash codes h(k) (the keys-only pass 1 of
-// the counting join writes them, the CSR build stores them), so hashing is
+// the counting join writes them, its code tables store them), so hashing is
 // the identity. Sound because both hashes are bijections of the 64-bit keys:
 // fmix64 is xor-shifts and multiplies by odd constants; XXH3's 8-byte path is
 // a half swap, an xor, x ^ rotl(x,49) ^ rotl(x,24) (the linear map

@@ -303,7 +303,6 @@ __global__ __launch_bounds__(256) void k_ht_fill(HtArgs a) {
     __shared__ __attribute__((aligned(16))) uint64_t wtab[4][kHtLcap];
     __shared__ uint32_t wcnt[4][kHtLcap / 2];      // per-wave bucket fill counters
     __shared__ uint32_t sb[kHtSegs][kHtPpw + 1];   // bounds of the workgroup's partitions, per segment
-    __shared__ uint32_t wpre[4][kHtSegs + 1];      // per wave: prefix of the current partition's runs
     const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const uint32_t nseg = a.nseg;
     const uint32_t P = a.nb1 * a.nb2;
@@ -316,25 +315,34 @@ __global__ __launch_bounds__(256) void k_ht_fill(HtArgs a) {
     for (uint32_t j = wave; j < np; j += 4) {
         const uint32_t p = p0 + j;
         const uint64_t e = ht_empty(p);
-        uint32_t bstart = 0;   // the partition's first code over all segments
-        {
-            const uint32_t len = lane < nseg ? sb[lane][j + 1] - sb[lane][j] : 0u;
-            uint32_t b0 = lane < nseg ? sb[lane][j] : 0u;
+        // lane g < nseg: segment g's run of p; x = inclusive prefix of the run
+        // lengths, base = where element r of p sits in segment g, minus r
+        const uint32_t len = lane < nseg ? sb[lane][j + 1] - sb[lane][j] : 0u;
+        uint32_t x = len;
 #pragma unroll
-            for (int o = 1; o < kHtSegs; o <<= 1) b0 += __shfl_xor(b0, o, 64);
-            bstart = __shfl(b0, 0, 64);   // lanes 0-15 hold the sum
-            uint32_t x = len;
-#pragma unroll
-            for (int o = 1; o < kHtSegs; o <<= 1) {
-                const uint32_t y = __shfl_up(x, o, 64);
-                if (lane >= static_cast<uint32_t>(o)) x += y;
-            }
-            if (lane < kHtSegs) wpre[wave][lane + 1] = x;
-            if (lane == 0) wpre[wave][0] = 0;
+        for (int o = 1; o < kHtSegs; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= static_cast<uint32_t>(o)) x += y;
         }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-        __builtin_amdgcn_wave_barrier();
-        const uint32_t m = wpre[wave][nseg];
+        const uint64_t base = lane < nseg ? reinterpret_cast<uint64_t>(a.codes[lane] + sb[lane][j]) - 8ull * (x - len) : 0ull;
+        uint32_t b0 = lane < nseg ? sb[lane][j] : 0u;
+#pragma unroll
+        for (int o = 1; o < kHtSegs; o <<= 1) b0 += __shfl_xor(b0, o, 64);
+        const uint32_t bstart = __builtin_amdgcn_readfirstlane(b0);   // the partition's first code over all segments
+        const uint32_t m = __builtin_amdgcn_readlane(x, nseg - 1);
+        // run ends and element bases, wave-uniform (read while every lane is
+        // active: src_of runs under divergent conditions, where a cross-lane
+        // read from an inactive lane would return garbage)
+        uint32_t xs[kHtSegs - 1];
+        uint64_t bs[kHtSegs];
+#pragma unroll
+        for (int k = 0; k < kHtSegs - 1; k++) xs[k] = __builtin_amdgcn_readlane(x, k);
+#pragma unroll
+        for (int k = 0; k < kHtSegs; k++) {
+            const uint32_t lo32 = __builtin_amdgcn_readlane(static_cast<uint32_t>(base), k);
+            const uint32_t hi32 = __builtin_amdgcn_readlane(static_cast<uint32_t>(base >> 32), k);
+            bs[k] = (static_cast<uint64_t>(hi32) << 32) | lo32;
+        }
         // the table's slots: closed form from the partition's start (a cap is
         // at most 4 m + 2 slots), or p * cap in the uniform layout
         uint2 ds;
@@ -344,9 +352,12 @@ __global__ __launch_bounds__(256) void k_ht_fill(HtArgs a) {
         const uint32_t cap = 2 * (ds.y + 1);
         uint64_t* out = a.table + ds.x;
         auto src_of = [&](uint32_t r) -> const int64_t* {
-            uint32_t g = 0;
-            while (g + 1 < nseg && r >= wpre[wave][g + 1]) g++;
-            return a.codes[g] + sb[g][j] + (r - wpre[wave][g]);
+            // element r lies in the last segment k whose run starts at or before r
+            uint64_t b = bs[0];
+#pragma unroll
+            for (int k = 1; k < kHtSegs; k++)
+                if (static_cast<uint32_t>(k) < nseg && xs[k - 1] <= r) b = bs[k];
+            return reinterpret_cast<const int64_t*>(b) + r;
         };
         if (cap <= kHtLcap && m <= CPL * 64) {
             uint64_t c[CPL];

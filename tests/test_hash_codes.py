@@ -1,6 +1,6 @@
 """Hash codes stand in for keys in the counting join (csrc/phj_hash.h kHashed).
 
-The keys-only pass 1 writes h(k) instead of k and the CSR tables store h(r),
+The keys-only pass 1 writes h(k) instead of k and the code tables store h(r),
 so the probe compares codes. That counts the key matches of
 /root/reference/src/RadixCluster/HashJoin.hpp:295-301 exactly iff h is a
 bijection of the 64-bit keys. Here both hashes are inverted step by step
