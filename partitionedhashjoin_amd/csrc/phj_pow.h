@@ -14,6 +14,14 @@
 // Checked against the host's pow on tens of millions of generator-domain and
 // random arguments (tests/test_pow.py), and device samples against the host
 // generator (tests/test_gpu_parity.py::test_gpu_generators).
+//
+// Attribution: the algorithm (log with a 128-entry table, exp with a 2^7
+// table, their polynomials and the special-case handling) is that of ARM's
+// optimized-routines math library (pow.c / pow_log_data.c / exp_data.c, MIT
+// OR Apache-2.0 WITH LLVM-exception), as shipped in glibc >= 2.28
+// (sysdeps/ieee754/dbl-64/e_pow.c, LGPL-2.1+). It is restated here from that
+// published algorithm, not copied; the coefficient tables are read from the
+// host's libm binary at generation time (phj_pow_tables.h).
 #pragma once
 
 #include <cstdint>
