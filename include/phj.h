@@ -87,6 +87,15 @@ typedef struct phj_join_params {
  * first pass then needs no histogram pass over the relation); partition
  * contents, bounds and every join count are identical either way. */
 #define PHJ_PART_STABLE 0x1
+/* flags: PHJ_TABLE_CHAINED (radix join) builds every partition's table as the
+ * reference's SeparateChainingHashTable does (SeparateChaining.hpp:143-277:
+ * buckets of slots, overflow chained on), in compacted form: per partition a
+ * bucket-chained table in HBM whose buckets are contiguous runs (CSR offsets,
+ * phj_join.h k_build_small / k_build_big), probed by k_probe. Without it the
+ * counting join uses the open-addressed code tables of LinearProbing
+ * semantics (phj_table.h). Counts are identical either way; the host driver's
+ * SeparateChainingFactory sets it. Ignored by NoPartitioning. */
+#define PHJ_TABLE_CHAINED 0x2
 #define PHJ_MAX_TIMERS 32
 #define PHJ_TIMER_NAME 24
 

@@ -23,17 +23,20 @@ __all__ = ["Context", "shard_range", "comm_unique_id", "CTX_EXCHANGE", "CTX_LOCA
 
 DEFAULT_SEED = 0x9E3779B97F4A7C15
 PART_STABLE = 0x1   # include/phj.h PHJ_PART_STABLE
+TABLE_CHAINED = 0x2   # include/phj.h PHJ_TABLE_CHAINED
 
 
 def radix_params(bits=(8, 8), num_partitions=0, hash=HASH_MURMUR3, seed=DEFAULT_SEED,
-                 stable=False) -> JoinParams:
+                 stable=False, chained=False) -> JoinParams:
     """RadixCluster parameters. num_partitions > 0 reproduces the reference's
     `hash % P` partitioning (`phjoin -p P`); otherwise q = hash & (2^(b0+b1)-1).
     stable=True asks `partition` for the reference's exact layout (input order
     inside each partition, RadixCluster/HashJoin.hpp:394-412); otherwise the
-    order inside a partition is unspecified (PHJ_PART_STABLE, include/phj.h)."""
+    order inside a partition is unspecified (PHJ_PART_STABLE, include/phj.h).
+    chained=True builds bucket-chained tables, the reference's
+    SeparateChainingHashTable (PHJ_TABLE_CHAINED)."""
     p = JoinParams()
-    p.flags = PART_STABLE if stable else 0
+    p.flags = (PART_STABLE if stable else 0) | (TABLE_CHAINED if chained else 0)
     p.algo = ALGO_RADIX
     p.hash = hash
     p.hash_seed = seed

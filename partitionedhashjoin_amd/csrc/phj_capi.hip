@@ -99,6 +99,7 @@ struct Plan {
     uint32_t Ppad = 1;    // nb1 * nb2 = final bounds length - 1
     uint32_t sub_bits = 0, sub_shift = 0;   // phj_join: sub-partitions per partition (refine_plan)
     bool stable = false;  // PHJ_PART_STABLE: the reference's order inside each partition (not compared by ==)
+    bool chained = false; // PHJ_TABLE_CHAINED: bucket-chained (CSR) tables in HBM (not compared by ==: tables only)
     bool operator==(const Plan& o) const {
         return hk == o.hk && seed == o.seed && mode == o.mode && P == o.P && npass == o.npass &&
                nb1 == o.nb1 && nb2 == o.nb2 && sub_bits == o.sub_bits && sub_shift == o.sub_shift;
@@ -350,6 +351,7 @@ int make_plan(phj_ctx* c, const phj_join_params* p, Plan& pl) {
         return set_err(c, PHJ_ERR_INVALID, "unknown hash function");
     pl = Plan{};
     pl.stable = (p->flags & PHJ_PART_STABLE) != 0;
+    pl.chained = (p->flags & PHJ_TABLE_CHAINED) != 0;
     pl.hk = p->hash;
     pl.seed = p->hash_seed;
     if (p->num_partitions > 0) {
@@ -909,7 +911,7 @@ int build_and_probe(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned*
     const uint64_t nS = c->dry ? PS.n : PS.view.n;
     // fused when the average partition fits one LDS round with margin (larger
     // ones take extra rounds, each re-probing the item's S keys)
-    if (c->tune.fused && (nR + P - 1) / P * 3 <= static_cast<uint64_t>(kFusedTcap) * 2) {
+    if (!pl.chained && c->tune.fused && (nR + P - 1) / P * 3 <= static_cast<uint64_t>(kFusedTcap) * 2) {
         // fused per-partition join with LDS tables: HashJoin.hpp:267-303
         const size_t nslots = nS / kFusedChunk + P + 1;
         PHJ_TRY(ensure(c, c->fitems, nslots * sizeof(FusedItem)));
@@ -965,7 +967,7 @@ int build_and_probe(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned*
     // partitioned bucket tables, whose build is one pass of atomics over all
     // tuples; the CSR build below gives each partition one workgroup (3.9 ms at
     // -p 32 against 0.76), while its probe is faster from -p 1024 up
-    if (c->tune.ptab > 1 || (c->tune.ptab == 1 && (nR + P - 1) / P >= 65536)) {
+    if (!pl.chained && (c->tune.ptab > 1 || (c->tune.ptab == 1 && (nR + P - 1) / P >= 65536))) {
         // partitioned bucket tables in HBM (large partitions)
         const uint32_t ratio_x256 = static_cast<uint32_t>(kNPDefaultRatio * 256);
         const size_t nbk_bound = static_cast<size_t>(nR) * ratio_x256 / 256 / kNPSlots + 2 * static_cast<size_t>(P) + 1;
@@ -1242,7 +1244,7 @@ int build_ht(phj_ctx* c, const Plan& pl, int nseg, const int64_t* const* codes, 
 // tuning knob changed the tile shape (the probe walks 512 x 4096 tiles).
 bool use_p2probe(const phj_ctx* c, const Plan& pl, uint64_t nS, uint64_t nR) {
     bool wc = false;
-    return c->tune.p2probe && pl.npass == 2 && tile_shape(c, pl.nb2).tile == 4096 && tile_shape(c, pl.nb2).block == 512 &&
+    return c->tune.p2probe && !pl.chained && pl.npass == 2 && tile_shape(c, pl.nb2).tile == 4096 && tile_shape(c, pl.nb2).block == 512 &&
            pass_tile(c, static_cast<uint32_t>(std::min<uint64_t>(nS, 0xffffffffu)), pl.nb1, &wc) == 4096 && !wc &&
            probe_ht_lds_bytes(kProbeBlock * kProbeItems, pl.nb2) <= 160 * 1024 &&
            4 * nR + 2ull * pl.Ppad < (1ull << 32);

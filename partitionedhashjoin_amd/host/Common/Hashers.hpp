@@ -62,10 +62,11 @@ class Murmur3Hasher : public IHasher {
 namespace HashTables {
 
 // Table descriptors of the reference's factories (LinearProbing.hpp:16-18,
-// 212-227; SeparateChaining.hpp:16-18, 279-294). On the device the radix join
-// always builds per-partition bucket-chained tables and the no-partitioning
-// join a bucketized linear-probing table; the factory contributes its hasher
-// and its size ratio (slots per build tuple = ratio x bucket slots).
+// 212-227; SeparateChaining.hpp:16-18, 279-294). The factory contributes its
+// hasher, its size ratio (slots per build tuple = ratio x bucket slots) and
+// the radix join's table kind: open-addressed code tables for LinearProbing,
+// bucket-chained tables (PHJ_TABLE_CHAINED) for SeparateChaining. The
+// no-partitioning join always uses its own global table.
 struct LinearProbingConfiguration {
     double HASH_TABLE_SIZE_RATIO = 1.25;
 };
@@ -77,6 +78,7 @@ template <typename BucketValueType, size_t BucketSize, typename HasherType>
 class LinearProbingFactory {
    public:
     using Hasher = HasherType;
+    static constexpr uint8_t kTableFlags = 0;
     LinearProbingFactory(const LinearProbingConfiguration& configuration, HasherType hasher)
         : m_hasher(hasher), m_configuration(configuration) {}
     const HasherType& GetHasher() const { return m_hasher; }
@@ -91,6 +93,7 @@ template <typename BucketValueType, size_t BucketSize, typename HasherType>
 class SeparateChainingFactory {
    public:
     using Hasher = HasherType;
+    static constexpr uint8_t kTableFlags = PHJ_TABLE_CHAINED;
     SeparateChainingFactory(const SeparateChainingConfiguration& configuration, HasherType hasher)
         : m_hasher(hasher), m_configuration(configuration) {}
     const HasherType& GetHasher() const { return m_hasher; }

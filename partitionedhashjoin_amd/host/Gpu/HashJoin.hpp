@@ -137,6 +137,7 @@ class HashJoiner {
         p.algo = PHJ_ALGO_RADIX;
         p.hash = HasherType::kKind;
         p.hash_seed = m_hasher.Seed();
+        p.flags = HashTableFactory::kTableFlags;   // the factory's table kind
         if (m_gpu.RadixBits[0] > 0) {
             p.num_partitions = 0;
             p.radix_bits[0] = static_cast<uint8_t>(m_gpu.RadixBits[0]);

@@ -118,6 +118,9 @@ ALL_PARAMS = [
     ("radix-mod32", phj.radix_params(num_partitions=32, hash=phj.HASH_XXH3, seed=SEED)),
     ("radix-mod1", phj.radix_params(num_partitions=1, hash=phj.HASH_XXH3, seed=1)),
     ("radix-mod5000", phj.radix_params(num_partitions=5000, hash=phj.HASH_XXH3, seed=2)),
+    # bucket-chained tables, the reference's SeparateChainingHashTable (PHJ_TABLE_CHAINED)
+    ("radix-8+8-chained", phj.radix_params((8, 8), hash=phj.HASH_MURMUR3, seed=SEED, chained=True)),
+    ("radix-mod1000-chained", phj.radix_params(num_partitions=1000, hash=phj.HASH_XXH3, seed=4, chained=True)),
 ]
 
 
