@@ -1235,7 +1235,8 @@ int build_ht(phj_ctx* c, const Plan& pl, int nseg, const int64_t* const* codes, 
     a.table = static_cast<uint64_t*>(c->ht_tab.p);
     a.desc = static_cast<uint2*>(c->ht_desc.p);
     a.uni = uni;
-    hipLaunchKernelGGL(k_ht_fill, dim3((P + kHtPpw - 1) / kHtPpw), dim3(256), 0, c->ks, a);
+    if (nseg == 1) hipLaunchKernelGGL(k_ht_fill<true>, dim3((P + kHtPpw - 1) / kHtPpw), dim3(256), 0, c->ks, a);
+    else hipLaunchKernelGGL(k_ht_fill<false>, dim3((P + kHtPpw - 1) / kHtPpw), dim3(256), 0, c->ks, a);
     PHJ_LAUNCHED(c, "k_ht_fill");
     return PHJ_OK;
 }

@@ -296,6 +296,7 @@ __device__ __forceinline__ void ht_insert(uint64_t* tab, uint32_t bmask, uint64_
 // probe onwards with compare-and-swap, and the table is written out in 16-B
 // stores. Duplicates may take two slots: harmless to a set test, and the cap
 // counts them.
+template <bool ONE>   // ONE: a single build segment (one device): element r is at codes[0] + start + r
 __global__ __launch_bounds__(256) void k_ht_fill(HtArgs a) {
     // codes per lane: a partition that fits the slice at load <= 0.8 (the
     // uniform layout's bound; the radix layout's caps keep it <= 2/3)
@@ -330,19 +331,7 @@ __global__ __launch_bounds__(256) void k_ht_fill(HtArgs a) {
         for (int o = 1; o < kHtSegs; o <<= 1) b0 += __shfl_xor(b0, o, 64);
         const uint32_t bstart = __builtin_amdgcn_readfirstlane(b0);   // the partition's first code over all segments
         const uint32_t m = __builtin_amdgcn_readlane(x, nseg - 1);
-        // run ends and element bases, wave-uniform (read while every lane is
-        // active: src_of runs under divergent conditions, where a cross-lane
-        // read from an inactive lane would return garbage)
-        uint32_t xs[kHtSegs - 1];
-        uint64_t bs[kHtSegs];
-#pragma unroll
-        for (int k = 0; k < kHtSegs - 1; k++) xs[k] = __builtin_amdgcn_readlane(x, k);
-#pragma unroll
-        for (int k = 0; k < kHtSegs; k++) {
-            const uint32_t lo32 = __builtin_amdgcn_readlane(static_cast<uint32_t>(base), k);
-            const uint32_t hi32 = __builtin_amdgcn_readlane(static_cast<uint32_t>(base >> 32), k);
-            bs[k] = (static_cast<uint64_t>(hi32) << 32) | lo32;
-        }
+        const uint32_t base_lo = static_cast<uint32_t>(base), base_hi = static_cast<uint32_t>(base >> 32);
         // the table's slots: closed form from the partition's start (a cap is
         // at most 4 m + 2 slots), or p * cap in the uniform layout
         uint2 ds;
@@ -351,20 +340,29 @@ __global__ __launch_bounds__(256) void k_ht_fill(HtArgs a) {
         if (lane == 0) a.desc[p] = ds;
         const uint32_t cap = 2 * (ds.y + 1);
         uint64_t* out = a.table + ds.x;
+        // element r lies in the last segment g whose run starts at or before r:
+        // a binary search over the run ends held lane-wise (lane k: x_k). The
+        // cross-lane reads need every lane active: src_of is only called
+        // outside divergent branches (r clamped, the load conditional after)
         auto src_of = [&](uint32_t r) -> const int64_t* {
-            // element r lies in the last segment k whose run starts at or before r
-            uint64_t b = bs[0];
+            if constexpr (ONE) return a.codes[0] + sb[0][j] + r;
+            int g = 0;
 #pragma unroll
-            for (int k = 1; k < kHtSegs; k++)
-                if (static_cast<uint32_t>(k) < nseg && xs[k - 1] <= r) b = bs[k];
-            return reinterpret_cast<const int64_t*>(b) + r;
+            for (int step = kHtSegs / 2; step >= 1; step >>= 1) {
+                const int cand = g + step;
+                const uint32_t xv = __shfl(x, cand - 1, 64);
+                if (static_cast<uint32_t>(cand) < nseg && xv <= r) g = cand;
+            }
+            const uint32_t lo32 = __shfl(base_lo, g, 64), hi32 = __shfl(base_hi, g, 64);
+            return reinterpret_cast<const int64_t*>((static_cast<uint64_t>(hi32) << 32) | lo32) + r;
         };
         if (cap <= kHtLcap && m <= CPL * 64) {
             uint64_t c[CPL];
 #pragma unroll
             for (uint32_t i = 0; i < CPL; i++) {
                 const uint32_t r = i * 64 + lane;
-                c[i] = r < m ? static_cast<uint64_t>(*src_of(r)) : 0ull;
+                const int64_t* src = src_of(min(r, m - 1u));   // every lane (m >= 1 when any loads)
+                c[i] = r < m ? static_cast<uint64_t>(*src) : 0ull;
             }
             uint32_t* bc = wcnt[wave];
             for (uint32_t sl = lane; sl < cap; sl += 64) wtab[wave][sl] = e;
@@ -406,7 +404,11 @@ __global__ __launch_bounds__(256) void k_ht_fill(HtArgs a) {
             for (uint32_t sl = lane; sl < cap; sl += 64) out[sl] = e;
             __threadfence();
             __builtin_amdgcn_wave_barrier();
-            for (uint32_t r = lane; r < m; r += 64) ht_insert(out, ds.y, e, static_cast<uint64_t>(*src_of(r)));
+            for (uint32_t r0 = 0; r0 < m; r0 += 64) {   // wave-uniform trip count
+                const uint32_t r = r0 + lane;
+                const int64_t* src = src_of(min(r, m - 1u));
+                if (r < m) ht_insert(out, ds.y, e, static_cast<uint64_t>(*src));
+            }
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
         __builtin_amdgcn_wave_barrier();
