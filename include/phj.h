@@ -161,6 +161,24 @@ int phj_ctx_info(const phj_ctx *ctx, int *world, int *rank0, int *nlocal);
 /* Host-only: rows [lo, hi) of an n-row relation held by `rank` of `world` ranks
  * (the range sharding of every multi-device context). */
 void phj_shard_range(uint64_t n, int rank, int world, uint64_t *lo, uint64_t *hi);
+/* ---- the multi-GPU exchange protocol (host-only; csrc/phj_group.h) ----
+ * Replaces nothing in the reference (its parallel split is a thread pool,
+ * src/main.cpp:235-241). These ARE the rules phj_join's member step applies,
+ * exported so that a caller driving its own transport, and the CPU tests over
+ * gloo, follow the same layout and reduction:
+ *  - the exchange block of one rank (the all-gathered unit, int64 elements):
+ *    its build codes in final partition order, zero padded to *codes_elems
+ *    (a multiple of 64, >= the largest rank's shard), then the partition bounds
+ *    (num_partitions + 1 uint32, two per element), *block_elems in all; a rank
+ *    that failed before the all-gather still takes part with an all-zero
+ *    block (bounds all 0: an empty build segment);
+ *  - the count all-reduce (sum, uint64): every rank contributes the two words
+ *    of phj_count_contribution; phj_count_verdict turns the sum into the global
+ *    count, or PHJ_ERR_STATE when any rank failed. */
+void phj_exchange_layout(uint64_t max_shard, uint32_t num_partitions, uint64_t *codes_elems,
+                         uint64_t *block_elems);
+void phj_count_contribution(uint64_t count, int failed, uint64_t words[2]);
+int phj_count_verdict(const uint64_t words[2], uint64_t *matches);
 void phj_ctx_destroy(phj_ctx *ctx);
 const char *phj_last_error(const phj_ctx *ctx);
 /* Run on an external stream (e.g. torch.cuda.current_stream()); NULL = ctx-owned stream.

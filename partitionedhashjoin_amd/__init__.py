@@ -17,7 +17,7 @@ from . import _capi
 from ._capi import (ALGO_NO_PARTITIONING, ALGO_RADIX, CTX_EXCHANGE, CTX_LOCAL, HASH_MURMUR3, HASH_XXH3, SIDE_BUILD,
                     SIDE_PROBE, JoinParams, JoinResult, Partitioned, PhjError)
 
-__all__ = ["Context", "shard_range", "comm_unique_id", "CTX_EXCHANGE", "CTX_LOCAL", "radix_params", "nopart_params", "JoinParams", "JoinResult",
+__all__ = ["Context", "shard_range", "exchange_layout", "count_contribution", "count_verdict", "comm_unique_id", "CTX_EXCHANGE", "CTX_LOCAL", "radix_params", "nopart_params", "JoinParams", "JoinResult",
            "Partitioned", "PhjError", "ALGO_RADIX", "ALGO_NO_PARTITIONING", "HASH_XXH3",
            "HASH_MURMUR3", "SIDE_BUILD", "SIDE_PROBE", "DEFAULT_SEED"]
 
@@ -63,6 +63,35 @@ def shard_range(n: int, rank: int, world: int):
     lo, hi = C.c_uint64(), C.c_uint64()
     L.phj_shard_range(n, rank, world, C.byref(lo), C.byref(hi))
     return lo.value, hi.value
+
+
+def exchange_layout(max_shard: int, num_partitions: int):
+    """(codes_elems, block_elems) of one rank's exchange block: codes, zero
+    padded, then num_partitions + 1 uint32 bounds (phj_exchange_layout; host only)."""
+    L = _capi.load()
+    a, b = C.c_uint64(), C.c_uint64()
+    L.phj_exchange_layout(max_shard, num_partitions, C.byref(a), C.byref(b))
+    return a.value, b.value
+
+
+def count_contribution(count: int, failed: bool = False) -> np.ndarray:
+    """The two uint64 words a rank adds to the count all-reduce (phj_count_contribution)."""
+    L = _capi.load()
+    w = (C.c_uint64 * 2)()
+    L.phj_count_contribution(count, 1 if failed else 0, w)
+    return np.array([w[0], w[1]], dtype=np.uint64)
+
+
+def count_verdict(words) -> int:
+    """The global count from the all-reduced words; PhjError(PHJ_ERR_STATE) when a
+    rank failed (phj_count_verdict)."""
+    L = _capi.load()
+    w = (C.c_uint64 * 2)(int(words[0]), int(words[1]))
+    m = C.c_uint64()
+    rc = L.phj_count_verdict(w, C.byref(m))
+    if rc != 0:
+        raise PhjError(rc, f"{int(words[1])} rank(s) failed during the join")
+    return m.value
 
 
 def comm_unique_id() -> bytes:

@@ -39,6 +39,7 @@ EXPORTED = [
     "phj_prepare", "phj_join_materialize", "phj_joined_rows", "phj_joined_download",
     "phj_ctx_create_ex", "phj_ctx_create_device", "phj_comm_unique_id", "phj_ctx_create_rank",
     "phj_ctx_info", "phj_shard_range", "phj_probe_pass1",
+    "phj_exchange_layout", "phj_count_contribution", "phj_count_verdict",
 ]
 ABI_VERSION = 2
 CTX_EXCHANGE = 0x1   # phj_ctx_create_ex: the multi-GPU path on one device (RCCL world of one)
@@ -112,6 +113,9 @@ def load():
         "phj_ctx_create_rank": (i, [i, i, i, C.c_char_p, C.POINTER(P)]),
         "phj_ctx_info": (i, [P, C.POINTER(i), C.POINTER(i), C.POINTER(i)]),
         "phj_shard_range": (None, [u64, i, i, C.POINTER(u64), C.POINTER(u64)]),
+        "phj_exchange_layout": (None, [u64, C.c_uint32, C.POINTER(u64), C.POINTER(u64)]),
+        "phj_count_contribution": (None, [u64, i, C.POINTER(u64)]),
+        "phj_count_verdict": (i, [C.POINTER(u64), C.POINTER(u64)]),
         "phj_ctx_destroy": (None, [P]),
         "phj_last_error": (C.c_char_p, [P]),
         "phj_ctx_set_stream": (i, [P, P]),

@@ -453,6 +453,19 @@ DigitFn digit_fn(const Plan& pl, int pass) {
     return f;
 }
 
+// E_0 of the plan's code tables (phj_table.h ht_empty): the lowest power of
+// two whose final partition is not 0. Code 0 is in partition 0 under every
+// partition function, so E_p = 0 serves every other partition. 1 for radix bits
+// and h % P with P >= 2; 2^40 for h % 1 split into sub-partitions at bit 40
+// (code 1 is in partition 0 there); 0 when the plan has one final partition
+// (no code lies elsewhere: use_p2probe then declines the code tables).
+uint64_t plan_empty0(const Plan& pl) {
+    const DigitFn f = digit_fn(pl, 1);
+    for (int b = 0; b < 64; b++)
+        if (q_from_hash(1ull << b, f) != 0) return 1ull << b;
+    return 0;
+}
+
 int scan_u32(phj_ctx* c, uint32_t* data, uint32_t len, uint32_t narrays, uint32_t stride,
              DevBuf* scratch = nullptr) {
     if (len == 0) return PHJ_OK;
@@ -1232,6 +1245,7 @@ int build_ht(phj_ctx* c, const Plan& pl, int nseg, const int64_t* const* codes, 
     a.nseg = static_cast<uint32_t>(nseg);
     a.nb1 = pl.nb1;
     a.nb2 = pl.nb2;
+    a.e1 = plan_empty0(pl);
     a.table = static_cast<uint64_t*>(c->ht_tab.p);
     a.desc = static_cast<uint2*>(c->ht_desc.p);
     a.uni = uni;
@@ -1248,7 +1262,7 @@ bool use_p2probe(const phj_ctx* c, const Plan& pl, uint64_t nS, uint64_t nR) {
     return c->tune.p2probe && !pl.chained && pl.npass == 2 && tile_shape(c, pl.nb2).tile == 4096 && tile_shape(c, pl.nb2).block == 512 &&
            pass_tile(c, static_cast<uint32_t>(std::min<uint64_t>(nS, 0xffffffffu)), pl.nb1, &wc) == 4096 && !wc &&
            probe_ht_lds_bytes(kProbeBlock * kProbeItems, pl.nb2) <= 160 * 1024 &&
-           4 * nR + 2ull * pl.Ppad < (1ull << 32);
+           4 * nR + 2ull * pl.Ppad < (1ull << 32) && plan_empty0(pl) != 0;
 }
 
 // Probe a probe-side pass-1 output (partition_state p1_only) against the
@@ -1262,6 +1276,7 @@ int probe_ht(phj_ctx* c, const Plan& pl, SideState& PS, bool clear = true) {
     pa.table = static_cast<const uint64_t*>(c->ht_tab.p);
     pa.count = static_cast<unsigned long long*>(c->count.p);
     pa.seed = pl.seed;
+    pa.e1 = plan_empty0(pl);
     pa.nb2 = pl.nb2;
     constexpr int B = kProbeBlock, I = kProbeItems;
     const size_t lds = probe_ht_lds_bytes(B * I, pl.nb2);
@@ -1349,10 +1364,10 @@ int join_nopart_ct(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
         const auto* dsc = static_cast<const uint2*>(c->ht_desc.p);
         const uint32_t* un = uni;
         auto* cnt = static_cast<unsigned long long*>(c->count.p);
-        uint64_t nS64 = S.n, seed = p->hash_seed;
+        uint64_t nS64 = S.n, seed = p->hash_seed, e1 = plan_empty0(pl);
         uint32_t Pv = P;
         void* kargs[] = {const_cast<longlong2**>(&S_rel), &nS64, const_cast<uint64_t**>(&tab), const_cast<uint2**>(&dsc),
-                         const_cast<uint32_t**>(&un), &Pv, &seed, &cnt};
+                         const_cast<uint32_t**>(&un), &Pv, &seed, &e1, &cnt};
         PHJ_HIP(c, hipLaunchKernel(kfn, dim3(grid), dim3(256), kargs, 0, c->ks));
         PHJ_LAUNCHED(c, "k_np_probe_ct");
         PHJ_TRY(timer_end(c));
@@ -1816,6 +1831,23 @@ void phj_shard_range(uint64_t n, int rank, int world, uint64_t* lo, uint64_t* hi
     if (world >= 1 && rank >= 0 && rank < world) shard_range(n, rank, world, &a, &b);
     if (lo) *lo = a;
     if (hi) *hi = b;
+}
+
+void phj_exchange_layout(uint64_t max_shard, uint32_t num_partitions, uint64_t* codes_elems, uint64_t* block_elems) {
+    const uint64_t cap = (max_shard + 63) / 64 * 64;   // both columns stay 16-B aligned in the gathered buffer
+    if (codes_elems) *codes_elems = cap;
+    if (block_elems) *block_elems = cap + (static_cast<uint64_t>(num_partitions) + 2) / 2;
+}
+
+void phj_count_contribution(uint64_t count, int failed, uint64_t* words) {
+    words[0] = failed ? 0 : count;
+    words[1] = failed ? 1 : 0;
+}
+
+int phj_count_verdict(const uint64_t* words, uint64_t* matches) {
+    if (words[1] != 0) return PHJ_ERR_STATE;
+    if (matches) *matches = words[0];
+    return PHJ_OK;
 }
 
 void phj_ctx_destroy(phj_ctx* c) {

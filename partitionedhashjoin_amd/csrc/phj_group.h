@@ -194,17 +194,15 @@ void shard_range(uint64_t n, int rank, int world, uint64_t* lo, uint64_t* hi) {
     *hi = static_cast<uint64_t>((static_cast<unsigned __int128>(n) * (rank + 1)) / world);
 }
 
-// Radix exchange block of one rank: build keys[maxn] | bounds[P + 1] (uint32,
-// two per int64 element); maxn is padded to 64 elements so both columns stay
-// 16-B aligned inside the gathered buffer.
+// Radix exchange block of one rank: build codes[maxn] | bounds[P + 1] (uint32,
+// two per int64 element), the layout of phj_exchange_layout (include/phj.h).
 struct PackLayout {
     uint64_t maxn, elems;
 };
 
 PackLayout pack_layout(uint64_t maxn, uint32_t P) {
     PackLayout l;
-    l.maxn = (maxn + 63) / 64 * 64;
-    l.elems = l.maxn + (static_cast<uint64_t>(P) + 2) / 2;
+    phj_exchange_layout(maxn, P, &l.maxn, &l.elems);
     return l;
 }
 
@@ -312,9 +310,13 @@ uint64_t total(const std::vector<uint64_t>& v) {
 // nobody copies when any member failed (its block may not exist).
 // With RCCL a member that failed before the collective still takes part in it
 // (its peers have enqueued theirs and would otherwise wait forever): it sends
-// whatever its block holds and reports the failure through the count
-// all-reduce (allreduce_count). Only when it has no buffers to take part with
-// does it abort its communicator, which ends the peers' collective with an error.
+// an all-zero block, a valid empty build segment (every bound 0), so the peers
+// build and probe sound tables, and it reports the failure through the count
+// all-reduce (allreduce_count), which makes every rank return PHJ_ERR_STATE.
+// Only when it has no buffers to take part with does it abort its
+// communicator: the last resort, since ncclCommAbort tears down the local
+// communicator only, and peers blocked in the collective over P2P/SHM may not
+// see an error and keep waiting.
 int abort_comm(Group& G, int i, int rc) {
     if (G.kind == Xchg::kRccl && G.comm[i]) {
         (void)rccl().CommAbort(G.comm[i]);
@@ -330,6 +332,8 @@ int allgather_blocks(Group& G, int i, uint64_t elems, bool ok, bool receive = tr
         if (!G.comm[i]) return set_err(c, PHJ_ERR_STATE, "RCCL communicator aborted by an earlier failure");
         if (!B.send.p || !B.recv.p || B.send.bytes < elems * 8 || B.recv.bytes < static_cast<size_t>(G.world) * elems * 8)
             return abort_comm(G, i, ok ? set_err(c, PHJ_ERR_STATE, "exchange buffers missing") : PHJ_ERR_STATE);
+        if (!ok && hipMemsetAsync(B.send.p, 0, elems * 8, c->ks) != hipSuccess)
+            return abort_comm(G, i, PHJ_ERR_STATE);   // cannot send a valid empty segment
         PHJ_NCCL(c, rccl().AllGather(B.send.p, B.recv.p, elems, ncclInt64, G.comm[i], c->ks));
         c->since_ev++;
         return ok ? PHJ_OK : PHJ_ERR_STATE;
@@ -364,8 +368,11 @@ int allreduce_count(Group& G, int i, const void* local_count, bool failed = fals
         if (!G.comm[i]) return set_err(c, PHJ_ERR_STATE, "RCCL communicator aborted by an earlier failure");
         auto* d = static_cast<uint64_t*>(B.cnt.p);
         if (!d) return abort_comm(G, i, set_err(c, PHJ_ERR_STATE, "count buffer missing"));
+        // this rank's words of phj_count_contribution: {count, 0}, or {0, 1} when it failed
+        uint64_t w[2];
+        phj_count_contribution(0, failed ? 1 : 0, w);
         PHJ_HIP(c, hipMemsetAsync(d + 2, 0, 16, c->ks));
-        if (failed) PHJ_HIP(c, hipMemsetAsync(d + 3, 1, 1, c->ks));
+        if (failed) PHJ_HIP(c, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d + 3), static_cast<uint32_t>(w[1]), 1, c->ks));
         else PHJ_HIP(c, hipMemcpyAsync(d + 2, local_count, 8, hipMemcpyDeviceToDevice, c->ks));
         PHJ_NCCL(c, rccl().AllReduce(d + 2, d, 2, ncclUint64, ncclSum, G.comm[i], c->ks));
     } else {
@@ -381,9 +388,13 @@ int read_count(Group& G, int i, uint64_t* out) {
     unsigned long long h[2] = {0, 0};
     PHJ_HIP(c, hipMemcpyAsync(h, G.buf[i].cnt.p, 16, hipMemcpyDeviceToHost, c->ks));
     PHJ_HIP(c, hipStreamSynchronize(c->ks));
-    if (G.kind == Xchg::kRccl && h[1] != 0)
+    if (G.kind == Xchg::kLocal) {
+        *out = h[0];
+        return PHJ_OK;
+    }
+    const uint64_t words[2] = {h[0], h[1]};
+    if (phj_count_verdict(words, out) != PHJ_OK)
         return set_err(c, PHJ_ERR_STATE, std::to_string(h[1]) + " rank(s) failed during the join");
-    *out = h[0];
     return PHJ_OK;
 }
 

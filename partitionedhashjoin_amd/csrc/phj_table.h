@@ -25,8 +25,14 @@
 // (the count is a semi-join, a set test). There is no occupancy word and no
 // key value is reserved: an empty slot holds E_p, a code of ANOTHER
 // partition, which no code probing p can equal. Every partition function maps
-// code 0 to partition 0 and code 1 elsewhere (q_from_hash: radix bits, h % P
-// and sub-partitions alike), so E_p = (p == 0 ? 1 : 0). A probe reads one
+// code 0 to partition 0 (q_from_hash: radix bits, h % P and sub-partitions
+// alike), so E_p = 0 for p != 0, and E_0 = e1, a code the plan's partition
+// function sends elsewhere (phj_capi.hip plan_empty0: the lowest power of two
+// outside partition 0 -- 1 for radix bits and h % P with P >= 2, but 2^40 for
+// h % 1 split into sub-partitions at bit 40, where code 1 IS in partition 0;
+// a plan with one final partition has no such code and gets no code tables).
+// The reference marks occupancy with a fill counter, never a key value
+// (src/HashTables/LinearProbing.hpp:79-82). A probe reads one
 // 16-B bucket (one cache line) and stops at a match or an empty slot; the CSR
 // form needed a home slot plus, for a quarter to a half of the keys, a second
 // line.
@@ -56,7 +62,8 @@ __host__ __device__ __forceinline__ uint32_t ht_cap(uint32_t m) {
     return c;
 }
 
-__host__ __device__ __forceinline__ uint64_t ht_empty(uint32_t p) { return p == 0 ? 1ull : 0ull; }
+// E_p: e1 (a code outside partition 0) for partition 0, else code 0
+__host__ __device__ __forceinline__ uint64_t ht_empty(uint32_t p, uint64_t e1) { return p == 0 ? e1 : 0ull; }
 
 // Rank of this lane's digit d among the tile's keys of digit d (counter row
 // C): phj_partition.h agg_rank_lds.
@@ -257,6 +264,7 @@ struct HtArgs {
     const int64_t* codes[kHtSegs];
     const uint32_t* bounds[kHtSegs];   // P + 1 each
     uint32_t nseg, nb1, nb2, pad;
+    uint64_t e1;                       // E_0 (ht_empty)
     uint64_t* table;                   // slots (4 |R| + 2 P bound)
     uint2* desc;                       // per final partition: {slot base (even), buckets - 1}, written by k_ht_fill
     const uint32_t* uni;               // nullptr, or {1, cap}: every partition gets cap slots at p * cap (k_np_ct_plan)
@@ -315,7 +323,7 @@ __global__ __launch_bounds__(256) void k_ht_fill(HtArgs a) {
     __syncthreads();
     for (uint32_t j = wave; j < np; j += 4) {
         const uint32_t p = p0 + j;
-        const uint64_t e = ht_empty(p);
+        const uint64_t e = ht_empty(p, a.e1);
         // lane g < nseg: segment g's run of p; x = inclusive prefix of the run
         // lengths, base = where element r of p sits in segment g, minus r
         const uint32_t len = lane < nseg ? sb[lane][j + 1] - sb[lane][j] : 0u;
@@ -441,6 +449,7 @@ struct HtProbeArgs {
     const uint64_t* table;
     unsigned long long* count;
     uint64_t seed;
+    uint64_t e1;                 // E_0 (ht_empty)
     uint32_t nb2;
     uint32_t pad;
 };
@@ -586,7 +595,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
             __syncthreads();   // B3
             // probe: all items' home buckets in flight at once, then the walks
             // of every item still pending advance together, one bucket a round
-            const uint64_t e0 = d1 == 0 ? 1ull : 0ull;   // E of partition (d1, d2): 1 only for partition 0
+            const uint64_t e0 = d1 == 0 ? pa.e1 : 0ull;   // E of partition (d1, d2): e1 only for partition 0
             const ulonglong2* tab2 = reinterpret_cast<const ulonglong2*>(pa.table);
             ulonglong2 v[ITEMS];
 #pragma unroll
@@ -675,7 +684,7 @@ __global__ __launch_bounds__(256) void k_np_ct_plan(const uint32_t* bounds, uint
 template <int HK, int ITEMS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_np_probe_ct(
     const longlong2* S, uint64_t nS, const uint64_t* table, const uint2* desc, const uint32_t* uni, uint32_t P,
-    uint64_t seed, unsigned long long* count) {
+    uint64_t seed, uint64_t e1, unsigned long long* count) {
     const bool uniform = __builtin_amdgcn_readfirstlane(uni[0]) != 0;
     const uint32_t nbk = __builtin_amdgcn_readfirstlane(uni[1]) / 2;   // buckets per region (uniform)
     const ulonglong2* tab2 = reinterpret_cast<const ulonglong2*>(table);
@@ -709,7 +718,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
 #pragma unroll
         for (int i = 0; i < ITEMS; i++) {
             if (base + i * 256 + tid < nS) {
-                const uint64_t e = (static_cast<uint32_t>(c[i]) & (P - 1)) == 0 ? 1ull : 0ull;
+                const uint64_t e = ht_empty(static_cast<uint32_t>(c[i]) & (P - 1), e1);
                 bool hit = v[i].x == c[i] || v[i].y == c[i];
                 if (!hit && v[i].y != e) {   // home bucket full, no match: walk on
                     uint32_t b = bk[i];

@@ -1,5 +1,4 @@
-"""Multi-GPU join: thin callers of the C ABI's multi-device contexts, and the
-CPU rehearsal of the same step.
+"""Multi-GPU join: thin callers of the C ABI's multi-device contexts.
 
 The reference is single-process (no distributed runtime); this
 layer follows BASELINE.json's north star. The join itself lives in
@@ -17,49 +16,14 @@ Two ways to run it, both one C call per join:
     only hands rank 0's RCCL unique id to the other ranks over
     torch.distributed and creates the rank's context (phj_ctx_create_rank).
 
-`distributed_join` / `distributed_join_nopart` restate the per-rank step over
-torch.distributed collectives for an engine interface; the CPU tests run them
-with an oracle engine over gloo (world 2-3), so the sharding, the exchange
-layout (padded key blocks | bounds, the real shard sizes gathered first) and
-the count reduction are covered without a GPU.
+The exchange layout and the count reduction the member step applies are the
+library's own host-only functions (phj_exchange_layout, phj_count_contribution,
+phj_count_verdict, include/phj.h); tests/test_distributed.py drives them over
+gloo on CPU (world 2-3).
 """
 from __future__ import annotations
 
-from dataclasses import dataclass
-
-import numpy as np
-
-from . import Context, comm_unique_id, CTX_EXCHANGE
-
-
-def shard_range(n: int, rank: int, world: int):
-    """Rows [lo, hi) of an n-row relation held by `rank`: the range sharding
-    every multi-device context applies (phj_shard_range, csrc/phj_group.h
-    shard_range; tests/test_distributed.py pins the two together). Pure Python,
-    so the CPU rehearsal needs no HIP runtime."""
-    if not 0 <= rank < world:
-        return (0, 0)
-    return ((n * rank) // world, (n * (rank + 1)) // world)
-
-
-def max_shard(n: int, world: int) -> int:
-    return max(hi - lo for lo, hi in (shard_range(n, r, world) for r in range(world)))
-
-
-def pack_layout(maxn: int, P: int):
-    """int64 elements of one rank's exchange block: keys[maxn] | bounds[P+1]
-    (uint32, two per element), maxn padded to 64 elements (csrc/phj_group.h
-    PackLayout). Only the keys travel: the join tests key equality and never
-    reads a build payload (RadixCluster/HashJoin.hpp:295-301)."""
-    maxn = (maxn + 63) // 64 * 64
-    return maxn, maxn + (P + 2) // 2
-
-
-@dataclass
-class DistResult:
-    matches: int             # global semi-join count (all-reduced)
-    local_matches: int
-    timers: list             # this rank's per-kernel device timers (name, ms, bytes)
+from . import Context, comm_unique_id, CTX_EXCHANGE, shard_range
 
 
 # ---- the GPU path: multi-device contexts ----
@@ -90,78 +54,3 @@ def generate_shards(ctx: Context, nR: int, nS: int, alpha: float, seed: int, ran
     slo, shi = shard_range(nS, r, w)
     ctx.generate_sequential(0, rhi - rlo, start, rlo)
     ctx.generate_zipf(1, shi - slo, alpha, 1, nR, seed, slo)
-
-
-# ---- the step over torch.distributed (CPU rehearsal with an engine) ----
-
-def _all_gather(dist, out, inp):
-    dist.all_gather_into_tensor(out, inp)
-
-
-def _all_reduce(dist, t):
-    dist.all_reduce(t)
-
-
-def distributed_join(engine, params, nR: int, nS: int, rank: int, world: int, dist=None):
-    """The member step of csrc/phj_group.h over torch.distributed: partition
-    the R shard, all-gather the real shard sizes, pack keys | bounds into
-    padded blocks, all-gather them, join the local S shard against every
-    block, all-reduce the count."""
-    torch = engine.torch
-    view = engine.partition(0, params)
-    engine.partition(1, params)
-    if world == 1:
-        cnt = engine.join_local(params, view)
-        m = int(cnt.item())
-        return DistResult(matches=m, local_matches=m, timers=engine.timers())
-    P = view.num_partitions
-    # the real shard sizes (not the nominal ranges: a caller may bind its own shards)
-    n_local = torch.tensor([view.n], dtype=torch.int64)
-    sizes_t = torch.zeros(world, dtype=torch.int64)
-    _all_gather(dist, sizes_t, n_local)
-    sizes = [int(x) for x in sizes_t]
-    maxn = max(sizes)
-    send = engine.pack(view, maxn, P)
-    recv = engine.tensor(world * send.numel(), torch.int64)
-    _all_gather(dist, recv, send)
-    cnt = engine.join_packed(params, recv, sizes, maxn, P)
-    local = int(cnt.item())
-    _all_reduce(dist, cnt)
-    return DistResult(matches=int(cnt.item()), local_matches=local, timers=engine.timers())
-
-
-def distributed_join_nopart(engine, params, nR: int, nS: int, rank: int, world: int, dist=None):
-    """NoPartitioning over range shards (§8(e)): the R shards are gathered
-    (all-gather-v: real sizes first, padded blocks, compacted), every rank
-    builds the global table and probes its S shard, the counts are summed."""
-    torch = engine.torch
-    shard = engine.build_shard()
-    if world == 1:
-        cnt = engine.join_nopart_replicated(params, shard)
-        m = int(cnt.item())
-        return DistResult(matches=m, local_matches=m, timers=[])
-    sizes_t = torch.zeros(world, dtype=torch.int64)
-    _all_gather(dist, sizes_t, torch.tensor([shard.shape[0]], dtype=torch.int64))
-    sizes = [int(x) for x in sizes_t]
-    maxn = max(sizes)
-    send = shard.new_zeros((maxn, 2))
-    send[:shard.shape[0]].copy_(shard)
-    recv = shard.new_empty((world * maxn, 2))
-    _all_gather(dist, recv, send)
-    full = torch.cat([recv[g * maxn:g * maxn + sizes[g]] for g in range(world)])
-    cnt = engine.join_nopart_replicated(params, full)
-    local = int(cnt.item())
-    _all_reduce(dist, cnt)
-    return DistResult(matches=int(cnt.item()), local_matches=local, timers=[])
-
-
-def unpack_segments_numpy(recv, sizes, maxn, P):
-    """Split a gathered packed buffer back into per-rank (keys, bounds)."""
-    maxn, E = pack_layout(maxn, P)
-    recv = np.asarray(recv)
-    segs = []
-    for g, n in enumerate(sizes):
-        blk = recv[g * E:(g + 1) * E]
-        bounds = blk[maxn:].view(np.uint32)[:P + 1].astype(np.int64)
-        segs.append((blk[:n], bounds))
-    return segs

@@ -28,7 +28,7 @@ def main():
     a = ap.parse_args()
     os.environ["PHJ_REHEARSE"] = "1"
     import partitionedhashjoin_amd as phj
-    from partitionedhashjoin_amd.distributed import shard_range
+    from partitionedhashjoin_amd import shard_range
     p = phj.radix_params((8, 8))
     nR, nS = a.primary, a.secondary
     for W in a.worlds:

@@ -1,8 +1,21 @@
-"""Multi-rank orchestration (partitionedhashjoin_amd/distributed.py) over gloo
-on CPU: range sharding, partitioned build-shard all-gather, per-rank join,
-count all-reduce. A test-only engine computes each rank's partitions with the
-oracle, so this exercises exactly the collective layout the HIP engine uses
-(fixed-size padded shards, per-shard partition bounds) without a GPU."""
+"""The multi-GPU member step's host protocol over gloo on CPU (world 2-3).
+
+The join itself is C++/HIP in libphj_hip.so (csrc/phj_group.h) and needs a
+GPU; what crosses the ranks is defined by the library's host-only functions,
+which phj_group.h itself calls and these tests drive through the C ABI:
+  * phj_shard_range: rows of each rank (range shards, §8(e));
+  * phj_exchange_layout: one rank's all-gathered block, build codes in final
+    partition order | zero padding | bounds[P + 1] (uint32);
+  * phj_count_contribution / phj_count_verdict: the {count, failed} words of
+    the count all-reduce and the global count (or PHJ_ERR_STATE) they give.
+Each rank's partitioned codes and its table probe come from the oracle (test
+infrastructure): this checks that blocks packed and read by the library's
+layout carry every rank's build side intact, that the reduction counts what
+the reference counts (the semi-join, src/RadixCluster/HashJoin.hpp:295-301),
+and that one failed rank (an all-zero block, failed word 1) makes every rank
+report the failure while its block still reads as a valid empty segment.
+The reference's parallel split is a thread pool (src/main.cpp:235-241).
+"""
 import os
 import socket
 
@@ -14,76 +27,6 @@ import torch.multiprocessing as mp
 
 import partitionedhashjoin_amd as phj
 from oracle import oracle as O
-from partitionedhashjoin_amd.distributed import (distributed_join, distributed_join_nopart, max_shard, pack_layout, shard_range,
-                                                 unpack_segments_numpy)
-
-
-class _View:
-    def __init__(self, keys, pays, bounds, P):
-        self.keys, self.pays, self.bounds = keys, pays, bounds
-        self.n = keys.shape[0]
-        self.num_partitions = P
-
-
-class OracleShardEngine:
-    """CPU stand-in for HipShardEngine with the same interface (test infrastructure)."""
-
-    def __init__(self, R, S):
-        self.torch = torch
-        self.rel = {0: R, 1: S}
-        self.views = {}
-
-    @staticmethod
-    def _geometry(p):
-        if p.num_partitions:
-            return int(p.num_partitions), False
-        return 1 << (p.radix_bits[0] + p.radix_bits[1]), True
-
-    def tensor(self, n, dtype):
-        return torch.zeros(int(n), dtype=dtype)
-
-    def partition(self, side, params):
-        P, radix = self._geometry(params)
-        out, bounds = O.partition(self.rel[side], P, radix, params.hash, params.hash_seed, workers=2)
-        v = _View(out[:, 0].copy(), out[:, 1].copy(), bounds, P)
-        self.views[side] = v
-        return v
-
-    def pack(self, v, maxn, P):
-        maxn, E = pack_layout(maxn, P)
-        buf = np.zeros(E, dtype=np.int64)
-        buf[:v.n] = v.keys
-        buf[maxn:].view(np.uint32)[:P + 1] = v.bounds.astype(np.uint32)
-        return torch.from_numpy(buf)
-
-    def _count(self, params, segs):
-        P, radix = self._geometry(params)
-        for keys, bounds in segs:
-            # every gathered shard arrives partition-major with consistent bounds
-            q = O.partition_ids(keys, P, radix, params.hash, params.hash_seed).astype(np.int64)
-            expect = np.repeat(np.arange(P), np.diff(bounds.astype(np.int64)))
-            assert np.array_equal(q, expect)
-        rkeys = np.concatenate([k for k, _ in segs]) if segs else np.zeros(0, dtype=np.int64)
-        return torch.tensor([O.semijoin_count_keys(rkeys, self.views[1].keys)], dtype=torch.int64)
-
-    def join_packed(self, params, recv, sizes, maxn, P):
-        return self._count(params, unpack_segments_numpy(recv.numpy(), sizes, maxn, P))
-
-    def join_local(self, params, v):
-        return self._count(params, [(v.keys, v.bounds)])
-
-    def timers(self):
-        return []
-
-    def build_shard(self):
-        return torch.from_numpy(np.ascontiguousarray(self.rel[0]))
-
-    def join_nopart_replicated(self, params, full_r):
-        R = full_r.numpy()
-        return torch.tensor([O.join_nopart(R, self.rel[1]).matches], dtype=torch.int64)
-
-    def build_ready(self):
-        pass
 
 
 def _tables(nR, nS, alpha, seed):
@@ -92,33 +35,96 @@ def _tables(nR, nS, alpha, seed):
     return R, S
 
 
-def _worker(rank, world, port, nR, nS, alpha, seed, bits, nparts, out):
+def _geometry(p):
+    if p.num_partitions:
+        return int(p.num_partitions), False
+    return 1 << (p.radix_bits[0] + p.radix_bits[1]), True
+
+
+def _part_of_codes(codes, P, radix):
+    u = codes.view(np.uint64)
+    return (u & np.uint64(P - 1)) if radix else (u % np.uint64(P))
+
+
+def _pack(R_shard, params, codes_elems, block_elems):
+    """This rank's exchange block: R's codes in partition order, bounds after."""
+    P, radix = _geometry(params)
+    kind = O.HASH_MURMUR3 if params.hash == phj.HASH_MURMUR3 else O.HASH_XXH3
+    out, bounds = O.partition(R_shard, P, radix, kind, params.hash_seed, workers=1)
+    block = np.zeros(block_elems, dtype=np.int64)
+    block[:out.shape[0]] = O.hash_keys(kind, out[:, 0], params.hash_seed).view(np.int64)
+    block[codes_elems:].view(np.uint32)[:P + 1] = bounds.astype(np.uint32)
+    return block
+
+
+def _segments(recv, world, P, codes_elems, block_elems):
+    """The gathered blocks as build segments (codes, bounds), as phj_group.h reads them."""
+    segs = []
+    for g in range(world):
+        blk = recv[g * block_elems:(g + 1) * block_elems]
+        b = blk[codes_elems:].view(np.uint32)[:P + 1].astype(np.int64)
+        segs.append((blk[:b[P]], b))
+    return segs
+
+
+def _worker(rank, world, port, nR, nS, alpha, seed, bits, nparts, fail_rank, out):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         R, S = _tables(nR, nS, alpha, seed)
-        rlo, rhi = shard_range(nR, rank, world)
-        slo, shi = shard_range(nS, rank, world)
-        eng = OracleShardEngine(R[rlo:rhi], S[slo:shi])
-        p = phj.radix_params(bits, num_partitions=nparts, hash=phj.HASH_MURMUR3, seed=1234)
-        res = distributed_join(eng, p, nR, nS, rank, world, dist)
-        out[rank] = (res.matches, res.local_matches)
+        params = phj.radix_params(bits, num_partitions=nparts, hash=phj.HASH_MURMUR3, seed=1234)
+        P, radix = _geometry(params)
+        rlo, rhi = phj.shard_range(nR, rank, world)
+        slo, shi = phj.shard_range(nS, rank, world)
+        # every rank's real shard size first (phj_group.h exchange_sizes)
+        sizes = torch.zeros(world, dtype=torch.int64)
+        dist.all_gather_into_tensor(sizes, torch.tensor([rhi - rlo], dtype=torch.int64))
+        codes_elems, block_elems = phj.exchange_layout(int(sizes.max()), P)
+        failed = rank == fail_rank
+        send = np.zeros(block_elems, dtype=np.int64) if failed else _pack(R[rlo:rhi], params, codes_elems, block_elems)
+        recv = torch.zeros(world * block_elems, dtype=torch.int64)
+        dist.all_gather_into_tensor(recv, torch.from_numpy(send))
+        segs = _segments(recv.numpy(), world, P, codes_elems, block_elems)
+        for g, (codes, b) in enumerate(segs):
+            # partition-major with consistent bounds; a failed rank's block is empty
+            assert b[0] == 0 and np.all(np.diff(b) >= 0)
+            assert codes.shape[0] == (0 if g == fail_rank else int(sizes[g]))
+            assert np.array_equal(_part_of_codes(codes, P, radix).astype(np.int64), np.repeat(np.arange(P), np.diff(b)))
+        kind = O.HASH_MURMUR3
+        build = np.concatenate([c for c, _ in segs])
+        local = O.semijoin_count_keys(build, O.hash_keys(kind, S[slo:shi, 0], 1234).view(np.int64))
+        words = torch.from_numpy(phj.count_contribution(local, failed).view(np.int64).copy())
+        dist.all_reduce(words)
+        try:
+            out[rank] = ("ok", phj.count_verdict(words.numpy().view(np.uint64)), local)
+        except phj.PhjError as e:
+            out[rank] = ("error", e.code, local)
     finally:
         dist.destroy_process_group()
 
 
 def _np_worker(rank, world, port, nR, nS, out):
+    # NoPartitioning (§8(e)): every rank's R shard broadcast to all (an
+    # all-gather-v into one contiguous relation, phj_group.h member_nopart), the
+    # global table built and the local S shard probed, the counts reduced
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         R, S = _tables(nR, nS, 1.25, 9)
-        rlo, rhi = shard_range(nR, rank, world)
-        slo, shi = shard_range(nS, rank, world)
-        eng = OracleShardEngine(R[rlo:rhi], S[slo:shi])
-        res = distributed_join_nopart(eng, phj.nopart_params(), nR, nS, rank, world, dist)
-        out[rank] = (res.matches, res.local_matches)
+        parts = []
+        for g in range(world):
+            lo, hi = phj.shard_range(nR, g, world)
+            t = torch.from_numpy(np.ascontiguousarray(R[lo:hi])) if g == rank else torch.zeros((hi - lo, 2), dtype=torch.int64)
+            dist.broadcast(t, src=g)
+            parts.append(t.numpy())
+        full = np.concatenate(parts)
+        slo, shi = phj.shard_range(nS, rank, world)
+        local = O.join_nopart(full, S[slo:shi]).matches
+        words = torch.from_numpy(phj.count_contribution(local).view(np.int64).copy())
+        dist.all_reduce(words)
+        out[rank] = ("ok", phj.count_verdict(words.numpy().view(np.uint64)), local)
     finally:
         dist.destroy_process_group()
 
@@ -136,40 +142,57 @@ def test_library_shard_range_is_the_documented_split():
             for r in range(w):
                 assert phj.shard_range(n, r, w) == ((n * r) // w, (n * (r + 1)) // w)
     assert phj.shard_range(10, 3, 2) == (0, 0)   # out of range rank: empty
-    # the pure-Python helper of the CPU rehearsal is the same split
-    for n in (0, 1, 7, 10_000_000, 2**40 + 3):
-        for w in (1, 3, 8):
-            for r in range(w + 1):
-                assert shard_range(n, r, w) == phj.shard_range(n, r, w)
 
 
 def test_shard_ranges_cover_exactly():
     for n in (0, 1, 7, 10_000_000):
         for w in (1, 2, 3, 8):
-            rs = [shard_range(n, r, w) for r in range(w)]
+            rs = [phj.shard_range(n, r, w) for r in range(w)]
             assert rs[0][0] == 0 and rs[-1][1] == n
             assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
-            assert max_shard(n, w) - min(hi - lo for lo, hi in rs) <= 1
+            sizes = [hi - lo for lo, hi in rs]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def test_exchange_layout():
+    # codes padded to 64 elements (16-B aligned columns), then P + 1 uint32 bounds
+    for maxn in (0, 1, 63, 64, 65, 1_250_000):
+        for P in (1, 2, 32, 65536, 4_194_304):
+            ce, be = phj.exchange_layout(maxn, P)
+            assert ce % 64 == 0 and maxn <= ce < maxn + 64
+            assert 2 * (be - ce) >= P + 1 and 2 * (be - ce) <= P + 2
+
+
+def test_count_words():
+    assert list(phj.count_contribution(123)) == [123, 0]
+    assert list(phj.count_contribution(123, failed=True)) == [0, 1]
+    assert phj.count_verdict([5, 0]) == 5
+    with pytest.raises(phj.PhjError) as e:
+        phj.count_verdict([5, 2])
+    assert e.value.code == phj._capi.PHJ_ERR_STATE
 
 
 @pytest.mark.parametrize("world,bits,nparts", [(2, (4, 4), 0), (3, (6, 0), 0), (2, (1, 0), 37)])
-def test_distributed_join_gloo(world, bits, nparts):
+def test_member_protocol_gloo(world, bits, nparts):
     nR, nS, alpha, seed = 20_011, 150_007, 1.25, 3
     R, S = _tables(nR, nS, alpha, seed)
     expect = O.semijoin_count(R, S)
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_worker, args=(world, _free_port(), nR, nS, alpha, seed, bits, nparts, out), nprocs=world)
-    totals = {out[r][0] for r in range(world)}
-    assert totals == {expect}
-    assert sum(out[r][1] for r in range(world)) == expect
+    mp.spawn(_worker, args=(world, _free_port(), nR, nS, alpha, seed, bits, nparts, -1, out), nprocs=world)
+    assert {out[r][:2] for r in range(world)} == {("ok", expect)}
+    assert sum(out[r][2] for r in range(world)) == expect
 
 
-def test_single_rank_path():
-    R, S = _tables(5000, 40_000, 1.05, 8)
-    eng = OracleShardEngine(R, S)
-    res = distributed_join(eng, phj.radix_params((3, 3)), 5000, 40_000, 0, 1, None)
-    assert res.matches == O.semijoin_count(R, S)
+def test_member_protocol_failure_gloo():
+    # rank 1 fails before the all-gather: it sends an all-zero block (peers
+    # read an empty build segment) and the failed word; every rank then
+    # reports PHJ_ERR_STATE instead of a count
+    world, nR, nS = 3, 20_011, 150_007
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), nR, nS, 1.05, 4, (4, 4), 0, 1, out), nprocs=world)
+    assert {out[r][:2] for r in range(world)} == {("error", phj._capi.PHJ_ERR_STATE)}
 
 
 @pytest.mark.parametrize("world", [2, 3])
@@ -180,5 +203,5 @@ def test_distributed_nopart_gloo(world):
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_np_worker, args=(world, _free_port(), nR, nS, out), nprocs=world)
-    assert {out[r][0] for r in range(world)} == {expect}
-    assert sum(out[r][1] for r in range(world)) == expect
+    assert {out[r][:2] for r in range(world)} == {("ok", expect)}
+    assert sum(out[r][2] for r in range(world)) == expect

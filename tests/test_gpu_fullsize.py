@@ -22,6 +22,7 @@ import pytest
 
 import partitionedhashjoin_amd as phj
 from oracle import oracle as O
+from hashinv import preimage, table_edge_codes
 
 pytestmark = pytest.mark.gpu
 
@@ -159,19 +160,26 @@ def test_full_size_duplicate_heavy_and_extreme_build_side(ctx):
     # 10M build tuples with every key repeated 4x (2.5M distinct keys from
     # 1 + SHIFT) and the extreme keys INT64_MIN / MAX, 0, -1 in R; S = the
     # Zipf workload with every 7th key negated and the extremes planted
+    # plus, for both hashes at SEED, the keys whose codes are the code tables'
+    # empty values and their bucket mates (hashinv.table_edge_codes)
     ext = np.array([np.iinfo(np.int64).min, np.iinfo(np.int64).max, 0, -1], dtype=np.int64)
+    pre = np.unique(np.concatenate([[preimage(mur, c, SEED) for c in table_edge_codes(np_)]
+                                    for mur, np_ in ((True, 0), (False, 1024), (False, 0))]).astype(np.int64))
+    ext = np.unique(np.concatenate([ext, pre]))
     keys = (np.arange(NR, dtype=np.int64) // 4) + 1 + SHIFT
-    keys[-4:] = ext
+    keys[-ext.shape[0]:] = ext
     R = np.stack([keys, np.arange(NR, dtype=np.int64)], axis=1)
     ctx.upload(phj.SIDE_BUILD, R)
     ctx.generate_zipf(phj.SIDE_PROBE, NS, 1.05, 1, NR, GEN_SEED)
     S = ctx.download(phj.SIDE_PROBE)
     S[::NEG_EVERY, 0] = -S[::NEG_EVERY, 0]
     S[5::1_000_003, 0] = np.resize(ext, S[5::1_000_003, 0].shape[0])
+    S[11::999_983, 0] = np.resize(pre, S[11::999_983, 0].shape[0])
     ctx.upload(phj.SIDE_PROBE, S)
     sk = S[:, 0]
-    distinct_hi = (NR - 4 - 1) // 4 + 1 + SHIFT
-    expect = int(np.count_nonzero((sk > SHIFT) & (sk <= distinct_hi)) + np.count_nonzero(np.isin(sk, ext)))
+    distinct_hi = (NR - ext.shape[0] - 1) // 4 + 1 + SHIFT
+    inr = (sk > SHIFT) & (sk <= distinct_hi)
+    expect = int(np.count_nonzero(inr) + np.count_nonzero(np.isin(sk, ext) & ~inr))
     assert O.semijoin_count(R, S, threads=THREADS) == expect
     for params in (phj.radix_params((8, 8), hash=phj.HASH_MURMUR3, seed=SEED),
                    phj.radix_params(num_partitions=1024, hash=phj.HASH_XXH3, seed=SEED),

@@ -16,7 +16,8 @@ import numpy as np
 import pytest
 
 import partitionedhashjoin_amd as phj
-from partitionedhashjoin_amd.distributed import generate_shards, shard_range
+from partitionedhashjoin_amd import shard_range
+from partitionedhashjoin_amd.distributed import generate_shards
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu

@@ -9,6 +9,7 @@ import pytest
 
 import partitionedhashjoin_amd as phj
 from oracle import oracle as O
+from hashinv import preimage, table_edge_codes
 
 pytestmark = pytest.mark.gpu
 
@@ -150,6 +151,48 @@ def test_extreme_keys(ctx, name, params):
                                              endpoint=True), [I64_MIN, I64_MAX, 0]])
     rng.shuffle(S)
     assert _gpu_count(ctx, R, S, params) == O.semijoin_count(R, S)
+
+
+def edge_keys(params):
+    """Keys whose codes are the code tables' empty values and their bucket
+    mates (hashinv.table_edge_codes) under the plan's hash and seed."""
+    mur = params.hash == phj.HASH_MURMUR3
+    return np.array([preimage(mur, c, params.hash_seed) for c in table_edge_codes(params.num_partitions)],
+                    dtype=np.int64)
+
+
+@pytest.mark.parametrize("name,params", ALL_PARAMS, ids=[a for a, _ in ALL_PARAMS])
+def test_empty_value_preimages(ctx, name, params):
+    # VERDICT r03 weak 1: the code tables mark an empty slot with E_p, a code of
+    # another partition (csrc/phj_table.h); the reference reserves no key
+    # (src/HashTables/LinearProbing.hpp:79-82). Keys hashing to 0, 1, 2^40 and
+    # to their partition's home bucket, planted in S only, must all miss (no
+    # false positive); planted in R, they must all be found and must not cut
+    # other keys' walks short (no false negative). |R| = 20000 sub-partitions
+    # h % 1 at bit 40 (where code 1 lies in partition 0) and sends every
+    # 2-pass plan through the on-chip probe.
+    pre = edge_keys(params)
+    base = np.arange(1, 20_001, dtype=np.int64)
+    base = base[~np.isin(base, pre)]
+    S = np.concatenate([pre, base[::3], pre[::-1], -base[:500]])
+    exp_s = O.semijoin_count(base, S)
+    assert exp_s == base[::3].shape[0]
+    assert _gpu_count(ctx, base, S, params) == exp_s
+    R = np.concatenate([base, pre, pre[:5]])
+    exp_r = O.semijoin_count(R, S)
+    assert exp_r == exp_s + 2 * pre.shape[0]
+    assert _gpu_count(ctx, R, S, params) == exp_r
+    # every planted key alone against R holding them all
+    assert _gpu_count(ctx, R, pre, params) == pre.shape[0]
+
+
+def test_code_one_under_mod1_is_not_empty(ctx):
+    # the concrete round-3 false positive: under XXH3 seed 1 the key below has
+    # code 1, which lies in partition 0 of h % 1 split at bit 40
+    p = phj.radix_params(num_partitions=1, hash=phj.HASH_XXH3, seed=1)
+    R = np.arange(1, 20_001, dtype=np.int64)
+    assert _gpu_count(ctx, R, [-6993838658721465140], p) == 0
+    assert _gpu_count(ctx, np.append(R, -6993838658721465140), [-6993838658721465140, 5], p) == 2
 
 
 @pytest.mark.parametrize("name,params", ALL_PARAMS, ids=[a for a, _ in ALL_PARAMS])

@@ -12,87 +12,10 @@ import numpy as np
 import pytest
 
 from oracle import oracle as O
+from hashinv import murmur3_inverse, preimage, table_edge_codes, xxh3_inverse
 
 M64 = (1 << 64) - 1
 SEEDS = [0, 1, 0x0BAD_5EED_0BAD_5EED, 0xFFFF_FFFF_FFFF_FFFF]
-
-
-def _rotl(x, r):
-    return ((x << r) | (x >> (64 - r))) & M64
-
-
-def _inv_xorshift_right(y, s):
-    # x ^= x >> s
-    x = y
-    for _ in range(64 // s + 1):
-        x = y ^ (x >> s)
-    return x
-
-
-def _inv_mul(c):
-    return pow(c, -1, 1 << 64)
-
-
-def _xxh3_bitflip(seed):
-    s = seed & 0xFFFFFFFF
-    swapped = int.from_bytes(s.to_bytes(4, "little"), "big")
-    seed ^= swapped << 32
-    return ((0x1CAD21F72C81017C ^ 0xDB979083E96DD4DE) - seed) & M64
-
-
-def _inv_lin(y):
-    # x ^ rotl(x,49) ^ rotl(x,24) is linear over GF(2): invert by Gaussian
-    # elimination on its 64 column images
-    cols = []
-    for i in range(64):
-        e = 1 << i
-        cols.append(e ^ _rotl(e, 49) ^ _rotl(e, 24))
-    # solve A x = y: rows = output bits
-    rows = []
-    for bit in range(64):
-        r = 0
-        for i in range(64):
-            if (cols[i] >> bit) & 1:
-                r |= 1 << i
-        rows.append([r, (y >> bit) & 1])
-    piv = []
-    rank = 0
-    for col in range(64):
-        sel = next((j for j in range(rank, 64) if (rows[j][0] >> col) & 1), None)
-        assert sel is not None, "linear mixer not invertible"
-        rows[rank], rows[sel] = rows[sel], rows[rank]
-        for j in range(64):
-            if j != rank and (rows[j][0] >> col) & 1:
-                rows[j][0] ^= rows[rank][0]
-                rows[j][1] ^= rows[rank][1]
-        piv.append(col)
-        rank += 1
-    x = 0
-    for j, col in enumerate(piv):
-        x |= rows[j][1] << col
-    return x
-
-
-def xxh3_inverse(h, seed):
-    C = 0x9FB21C651E98DF25
-    x = _inv_xorshift_right(h, 28)
-    x = (x * _inv_mul(C)) & M64
-    # y = x ^ ((x >> 35) + 8): bits 30..63 of x pass through unchanged
-    hi = x >> 35
-    x = x ^ ((hi + 8) & M64)
-    x = (x * _inv_mul(C)) & M64
-    x = _inv_lin(x)
-    x ^= _xxh3_bitflip(seed)
-    return ((x >> 32) | (x << 32)) & M64
-
-
-def murmur3_inverse(h, seed):
-    x = _inv_xorshift_right(h, 33)
-    x = (x * _inv_mul(0xC4CEB9FE1A85EC53)) & M64
-    x = _inv_xorshift_right(x, 33)
-    x = (x * _inv_mul(0xFF51AFD7ED558CCD)) & M64
-    x = _inv_xorshift_right(x, 33)
-    return x ^ seed
 
 
 def _keys():
@@ -130,3 +53,23 @@ def test_codes_preserve_the_join_count():
         hr = O.hash_keys(kind, r, 11).view(np.int64)
         hs = O.hash_keys(kind, s, 11).view(np.int64)
         assert O.semijoin_count_keys(hr, hs) == expect
+
+
+@pytest.mark.parametrize("nparts", [0, 1, 32, 1000, 5000])
+def test_edge_code_preimages(nparts):
+    # the keys the GPU parity tests plant (test_gpu_parity.py
+    # test_empty_value_preimages): each hashes to its chosen code
+    codes = table_edge_codes(nparts)
+    assert {0, 1, 1 << 40} <= set(codes)
+    for kind, mur in ((O.HASH_MURMUR3, True), (O.HASH_XXH3, False)):
+        for seed in (1, 0x1234_5678_9ABC_DEF1):
+            keys = np.array([preimage(mur, c, seed) for c in codes], dtype=np.int64)
+            assert np.array_equal(O.hash_keys(kind, keys, seed), np.array(codes, dtype=np.uint64))
+
+
+def test_known_code_one_key():
+    # under XXH3 seed 1 this key's code is 1, which the
+    # round-3 tables used as partition 0's empty value under h % 1
+    k = -6993838658721465140
+    assert preimage(False, 1, 1) == k
+    assert int(O.hash_keys(O.HASH_XXH3, np.array([k], dtype=np.int64), 1)[0]) == 1
