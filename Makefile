@@ -14,7 +14,7 @@ CXXFLAGS := -std=c++17 -O2 -Wall -Wextra -pthread -ffp-contract=off
 LIB := $(PKG)/libphj_hip.so
 CLI := $(PKG)/phjoin
 HIP_SRC := $(PKG)/csrc/phj_capi.hip
-HIP_HDR := $(PKG)/csrc/phj_table.h $(PKG)/csrc/phj_pow.h $(PKG)/csrc/phj_pow_tables.h $(PKG)/csrc/phj_group.h $(PKG)/csrc/phj_partition.h $(PKG)/csrc/phj_partition_wc.h $(PKG)/csrc/phj_join.h $(PKG)/csrc/phj_mat.h $(PKG)/csrc/phj_hash.h include/phj.h
+HIP_HDR := $(PKG)/csrc/phj_table.h $(PKG)/csrc/phj_pow.h $(PKG)/csrc/phj_pow_tables.h $(PKG)/csrc/phj_group.h $(PKG)/csrc/phj_partition.h $(PKG)/csrc/phj_join.h $(PKG)/csrc/phj_mat.h $(PKG)/csrc/phj_hash.h include/phj.h
 HOST_SRC := $(wildcard $(PKG)/host/*.cpp $(PKG)/host/*/*.cpp)
 HOST_HDR := $(wildcard $(PKG)/host/*.hpp $(PKG)/host/*/*.hpp) $(PKG)/csrc/phj_hash.h
 

@@ -23,7 +23,6 @@
 #include "phj_join.h"
 #include "phj_mat.h"
 #include "phj_partition.h"
-#include "phj_partition_wc.h"
 #include "phj_table.h"
 
 using namespace phj;
@@ -32,6 +31,7 @@ namespace {
 
 constexpr double kNPDefaultRatio = 2.0;             // slots per build tuple
 constexpr uint32_t kNPRegionBuckets = 1024;           // NoPartitioning region build: buckets per region (LDS 60 B each)
+constexpr int kOnePassMax = 256;                      // hash % P: largest P partitioned in one pass
 
 struct DevBuf {
     void* p = nullptr;
@@ -42,44 +42,19 @@ struct DevBuf {
 // values; PHJ_TILE_ITEMS / PHJ_P1_AOS / PHJ_XCD_REMAP override them for sweeps.
 struct Tuning {
     int tile = 4096;      // tile kernels: tuples per tile (2048, 4096 or 8192)
-    bool p1_aos = true;   // tile kernels, 2-pass: pass-1 output as 16-B tuples (16-B stores)
-    bool xcd_remap = true;
-    bool wc = false;      // write-combining super-tile kernels (slower on MI355X: DESIGN.md)
-    int wc_items = 8;     // WC sub-tile = 256 * wc_items tuples (4 or 8)
-    int wc_lw = 8;        // WC line: elements per column (8 = 64 B, 16 = 128 B)
-    int wc_wgs = 1024;    // target workgroups per WC pass (super-tile size follows)
-    bool r_aux = true;    // phj_join: partition R on the aux stream beside S
-    int probe_items = 8;  // block probe: S keys per lane per work item (8 or 16)
-    int probe_wave = 1;   // wave-per-item probe: 0 never, 1 small partitions (auto), 2 always
     int block = 512;      // threads per workgroup of the tile kernels (256, 512 or 1024; tile_shape)
-    bool nt_store = false; // nontemporal scatter stores
-    int nt_load = 1;       // nontemporal tuple loads in the partition passes: 1 pass 1, 2 both
-    bool dcol = true;     // 2-pass: pass 1 writes the pass-2 digit column
+    int nt_load = 1;      // nontemporal tuple loads in the partition passes: 1 pass 1, 2 both
     bool fused = true;    // radix join: fused per-partition LDS build + probe when partitions are small
-    int onepass_max = 256; // hash % P: largest P partitioned in one pass
     int ptab = 1;         // partitioned bucket tables: 0 never, 1 very large partitions, 2 always
     bool subpart = true;  // phj_join: sub-partition large partitions for the fused join
     bool timers = true;   // per-kernel timer events (phase events are always recorded)
-    int fused_kpl = 4;    // fused join: S keys per lane per probe round (2, 4 or 8)
     bool p1_chunk = true; // 2-pass, unordered partitions: chunked pass 1 without a histogram pass
     int p1_slots = 0;     // chunked pass 1: workgroups per shard (0 = fill the chip once, -1 = one per tile)
     int p1_wpc2 = 2;      // ... keys-only: workgroups per CU x 2 (0 = fill the chip once)
     int p1_tps = static_cast<int>(kTilesPerShard);   // chunked pass 1: tiles per shard (sets the shard count)
     int p1_min_tiles = 32768;  // chunked pass 1: smallest relation (in 4096-tuple tiles, ~134M tuples)
-    int p1_ko_tps = 1024;      // ... the keys-only form for the counting probe: tiles per shard
-    int p1_ko_min_tiles = 0;   // ... and its smallest relation (measured: wins at 25M-200M)
-    int np_nt = 1;        // NoPartitioning probe: 1 nontemporal S loads, 2 also the bucket loads
-    int np_items = 4;     // NoPartitioning probe: S keys per thread per round (4 or 8)
-    bool np_region = true;   // NoPartitioning build: partition R into table regions, build each in LDS
-    int np_hot = 1;          // NoPartitioning probe: hot-key LDS cache (0 off, 1 from np_hot_min probes)
-    int np_ct = 1;           // NoPartitioning count: region code tables (k_np_probe_ct) instead of 64-B buckets
-    uint64_t np_hot_min = 1u << 20;
-    uint32_t np_hot_samples = 65536;
-    int p2probe = 1;         // radix join, 2 passes: the probe side's pass 2 on-chip (k_probe_ht)
-    int p1_ko = 1;           // chunked pass 1 consumed by the on-chip probe: keys only (k_scatter_chunked VAR 5)
-    int p1_hcode = 1;        // ... written as hash codes, so the probe never hashes (VAR 13)
-    double np_ratio = kNPDefaultRatio;   // NoPartitioning: slots per build tuple when the params leave it 0
-    int p1_var = 3;          // chunked pass 1 variant (k_scatter_chunked VAR: 1 atomic rank, 2 tuple LDS)
+    int p1_ko_tps = 1024;      // ... the keys-only form for the on-chip probe: tiles per shard (at every size)
+    int p2probe = 1;      // radix join, 2 passes: the probe side's pass 2 on-chip (k_probe_ht)
 };
 
 int env_int(const char* name, int dflt) {
@@ -121,6 +96,7 @@ struct SideState {
     DevBuf hist1, hist2, bounds1, tbase2, tseg2, bounds, partials;
     DevBuf dig;           // pass-2 digit column written by pass 1
     DevBuf ccur, ctab, tstart;   // chunked pass 1: digit cursors + pool counter, chunk table, pass-2 tile starts
+    DevBuf csink;                // ... code form: the void claims' / stores' sink words (never read)
     uint32_t gen = 0;            // chunked pass 1: tag of the current chunk-table entries
     bool hcoded = false;         // the last pass 1 wrote hash codes (keys only, PHJ_P1_HCODE)
     phj_partitioned view{};
@@ -162,7 +138,6 @@ struct phj_ctx {
     DevBuf r_codes, r_bounds;         // ... the build side's codes in partition order and bounds (single device)
     DevBuf np_tab, np_pays;
     DevBuf np_ovf, np_ovfb, np_ovfn;   // region build: overflow tuples, their start buckets, count
-    DevBuf np_hot, np_img;             // hot-key cache: sampled keys + count, LDS image (keys, states)
     DevBuf np_uni;                     // code-table NoPartitioning: {uniform?, cap} (k_np_ct_plan)
     DevBuf fitems, split;
     DevBuf mat_mark, mat_cnt, mat_rows;   // materialised join: per-probe match, block offsets, rows
@@ -360,7 +335,7 @@ int make_plan(phj_ctx* c, const phj_join_params* p, Plan& pl) {
         // one pass while the scatter's runs stay long (a 4096-tuple tile over
         // <= 256 digits); beyond, two passes with balanced digits: pass 1 on
         // q >> b2, pass 2 on q & (2^b2 - 1), 2^b2 ~ sqrt(P)
-        if (pl.P <= static_cast<uint64_t>(std::min<int>(c->tune.onepass_max, kMaxBins))) {
+        if (pl.P <= static_cast<uint64_t>(kOnePassMax)) {
             pl.npass = 1;
             pl.nb1 = static_cast<uint32_t>(pl.P);
             pl.bits1 = ceil_log2(pl.P);
@@ -505,22 +480,16 @@ int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const st
             // (two per CU at 81 KB of LDS), never more than the shard's tiles
             const uint32_t ntiles = static_cast<uint32_t>((n + T - 1) / T);
             const uint32_t per = (ntiles + a.nshards - 1) / a.nshards;
-            const size_t lds = a.keys_only ? sc_lds - static_cast<size_t>(T) * 8 : sc_lds;   // no payload rows
+            const size_t lds = a.keys_only ? chunk_codes_lds_bytes(T, a.nbins) : sc_lds;
             const void* kfn = nullptr;
-            switch (a.keys_only ? (c->tune.p1_hcode ? 13 : 5) : (c->tune.p1_var & 3)) {
-#define PHJ_P1_VARIANT(V)                                                                            \
-    case V:                                                                                          \
-        kfn = hk == kMurmur3 ? reinterpret_cast<const void*>(&k_scatter_chunked<BLOCK, ITEMS, kMurmur3, V>) \
-                             : reinterpret_cast<const void*>(&k_scatter_chunked<BLOCK, ITEMS, kXXH3, V>);    \
-        break;
-                PHJ_P1_VARIANT(0)
-                PHJ_P1_VARIANT(1)
-                PHJ_P1_VARIANT(2)
-                PHJ_P1_VARIANT(3)
-                PHJ_P1_VARIANT(5)
-                PHJ_P1_VARIANT(13)
-#undef PHJ_P1_VARIANT
-            }
+            // keys only, written as hash codes (the on-chip probe): k_chunk_codes;
+            // whole tuples: VAR 3, LDS-atomic ranking, 16-B LDS entries (phj_partition.h)
+            if (a.keys_only)
+                kfn = hk == kMurmur3 ? reinterpret_cast<const void*>(&k_chunk_codes<BLOCK, ITEMS, kMurmur3>)
+                                     : reinterpret_cast<const void*>(&k_chunk_codes<BLOCK, ITEMS, kXXH3>);
+            else
+                kfn = hk == kMurmur3 ? reinterpret_cast<const void*>(&k_scatter_chunked<BLOCK, ITEMS, kMurmur3, 3>)
+                                     : reinterpret_cast<const void*>(&k_scatter_chunked<BLOCK, ITEMS, kXXH3, 3>);
             // workgroups per CU: what the LDS and the kernel's registers allow
             // (cached per kernel and LDS size; one cache per worker thread)
             thread_local std::unordered_map<const void*, std::pair<size_t, int>> occ_cache;
@@ -562,7 +531,7 @@ int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const st
         // wave per tile: 4 tiles per workgroup
         PassArgs ac = a;
         uint32_t cgrid = (grid + 3) / 4;
-        if (ac.xcd_remap) cgrid = (cgrid + 7) & ~7u;
+        cgrid = (cgrid + 7) & ~7u;
         const size_t clds = 4ull * a.nbins * 4;
         if (a.dig_wide)
             hipLaunchKernelGGL((k_hist_col<T, uint16_t>), dim3(cgrid), dim3(256), clds, c->ks, ac);
@@ -607,11 +576,8 @@ int launch_pass(phj_ctx* c, int hk, bool in_aos, bool out_aos, PassArgs a, uint3
                 const std::string& prefix, uint64_t n, uint32_t hist_len) {
     if (ntiles == 0) return PHJ_OK;
     uint32_t grid = ntiles;
-    a.xcd_remap = 0;
-    if (c->tune.xcd_remap) {
-        grid = (ntiles + 7) & ~7u;
-        a.xcd_remap = 1;
-    }
+    grid = (ntiles + 7) & ~7u;
+    a.xcd_remap = 1;
     const TileShape sh = tile_shape(c, a.nbins);
     const int io = (in_aos ? 2 : 0) + (out_aos ? 1 : 0);
 #define PHJ_PASS_CASES(B, I)                                                        \
@@ -621,7 +587,7 @@ int launch_pass(phj_ctx* c, int hk, bool in_aos, bool out_aos, PassArgs a, uint3
         case 3: return launch_pass_t<B, I, true, true>(c, hk, a, grid, prefix, n, hist_len);   \
         default: return set_err(c, PHJ_ERR_INVALID, "unsupported pass layout");     \
     }
-    a.nt_store = c->tune.nt_store ? 1u : 0u;
+    a.nt_store = 0;
     // nontemporal tuple loads: 1 = the chunked pass 1 only (the relation is read
     // once there; the stable pass 1 re-reads it after its histogram, and at
     // 25-100M tuples that re-read is measured 0.01-0.02 ms slower with them),
@@ -637,81 +603,19 @@ int launch_pass(phj_ctx* c, int hk, bool in_aos, bool out_aos, PassArgs a, uint3
 #undef PHJ_PASS_CASES
 }
 
-template <int ITEMS, bool IN_AOS, int LW>
-int launch_pass_wc_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, uint32_t tsz,
-                     const std::string& prefix, uint64_t n, uint32_t hist_len) {
-    const size_t hist_lds = static_cast<size_t>(kWaves) * a.nbins * 4;
-    const size_t sc_lds = scatter_wc_lds_bytes(kBlock * ITEMS, LW);
-    const std::string hname = prefix + ".hist", cname = prefix + ".scan", sname = prefix + ".scatter";
-    PHJ_TRY(timer_begin(c, hname.c_str(), n * (IN_AOS ? 16 : 8)));
-    if (hk == kMurmur3)
-        hipLaunchKernelGGL((k_hist_super<ITEMS, IN_AOS, kMurmur3>), dim3(grid), dim3(kBlock), hist_lds, c->ks, a, tsz);
-    else
-        hipLaunchKernelGGL((k_hist_super<ITEMS, IN_AOS, kXXH3>), dim3(grid), dim3(kBlock), hist_lds, c->ks, a, tsz);
-    PHJ_LAUNCHED(c, hname);
-    PHJ_TRY(timer_end(c));
-    PHJ_TRY(timer_begin(c, cname.c_str(), static_cast<uint64_t>(hist_len) * 12));
-    PHJ_TRY(scan_u32(c, a.hist, hist_len, 1, hist_len, c->scan_scratch));
-    PHJ_TRY(timer_end(c));
-    PHJ_TRY(timer_begin(c, sname.c_str(), n * 32 + (a.out_dig ? n * (a.dig_wide ? 2 : 1) : 0)));
-    if (hk == kMurmur3)
-        hipLaunchKernelGGL((k_scatter_wc<ITEMS, IN_AOS, kMurmur3, LW>), dim3(grid), dim3(kBlock), sc_lds, c->ks, a, tsz);
-    else
-        hipLaunchKernelGGL((k_scatter_wc<ITEMS, IN_AOS, kXXH3, LW>), dim3(grid), dim3(kBlock), sc_lds, c->ks, a, tsz);
-    PHJ_LAUNCHED(c, sname);
-    PHJ_TRY(timer_end(c));
-    return PHJ_OK;
-}
-
-int launch_pass_wc(phj_ctx* c, int hk, bool in_aos, PassArgs a, uint32_t ntiles, uint32_t tsz,
-                   const std::string& prefix, uint64_t n, uint32_t hist_len) {
-    if (ntiles == 0) return PHJ_OK;
-    uint32_t grid = ntiles;
-    a.xcd_remap = 0;
-    if (c->tune.xcd_remap) {
-        grid = (ntiles + 7) & ~7u;
-        a.xcd_remap = 1;
-    }
-    const int key = (c->tune.wc_lw == 16 ? 2 : 0) + (in_aos ? 1 : 0);
-    if (c->tune.wc_items == 4) {
-        switch (key) {
-            case 0: return launch_pass_wc_t<4, false, 8>(c, hk, a, grid, tsz, prefix, n, hist_len);
-            case 1: return launch_pass_wc_t<4, true, 8>(c, hk, a, grid, tsz, prefix, n, hist_len);
-            case 2: return launch_pass_wc_t<4, false, 16>(c, hk, a, grid, tsz, prefix, n, hist_len);
-            default: return launch_pass_wc_t<4, true, 16>(c, hk, a, grid, tsz, prefix, n, hist_len);
-        }
-    }
-    switch (key) {
-        case 0: return launch_pass_wc_t<8, false, 8>(c, hk, a, grid, tsz, prefix, n, hist_len);
-        case 1: return launch_pass_wc_t<8, true, 8>(c, hk, a, grid, tsz, prefix, n, hist_len);
-        default: return set_err(c, PHJ_ERR_INVALID, "unsupported WC shape");
-    }
-}
-
-// Tuples per (super-)tile of a pass over n tuples with nb digits.
-uint32_t pass_tile(const phj_ctx* c, uint32_t n, uint32_t nb, bool* wc) {
-    *wc = c->tune.wc && nb <= static_cast<uint32_t>(kWcMaxBins);
-    if (!*wc) return tile_shape(c, nb).tile;
-    const uint32_t sub = kBlock * static_cast<uint32_t>(c->tune.wc_items);
-    const uint64_t subs = (static_cast<uint64_t>(n) + sub - 1) / sub;
-    const uint64_t k = std::min<uint64_t>(64, std::max<uint64_t>(1, (subs + c->tune.wc_wgs - 1) / c->tune.wc_wgs));
-    return static_cast<uint32_t>(sub * k);
-}
-
 int partition_state(phj_ctx* c, SideState& S, const char* tag, const Plan& pl, bool p1_only) {
     c->scan_scratch = &S.partials;
     if (!S.rel && S.n > 0) return set_err(c, PHJ_ERR_STATE, "relation not bound");
     const uint64_t n64 = S.n;
     if (n64 >= (1ull << 32) - 2 * 4096) return set_err(c, PHJ_ERR_RANGE, "relation above 2^32 tuples per device");
     const uint32_t n = static_cast<uint32_t>(n64);
-    bool wc1 = false, wc2 = false;
-    const uint32_t tile = pass_tile(c, n, pl.nb1, &wc1);
-    const uint32_t tile2 = pl.npass == 2 ? pass_tile(c, n, pl.nb2, &wc2) : 0;
+    const uint32_t tile = tile_shape(c, pl.nb1).tile;
+    const uint32_t tile2 = pl.npass == 2 ? tile_shape(c, pl.nb2).tile : 0;
     const uint32_t nt1 = (n + tile - 1) / tile;
-    const bool p1_aos = pl.npass == 2 && c->tune.p1_aos && !wc1;
+    const bool p1_aos = pl.npass == 2;
     // pass 1 leaves the pass-2 digit in a column (tile kernels only)
     // (p1_only: the probe re-hashes the keys itself, nothing reads the column)
-    const bool dcol = pl.npass == 2 && c->tune.dcol && !wc1 && !wc2 && !p1_only;
+    const bool dcol = pl.npass == 2 && !p1_only;
     const uint32_t dbytes = pl.bits2 > 8 ? 2 : 1;
     // Chunked pass 1 (unordered partitions, tile kernels): pass-1 chunks are
     // the pass-2 tiles, every digit's run of a tile fits one workgroup thread
@@ -722,13 +626,13 @@ int partition_state(phj_ctx* c, SideState& S, const char* tag, const Plan& pl, b
     // histogram read saves; so it starts at p1_min_tiles tiles. The keys-only
     // form for the on-chip probe (half the bytes, three workgroups per CU)
     // wins at every size measured (25M-200M), with shards of p1_ko_tps tiles.
-    const bool ko = p1_only && c->tune.p1_ko;
+    const bool ko = p1_only;
     const bool chunked = pl.npass == 2 && !pl.stable && c->tune.p1_chunk && (dcol || p1_only) && p1_aos && n > 0 &&
-                         nt1 >= static_cast<uint32_t>(ko ? c->tune.p1_ko_min_tiles : c->tune.p1_min_tiles) &&
+                         (ko || nt1 >= static_cast<uint32_t>(c->tune.p1_min_tiles)) &&
                          tile == tile2 && pl.nb1 <= static_cast<uint32_t>(tile_shape(c, pl.nb1).block) &&
                          tile / tile_shape(c, pl.nb1).block <= 8 &&   // registers: the next tile is prefetched
                          (3 * (static_cast<uint64_t>(n) / tile + kShards) + kShards * pl.nb1) * tile < (1ull << 32);
-    S.hcoded = chunked && ko && c->tune.p1_hcode;   // k_scatter_chunked VAR 13
+    S.hcoded = chunked && ko;   // k_chunk_codes
     // chains per digit: ~kTilesPerShard tiles each, a power of two <= kShards
     uint32_t nshards = 1;
     const uint32_t tps = static_cast<uint32_t>(ko ? c->tune.p1_ko_tps : c->tune.p1_tps);
@@ -760,6 +664,7 @@ int partition_state(phj_ctx* c, SideState& S, const char* tag, const Plan& pl, b
     }
     if (chunked) {
         PHJ_TRY(ensure(c, S.ccur, chunk_state_bytes(pl.nb1)));
+        if (ko) PHJ_TRY(ensure(c, S.csink, static_cast<size_t>(kSinkGroups) * tile_shape(c, pl.nb1).block * 8));
         PHJ_TRY(ensure(c, S.tstart, static_cast<size_t>(nt2max) * 8));   // tile_start, tile_cnt
         // entries are tagged with the pass's generation: a fresh (zeroed, tag 0)
         // table is never mistaken for a published chunk
@@ -798,6 +703,7 @@ int partition_state(phj_ctx* c, SideState& S, const char* tag, const Plan& pl, b
         // the counting probe consumes pass 1 on chip and reads only keys
         a.keys_only = ko ? 1u : 0u;
         a.chunk_cursor = static_cast<uint32_t*>(S.ccur.p);
+        a.sink = static_cast<unsigned long long*>(S.csink.p);
         a.chunk_tab = static_cast<unsigned long long*>(S.ctab.p);
         a.maxch = maxch;
         a.pool_stride = pool_stride;
@@ -809,11 +715,7 @@ int partition_state(phj_ctx* c, SideState& S, const char* tag, const Plan& pl, b
         a.gen = S.gen;
     }
     uint32_t* tb2 = pl.npass == 2 ? static_cast<uint32_t*>(S.tbase2.p) : nullptr;
-    if (wc1) {
-        PHJ_TRY(launch_pass_wc(c, pl.hk, true, a, nt1, tile, std::string(tag) + ".p1", n, nt1 * pl.nb1));
-    } else {
-        PHJ_TRY(launch_pass(c, pl.hk, true, p1_aos, a, nt1, std::string(tag) + ".p1", n, nt1 * pl.nb1));
-    }
+    PHJ_TRY(launch_pass(c, pl.hk, true, p1_aos, a, nt1, std::string(tag) + ".p1", n, nt1 * pl.nb1));
     if (chunked) {
         hipLaunchKernelGGL(k_pass1_finish_sizes, dim3(1), dim3(kFinBlock), 0, c->ks, a.chunk_cursor, pl.nb1, nshards, n, tile2,
                            static_cast<uint32_t*>(S.bounds1.p), tb2);
@@ -874,10 +776,7 @@ int partition_state(phj_ctx* c, SideState& S, const char* tag, const Plan& pl, b
             S.plan = pl;
             return PHJ_OK;
         }
-        if (wc2)
-            PHJ_TRY(launch_pass_wc(c, pl.hk, false, b, grid2, tile2, std::string(tag) + ".p2", n, grid2 * pl.nb2));
-        else
-            PHJ_TRY(launch_pass(c, pl.hk, p1_aos, false, b, grid2, std::string(tag) + ".p2", n, grid2 * pl.nb2));
+        PHJ_TRY(launch_pass(c, pl.hk, p1_aos, false, b, grid2, std::string(tag) + ".p2", n, grid2 * pl.nb2));
         const uint32_t nbnd = pl.Ppad + 1;
         hipLaunchKernelGGL(k_pass2_bounds, dim3((nbnd + kBlock - 1) / kBlock), dim3(kBlock), 0, c->ks,
                            b.hist, tb2, b.seg_bounds, pl.nb1, pl.nb2, n, static_cast<uint32_t*>(S.bounds.p));
@@ -950,16 +849,8 @@ int build_and_probe(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned*
         fa.count = static_cast<unsigned long long*>(c->count.p);
         fa.cycles = static_cast<unsigned long long*>(c->split.p);
         fa.seed = pl.seed;
-        const void* kfn;
-        if (c->tune.fused_kpl == 2)
-            kfn = pl.hk == kMurmur3 ? reinterpret_cast<const void*>(&k_join_fused<kMurmur3, 2, kFusedTcap>)
-                                    : reinterpret_cast<const void*>(&k_join_fused<kXXH3, 2, kFusedTcap>);
-        else if (c->tune.fused_kpl == 8)
-            kfn = pl.hk == kMurmur3 ? reinterpret_cast<const void*>(&k_join_fused<kMurmur3, 8, kFusedTcap>)
-                                    : reinterpret_cast<const void*>(&k_join_fused<kXXH3, 8, kFusedTcap>);
-        else
-            kfn = pl.hk == kMurmur3 ? reinterpret_cast<const void*>(&k_join_fused<kMurmur3, kFusedKPL, kFusedTcap>)
-                                    : reinterpret_cast<const void*>(&k_join_fused<kXXH3, kFusedKPL, kFusedTcap>);
+        const void* kfn = pl.hk == kMurmur3 ? reinterpret_cast<const void*>(&k_join_fused<kMurmur3, kFusedKPL, kFusedTcap>)
+                                            : reinterpret_cast<const void*>(&k_join_fused<kXXH3, kFusedKPL, kFusedTcap>);
         int per_cu = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, kBlock, 0) != hipSuccess || per_cu < 1)
             per_cu = 2;
@@ -1051,9 +942,8 @@ int build_and_probe(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned*
     // (measured on C2: the wave schedule wins at <= ~800 S keys per partition,
     // i.e. the multi-GPU shards; the workgroup schedule at 3000)
     const uint64_t expect_s = (nS + P - 1) / P;
-    const bool wave_probe = c->tune.probe_wave && expect_m * 2 <= kProbeWaveTcap &&
-                            (c->tune.probe_wave > 1 || expect_s <= 1024);
-    const uint32_t kChunk = wave_probe ? 64u * kProbeWaveKPL : kBlock * static_cast<uint32_t>(c->tune.probe_items);
+    const bool wave_probe = expect_m * 2 <= kProbeWaveTcap && expect_s <= 1024;
+    const uint32_t kChunk = wave_probe ? 64u * kProbeWaveKPL : kBlock * 8u;
     const size_t item_bound = P + (nS + kChunk - 1) / kChunk;
     PHJ_TRY(ensure(c, c->items, item_bound * sizeof(ProbeItem)));
     PHJ_TRY(ensure(c, c->count, 16));
@@ -1126,13 +1016,8 @@ int build_and_probe(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned*
     const bool small = expect * 2 <= 512;
     const void* kfn = nullptr;
 #define PHJ_PROBE_PICK(HK_, IT_, KPT_) kfn = reinterpret_cast<const void*>(&k_probe<HK_, IT_, KPT_>)
-    if (c->tune.probe_items == 8) {
-        if (pl.hk == kMurmur3) { if (small) PHJ_PROBE_PICK(kMurmur3, 8, 2); else PHJ_PROBE_PICK(kMurmur3, 8, 8); }
-        else { if (small) PHJ_PROBE_PICK(kXXH3, 8, 2); else PHJ_PROBE_PICK(kXXH3, 8, 8); }
-    } else {
-        if (pl.hk == kMurmur3) { if (small) PHJ_PROBE_PICK(kMurmur3, 16, 2); else PHJ_PROBE_PICK(kMurmur3, 16, 8); }
-        else { if (small) PHJ_PROBE_PICK(kXXH3, 16, 2); else PHJ_PROBE_PICK(kXXH3, 16, 8); }
-    }
+    if (pl.hk == kMurmur3) { if (small) PHJ_PROBE_PICK(kMurmur3, 8, 2); else PHJ_PROBE_PICK(kMurmur3, 8, 8); }
+    else { if (small) PHJ_PROBE_PICK(kXXH3, 8, 2); else PHJ_PROBE_PICK(kXXH3, 8, 8); }
 #undef PHJ_PROBE_PICK
     if (wave_probe) {
         if (pl.hk == kMurmur3) kfn = reinterpret_cast<const void*>(&k_probe_wave<kMurmur3, kProbeWaveKPL, kProbeWaveTcap>);
@@ -1184,8 +1069,8 @@ int partition_build(phj_ctx* c, const Plan& pl, int64_t* out, uint32_t* bounds) 
     a.nbins = nb;
     a.nbits = pl.bits1;
     a.f = digit_fn(pl, 1);
-    a.xcd_remap = c->tune.xcd_remap ? 1u : 0u;
-    const uint32_t grid = a.xcd_remap ? (nt + 7) & ~7u : nt;
+    a.xcd_remap = 1;
+    const uint32_t grid = (nt + 7) & ~7u;
     const size_t hlds = static_cast<size_t>(BLOCK / 64) * nb * 4;
     PHJ_TRY(timer_begin(c, "R.p1.hist", static_cast<uint64_t>(n) * 16));
     if (pl.hk == kMurmur3) hipLaunchKernelGGL((k_hist<BLOCK, ITEMS, true, kMurmur3>), dim3(grid), dim3(BLOCK), hlds, c->ks, a);
@@ -1258,9 +1143,9 @@ int build_ht(phj_ctx* c, const Plan& pl, int nseg, const int64_t* const* codes, 
 // phj_join takes the on-chip path for a 2-pass plan unless PHJ_P2PROBE=0 or a
 // tuning knob changed the tile shape (the probe walks 512 x 4096 tiles).
 bool use_p2probe(const phj_ctx* c, const Plan& pl, uint64_t nS, uint64_t nR) {
-    bool wc = false;
+    (void)nS;
     return c->tune.p2probe && !pl.chained && pl.npass == 2 && tile_shape(c, pl.nb2).tile == 4096 && tile_shape(c, pl.nb2).block == 512 &&
-           pass_tile(c, static_cast<uint32_t>(std::min<uint64_t>(nS, 0xffffffffu)), pl.nb1, &wc) == 4096 && !wc &&
+           tile_shape(c, pl.nb1).tile == 4096 &&
            probe_ht_lds_bytes(kProbeBlock * kProbeItems, pl.nb2) <= 160 * 1024 &&
            4 * nR + 2ull * pl.Ppad < (1ull << 32) && plan_empty0(pl) != 0;
 }
@@ -1396,21 +1281,19 @@ int join_nopart(phj_ctx* c, const phj_join_params* p, phj_join_result* r, uint32
         return set_err(c, PHJ_ERR_INVALID,
                        "LinearProbingHashTable::LinearProbingHashTable: numberOfObjects must be greater than zero.");
     if (R.n >= (1ull << 32)) return set_err(c, PHJ_ERR_RANGE, "build side above 2^32 tuples");
-    if (!marks && c->tune.np_ct && R.n < (1ull << 30)) return join_nopart_ct(c, p, r);
-    const double ratio = p->table_ratio > 0 ? p->table_ratio : c->tune.np_ratio;
+    if (!marks && R.n < (1ull << 30)) return join_nopart_ct(c, p, r);
+    const double ratio = p->table_ratio > 0 ? p->table_ratio : kNPDefaultRatio;
     if (ratio < 1.0) return set_err(c, PHJ_ERR_INVALID, "table_ratio must be >= 1");
     const double nbd = std::ceil(static_cast<double>(R.n) * ratio / kNPSlots);
     if (nbd >= 4294967295.0) return set_err(c, PHJ_ERR_RANGE, "table too large");
     const uint32_t nb0 = std::max<uint32_t>(1, static_cast<uint32_t>(nbd));
     // region build: 2^rbits regions of <= kNPRegionBuckets buckets (LDS-sized)
     NPHome g{nb0, nb0, 0, 0};
-    if (c->tune.np_region) {
-        g.rbits = std::min<uint32_t>(22, std::max<uint32_t>(1, ceil_log2((nb0 + kNPRegionBuckets - 1) / kNPRegionBuckets)));
-        g.nbr = (nb0 + (1u << g.rbits) - 1) >> g.rbits;
-        const uint64_t nbw = static_cast<uint64_t>(g.nbr) << g.rbits;
-        if (nbw >= 4294967295ull || g.nbr > 2 * kNPRegionBuckets) return set_err(c, PHJ_ERR_RANGE, "table too large");
-        g.nb = static_cast<uint32_t>(nbw);
-    }
+    g.rbits = std::min<uint32_t>(22, std::max<uint32_t>(1, ceil_log2((nb0 + kNPRegionBuckets - 1) / kNPRegionBuckets)));
+    g.nbr = (nb0 + (1u << g.rbits) - 1) >> g.rbits;
+    const uint64_t nbw = static_cast<uint64_t>(g.nbr) << g.rbits;
+    if (nbw >= 4294967295ull || g.nbr > 2 * kNPRegionBuckets) return set_err(c, PHJ_ERR_RANGE, "table too large");
+    g.nb = static_cast<uint32_t>(nbw);
     const uint32_t nb = g.nb;
     // the materialising probe stores a match as the uint32 slot b * 7 + s, and
     // kNoMatch (0xffffffff) must stay out of that range
@@ -1419,17 +1302,11 @@ int join_nopart(phj_ctx* c, const phj_join_params* p, phj_join_result* r, uint32
     PHJ_TRY(ensure(c, c->np_tab, static_cast<size_t>(nb) * sizeof(NPBucket)));
     PHJ_TRY(ensure(c, c->np_pays, static_cast<size_t>(nb) * kNPSlots * 8));
     PHJ_TRY(ensure(c, c->count, 8));
-    // hot-key cache for the count probe (not the materialising one)
-    const bool hot = !marks && c->tune.np_hot > 0 && S.n >= c->tune.np_hot_min;
-    if (hot) {
-        PHJ_TRY(ensure(c, c->np_hot, static_cast<size_t>(c->tune.np_hot_samples) * 8 + kHotCand * 16 + 16));
-        PHJ_TRY(ensure(c, c->np_img, kHotSlots * 9));
-    }
+    PHJ_TRY(ensure(c, c->np_ovf, R.n * 16));
+    PHJ_TRY(ensure(c, c->np_ovfb, R.n * 4));
+    PHJ_TRY(ensure(c, c->np_ovfn, 4));
     Plan rp;
-    if (g.rbits) {
-        PHJ_TRY(ensure(c, c->np_ovf, R.n * 16));
-        PHJ_TRY(ensure(c, c->np_ovfb, R.n * 4));
-        PHJ_TRY(ensure(c, c->np_ovfn, 4));
+    {
         phj_join_params pp = *p;
         pp.algo = PHJ_ALGO_RADIX;
         pp.num_partitions = 0;
@@ -1439,33 +1316,10 @@ int join_nopart(phj_ctx* c, const phj_join_params* p, phj_join_result* r, uint32
         PHJ_TRY(make_plan(c, &pp, rp));
         if (c->dry) return partition_side(c, PHJ_SIDE_BUILD, rp);
     }
-    if (c->dry) return PHJ_OK;
-    hipEvent_t e0, e1, e2, es = nullptr;
+    hipEvent_t e0, e1, e2;
     const uint32_t nR = static_cast<uint32_t>(R.n);
     PHJ_TRY(mark(c, &e0));
-    const uint32_t nsamp = c->tune.np_hot_samples;
-    auto* samp = static_cast<int64_t*>(c->np_hot.p);
-    auto* cand = reinterpret_cast<longlong2*>(samp + nsamp);
-    auto* cand_n = reinterpret_cast<uint32_t*>(cand + kHotCand);
-    if (hot) {
-        // the sample reads only S: it runs on the aux stream beside the build
-        PHJ_HIP(c, hipStreamWaitEvent(c->aux, e0, 0));
-        PHJ_HIP(c, hipMemsetAsync(cand_n, 0, 4, c->aux));
-        const auto* S_rel = reinterpret_cast<const longlong2*>(S.rel);
-        hipLaunchKernelGGL(k_np_hot_gather, dim3((nsamp + kBlock - 1) / kBlock), dim3(kBlock), 0, c->aux, S_rel, S.n,
-                           nsamp, samp);
-        if (p->hash == PHJ_HASH_MURMUR3)
-            hipLaunchKernelGGL(k_np_hot_count<kMurmur3>, dim3(kHotClasses), dim3(kBlock), 0, c->aux, samp, nsamp,
-                               p->hash_seed, cand, cand_n);
-        else
-            hipLaunchKernelGGL(k_np_hot_count<kXXH3>, dim3(kHotClasses), dim3(kBlock), 0, c->aux, samp, nsamp,
-                               p->hash_seed, cand, cand_n);
-        PHJ_LAUNCHED(c, "k_np_hot_count");
-        es = next_event(c);
-        if (!es) return set_err(c, PHJ_ERR_HIP, "hipEventCreate failed");
-        PHJ_HIP(c, hipEventRecord(es, c->aux));
-    }
-    if (g.rbits) {
+    {
         // the partition is part of the build (its R.* timers show it)
         PHJ_TRY(partition_side(c, PHJ_SIDE_BUILD, rp));
         const phj_partitioned& v = R.view;
@@ -1488,69 +1342,19 @@ int join_nopart(phj_ctx* c, const phj_join_params* p, phj_join_result* r, uint32
         hipLaunchKernelGGL(k_np_build_overflow, dim3(64), dim3(kBlock), 0, c->ks, ovn, ov, ovb, tab, pays, nb);
         PHJ_LAUNCHED(c, "k_np_build_overflow");
         PHJ_TRY(timer_end(c));
-    } else {
-        PHJ_TRY(timer_begin(c, "np.build", static_cast<uint64_t>(nR) * 32 + static_cast<uint64_t>(nb) * 64));
-        PHJ_HIP(c, hipMemsetAsync(c->np_tab.p, 0, static_cast<size_t>(nb) * sizeof(NPBucket), c->ks));
-        const uint32_t bg = (nR + kBlock - 1) / kBlock;
-        if (p->hash == PHJ_HASH_MURMUR3)
-            hipLaunchKernelGGL((k_np_build<kMurmur3>), dim3(bg), dim3(kBlock), 0, c->ks,
-                               reinterpret_cast<const longlong2*>(R.rel), nR, static_cast<NPBucket*>(c->np_tab.p),
-                               static_cast<int64_t*>(c->np_pays.p), nb, p->hash_seed);
-        else
-            hipLaunchKernelGGL((k_np_build<kXXH3>), dim3(bg), dim3(kBlock), 0, c->ks,
-                               reinterpret_cast<const longlong2*>(R.rel), nR, static_cast<NPBucket*>(c->np_tab.p),
-                               static_cast<int64_t*>(c->np_pays.p), nb, p->hash_seed);
-        PHJ_LAUNCHED(c, "k_np_build");
-        PHJ_TRY(timer_end(c));
     }
     PHJ_TRY(mark(c, &e1));
     PHJ_HIP(c, hipMemsetAsync(c->count.p, 0, 8, c->ks));
     if (S.n > 0) {
-        const uint64_t per = static_cast<uint64_t>(kBlock) * c->tune.np_items;
+        const uint64_t per = static_cast<uint64_t>(kBlock) * 4;
         const uint32_t pg = static_cast<uint32_t>(std::min<uint64_t>((S.n + per - 1) / per, 8192));
         PHJ_TRY(timer_begin(c, "np.probe", S.n * 16 + static_cast<uint64_t>(nb) * 64));
         const auto* S_rel = reinterpret_cast<const longlong2*>(S.rel);
         const auto* tab = static_cast<const NPBucket*>(c->np_tab.p);
         auto* cnt = static_cast<unsigned long long*>(c->count.p);
-#define PHJ_NP_PROBE(HKV, IT, NTV) \
-    hipLaunchKernelGGL((k_np_probe<HKV, IT, NTV>), dim3(pg), dim3(kBlock), 0, c->ks, S_rel, S.n, tab, g, p->hash_seed, cnt)
-#define PHJ_NP_PROBE_H(HKV)                                                      \
-    do {                                                                         \
-        if (c->tune.np_items == 8) {                                             \
-            if (c->tune.np_nt == 2) PHJ_NP_PROBE(HKV, 8, 2); else if (c->tune.np_nt) PHJ_NP_PROBE(HKV, 8, 1); else PHJ_NP_PROBE(HKV, 8, 0); \
-        } else {                                                                 \
-            if (c->tune.np_nt == 2) PHJ_NP_PROBE(HKV, 4, 2); else if (c->tune.np_nt) PHJ_NP_PROBE(HKV, 4, 1); else PHJ_NP_PROBE(HKV, 4, 0); \
-        }                                                                        \
-    } while (0)
-        if (hot) {
-            PHJ_HIP(c, hipStreamWaitEvent(c->ks, es, 0));
-            auto* img_keys = static_cast<int64_t*>(c->np_img.p);
-            auto* img_st = reinterpret_cast<uint8_t*>(img_keys + kHotSlots);
-            const void* kfn;
-            if (p->hash == PHJ_HASH_MURMUR3) {
-                hipLaunchKernelGGL(k_np_hot_resolve<kMurmur3>, dim3(1), dim3(kBlock), 0, c->ks, cand, cand_n, tab, g,
-                                   p->hash_seed, img_keys, img_st);
-                kfn = reinterpret_cast<const void*>(&k_np_probe_hot<kMurmur3, 4, 1>);
-            } else {
-                hipLaunchKernelGGL(k_np_hot_resolve<kXXH3>, dim3(1), dim3(kBlock), 0, c->ks, cand, cand_n, tab, g,
-                                   p->hash_seed, img_keys, img_st);
-                kfn = reinterpret_cast<const void*>(&k_np_probe_hot<kXXH3, 4, 1>);
-            }
-            PHJ_LAUNCHED(c, "k_np_hot_resolve");
-            int per_cu = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, kBlock, 0) != hipSuccess || per_cu < 1)
-                per_cu = 4;
-            const uint64_t want = (S.n + 4ull * kBlock - 1) / (4ull * kBlock);
-            const uint32_t hg = static_cast<uint32_t>(std::max<uint64_t>(
-                1, std::min<uint64_t>(want, static_cast<uint64_t>(per_cu) * c->num_cus)));
-            const auto* img_k = img_keys;
-            const auto* img_s = img_st;
-            uint64_t nS64 = S.n;
-            uint64_t seed = p->hash_seed;
-            void* kargs[] = {const_cast<longlong2**>(&S_rel), &nS64, const_cast<NPBucket**>(&tab), &g, &seed,
-                             const_cast<int64_t**>(&img_k), const_cast<uint8_t**>(&img_s), &cnt};
-            PHJ_HIP(c, hipLaunchKernel(kfn, dim3(hg), dim3(kBlock), kargs, 0, c->ks));
-        } else if (marks) {
+        // (the count takes join_nopart_ct below 2^30 build tuples; this bucket
+        // probe serves larger build sides and, with marks, the materialised join)
+        if (marks) {
             const uint32_t mg = static_cast<uint32_t>(std::min<uint64_t>((S.n + 4 * kBlock - 1) / (4 * kBlock), 8192));
             if (p->hash == PHJ_HASH_MURMUR3)
                 hipLaunchKernelGGL((k_np_probe_mark<kMurmur3>), dim3(mg), dim3(kBlock), 0, c->ks, S_rel, S.n, tab, g,
@@ -1558,12 +1362,11 @@ int join_nopart(phj_ctx* c, const phj_join_params* p, phj_join_result* r, uint32
             else
                 hipLaunchKernelGGL((k_np_probe_mark<kXXH3>), dim3(mg), dim3(kBlock), 0, c->ks, S_rel, S.n, tab, g,
                                    p->hash_seed, marks, cnt);
-        } else if (p->hash == PHJ_HASH_MURMUR3)
-            PHJ_NP_PROBE_H(kMurmur3);
-        else
-            PHJ_NP_PROBE_H(kXXH3);
-#undef PHJ_NP_PROBE_H
-#undef PHJ_NP_PROBE
+        } else if (p->hash == PHJ_HASH_MURMUR3) {
+            hipLaunchKernelGGL((k_np_probe<kMurmur3, 4, 1>), dim3(pg), dim3(kBlock), 0, c->ks, S_rel, S.n, tab, g, p->hash_seed, cnt);
+        } else {
+            hipLaunchKernelGGL((k_np_probe<kXXH3, 4, 1>), dim3(pg), dim3(kBlock), 0, c->ks, S_rel, S.n, tab, g, p->hash_seed, cnt);
+        }
         PHJ_LAUNCHED(c, "k_np_probe");
         PHJ_TRY(timer_end(c));
     }
@@ -1707,52 +1510,23 @@ int ctx_create_device(int device, phj_ctx** out) {
         const int t = env_int("PHJ_TILE", 4096);
         c->tune.tile = (t == 2048 || t == 8192) ? t : 4096;
     }
-    c->tune.p1_aos = env_int("PHJ_P1_AOS", 1) != 0;
-    c->tune.xcd_remap = env_int("PHJ_XCD_REMAP", 1) != 0;
-    c->tune.wc = env_int("PHJ_WC", 0) != 0;
-    c->tune.r_aux = env_int("PHJ_R_AUX", 1) != 0;
-    c->tune.probe_items = env_int("PHJ_PROBE_ITEMS", 8) == 16 ? 16 : 8;
-    c->tune.probe_wave = env_int("PHJ_PROBE_WAVE", 1);
     c->tune.block = env_int("PHJ_BLOCK", 512);
-    c->tune.nt_store = env_int("PHJ_NT", 0) != 0;
     c->tune.nt_load = std::min(2, std::max(0, env_int("PHJ_NT_LOAD", 1)));
-    c->tune.dcol = env_int("PHJ_DCOL", 1) != 0;
     c->tune.fused = env_int("PHJ_FUSED", 1) != 0;
-    c->tune.onepass_max = std::max(1, env_int("PHJ_ONEPASS_MAX", 256));
     c->tune.ptab = env_int("PHJ_PTAB", 1);
     c->tune.subpart = env_int("PHJ_SUBPART", 1) != 0;
     c->tune.timers = env_int("PHJ_TIMERS", 1) != 0;
-    {
-        const int k = env_int("PHJ_FUSED_KPL", 4);
-        c->tune.fused_kpl = (k == 2 || k == 8) ? k : 4;
-    }
     c->tune.p1_chunk = env_int("PHJ_P1_CHUNK", 1) != 0;
-    c->tune.np_nt = std::min(2, std::max(0, env_int("PHJ_NP_NT", 1)));
-    c->tune.np_items = env_int("PHJ_NP_ITEMS", 4) == 8 ? 8 : 4;
-    c->tune.np_region = env_int("PHJ_NP_REGION", 1) != 0;
-    c->tune.np_ct = env_int("PHJ_NP_CT", 1);
-    c->tune.np_hot = env_int("PHJ_NP_HOT", 1);
-    c->tune.np_hot_min = static_cast<uint64_t>(std::max(0, env_int("PHJ_NP_HOT_MIN", 1 << 20)));
-    c->tune.np_hot_samples = static_cast<uint32_t>(std::max(256, env_int("PHJ_NP_HOT_SAMPLES", 65536)));
     c->tune.p2probe = env_int("PHJ_P2PROBE", 1);
-    c->tune.p1_var = env_int("PHJ_P1_VAR", 3) & 3;
-    c->tune.p1_ko = env_int("PHJ_P1_KO", 1);
-    c->tune.p1_hcode = env_int("PHJ_P1_HCODE", 1);
-    if (const char* r = std::getenv("PHJ_NP_RATIO")) c->tune.np_ratio = std::max(1.0, std::atof(r));
     c->tune.p1_slots = env_int("PHJ_P1_SLOTS", 0);
     c->tune.p1_wpc2 = std::max(0, env_int("PHJ_P1_WPC2", 2));
     c->tune.p1_tps = std::max(1, env_int("PHJ_P1_TPS", static_cast<int>(kTilesPerShard)));
     c->tune.p1_min_tiles = std::max(0, env_int("PHJ_P1_MIN_TILES", 32768));
     c->tune.p1_ko_tps = std::max(1, env_int("PHJ_P1_KO_TPS", 1024));
-    c->tune.p1_ko_min_tiles = std::max(0, env_int("PHJ_P1_KO_MIN_TILES", 0));
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
     }
-    c->tune.wc_items = env_int("PHJ_WC_ITEMS", 8) == 4 ? 4 : 8;
-    c->tune.wc_lw = env_int("PHJ_WC_LW", 8) == 16 ? 16 : 8;
-    c->tune.wc_wgs = std::max(64, env_int("PHJ_WC_WGS", 1024));
-    if (c->tune.wc_items == 8 && c->tune.wc_lw == 16) c->tune.wc_items = 4;  // LDS budget
     // gfx950 launches accept dynamic LDS up to the 160 KiB per workgroup without an
     // opt-in attribute; clear any error a probe of the runtime left behind
     (void)hipGetLastError();
@@ -1862,11 +1636,11 @@ void phj_ctx_destroy(phj_ctx* c) {
     (void)hipStreamSynchronize(c->aux);
     for (SideState& S : c->side) {
         for (DevBuf* b : {&S.owned, &S.kA, &S.pA, &S.kB, &S.pB, &S.hist1, &S.hist2, &S.bounds1, &S.tbase2,
-                          &S.bounds, &S.partials, &S.tseg2, &S.dig, &S.ccur, &S.ctab, &S.tstart})
+                          &S.bounds, &S.partials, &S.tseg2, &S.dig, &S.ccur, &S.ctab, &S.tstart, &S.csink})
             free_buf(*b);
     }
     for (DevBuf* b : {&c->ht_tab, &c->ht_desc, &c->r_codes, &c->r_bounds, &c->scan_partials, &c->prep, &c->tkeys, &c->tpays, &c->toffs, &c->gcursor, &c->items, &c->biglist,
-                      &c->count, &c->np_tab, &c->np_pays, &c->np_ovf, &c->np_ovfb, &c->np_ovfn, &c->np_hot, &c->np_img, &c->fitems, &c->split, &c->mat_mark, &c->mat_cnt, &c->mat_rows})
+                      &c->count, &c->np_tab, &c->np_pays, &c->np_ovf, &c->np_ovfb, &c->np_ovfn, &c->fitems, &c->split, &c->mat_mark, &c->mat_cnt, &c->mat_rows})
         free_buf(*b);
     for (hipEvent_t e : c->evpool) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->stream);
@@ -2179,7 +1953,7 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
     PHJ_TRY(mark(c, &t0));
     PHJ_HIP(c, hipStreamWaitEvent(c->aux, t0, 0));
     PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, pl));
-    c->ks = c->tune.r_aux ? c->aux : c->stream;
+    c->ks = c->aux;
     int rc = partition_side(c, PHJ_SIDE_BUILD, pl);
     if (rc == PHJ_OK) rc = mark(c, &tr);
     c->ks = c->stream;

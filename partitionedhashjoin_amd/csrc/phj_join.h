@@ -16,7 +16,7 @@
 // Skew is handled by the item split: a hot partition becomes many S chunks.
 //
 // NoPartitioning path (src/NoPartitioning/HashJoin.hpp:76-187):
-//   k_np_build / k_np_probe    : one global bucketized linear-probing table in
+//   k_np_build_region / k_np_probe : one global bucketized linear-probing table in
 //                                HBM, 64-B buckets {7 keys, fill count}. As in
 //                                LinearProbing.hpp:22-83 occupancy is a
 //                                per-bucket fill counter (no sentinel key: every
@@ -856,32 +856,12 @@ __device__ __forceinline__ uint32_t np_home(uint64_t h, uint32_t nb) {
     return static_cast<uint32_t>(((h >> 32) * static_cast<uint64_t>(nb)) >> 32);
 }
 
-template <int HK>
-__global__ __launch_bounds__(kBlock) void k_np_build(const longlong2* R, uint32_t nR,
-                                                     NPBucket* tab, int64_t* pays, uint32_t nb,
-                                                     uint64_t seed) {
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= nR) return;
-    const longlong2 t = R[i];
-    uint32_t b = np_home(hash64<HK>(static_cast<uint64_t>(t.x), seed), nb);
-    for (uint32_t step = 0; step < nb; step++) {
-        const uint32_t slot = atomicAdd(&tab[b].fill, 1u);
-        if (slot < kNPSlots) {
-            tab[b].key[slot] = t.x;
-            pays[static_cast<size_t>(b) * kNPSlots + slot] = t.y;
-            return;
-        }
-        b = (b + 1 == nb) ? 0 : b + 1;
-    }
-}
-
 // Region layout of the NoPartitioning table (the default build): the table is
 // 2^rbits regions of nbr buckets; a key's region is the low rbits of its hash
 // (exactly the radix partition q = h & (2^rbits - 1)) and its home bucket
 // inside the region comes from the high 32 bits. Linear probing still walks
 // b, b + 1, ... over the whole table, so a full last bucket of a region
-// continues in the next region. rbits == 0: one region of nb buckets (the
-// atomic build's plain multiply-shift home).
+// continues in the next region.
 struct NPHome {
     uint32_t nb, nbr, rbits, pad;
 };
@@ -1055,192 +1035,6 @@ __global__ __launch_bounds__(kBlock) void k_np_probe(const longlong2* S, uint64_
                 if (hit)
                     hits++;
                 else if (fill >= kNPSlots)   // full home bucket: continue in the next ones (rare)
-                    hits += np_lookup(tab, nb, b[j] + 1 == nb ? 0 : b[j] + 1, key) ? 1u : 0u;
-            }
-        }
-    }
-    uint32_t x = hits;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x += __shfl_down(x, o, 64);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = x;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long t = 0;
-        for (int w = 0; w < kWaves; w++) t += red[w];
-        if (t) atomicAdd(count, t);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// NoPartitioning hot-key cache. Under Zipf a few keys
-// take most probes (s = 1.05 over 10M keys: the top key 8.7 %, the top ~1000
-// about half); their buckets are L2 hits, but every probe of one key lands on
-// the same cache line and L2 channel, which serialises. The probe therefore
-// answers the hottest keys from a small LDS table first: a strided sample of S
-// is counted (k_np_hot_sample), keys seen >= kHotMinCount times are looked up
-// once in the global table after the build (k_np_hot_resolve) and every probe
-// workgroup copies the resulting image (keys + {empty, absent, present}) into
-// LDS (k_np_probe_hot). The sample only chooses WHICH keys are cached; each
-// cached answer is the global table's own lookup, so the count is unchanged.
-// ---------------------------------------------------------------------------
-constexpr uint32_t kHotSlots = 4096;     // direct-mapped LDS table slots
-constexpr uint32_t kHotCand = 4096;      // sampled candidates (key, count)
-constexpr uint32_t kHotClasses = 64;     // sampler workgroups (a hash class each)
-constexpr uint32_t kHotSampleSlots = 2048;
-constexpr uint32_t kHotMinCount = 3;
-
-__device__ __forceinline__ uint32_t hot_slot(uint64_t h) { return static_cast<uint32_t>(h >> 20) & (kHotSlots - 1); }
-
-// A strided sample of the probe keys, gathered contiguously (one load per lane).
-__global__ __launch_bounds__(kBlock) void k_np_hot_gather(const longlong2* S, uint64_t nS, uint32_t nsamp,
-                                                          int64_t* samp) {
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= nsamp) return;
-    const uint64_t stride = nS / nsamp > 0 ? nS / nsamp : 1;
-    const uint64_t idx = static_cast<uint64_t>(i) * stride;
-    samp[i] = idx < nS ? S[idx].x : S[0].x;
-}
-
-// Count the sampled keys per hash class (workgroup c takes the keys with
-// (h >> 58) == c); append (key, count) for those seen >= kHotMinCount times.
-template <int HK>
-__global__ __launch_bounds__(kBlock) void k_np_hot_count(const int64_t* samp, uint32_t nsamp, uint64_t seed,
-                                                         longlong2* cand, uint32_t* cand_n) {
-    constexpr unsigned long long kEmpty = 0x8000000000000000ull;   // a sampled INT64_MIN is skipped
-    __shared__ unsigned long long lkey[kHotSampleSlots];
-    __shared__ uint32_t lcnt[kHotSampleSlots];
-    for (uint32_t i = threadIdx.x; i < kHotSampleSlots; i += kBlock) {
-        lkey[i] = kEmpty;
-        lcnt[i] = 0;
-    }
-    __syncthreads();
-    const uint32_t c = blockIdx.x;
-    for (uint32_t i = threadIdx.x; i < nsamp; i += kBlock) {
-        const unsigned long long key = static_cast<unsigned long long>(samp[i]);
-        const uint64_t h = hash64<HK>(key, seed);
-        if (static_cast<uint32_t>(h >> 58) != c || key == kEmpty) continue;
-        uint32_t sl = static_cast<uint32_t>(h >> 32) & (kHotSampleSlots - 1);
-        for (uint32_t t = 0; t < kHotSampleSlots; t++) {
-            const unsigned long long prev = atomicCAS(&lkey[sl], kEmpty, key);
-            if (prev == kEmpty || prev == key) {
-                atomicAdd(&lcnt[sl], 1u);
-                break;
-            }
-            sl = (sl + 1) & (kHotSampleSlots - 1);
-        }
-    }
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < kHotSampleSlots; i += kBlock) {
-        if (lcnt[i] >= kHotMinCount) {
-            const uint32_t o = atomicAdd(cand_n, 1u);
-            if (o < kHotCand) cand[o] = make_longlong2(static_cast<int64_t>(lkey[i]), lcnt[i]);
-        }
-    }
-}
-
-// One workgroup: a direct-mapped table of the candidates (a slot keeps its
-// most-sampled key), each kept key looked up once in the built table. The
-// image the probe copies: keys[kHotSlots] then state[kHotSlots] (u8: 0 empty,
-// 1 absent from R, 2 present).
-template <int HK>
-__global__ __launch_bounds__(kBlock) void k_np_hot_resolve(const longlong2* cand, const uint32_t* cand_n,
-                                                           const NPBucket* tab, NPHome g, uint64_t seed,
-                                                           int64_t* img_keys, uint8_t* img_state) {
-    __shared__ uint32_t lwin[kHotSlots];
-    for (uint32_t i = threadIdx.x; i < kHotSlots; i += kBlock) lwin[i] = 0;
-    __syncthreads();
-    const uint32_t n = min(*cand_n, kHotCand);
-    for (uint32_t i = threadIdx.x; i < n; i += kBlock) {
-        const longlong2 kc = cand[i];
-        const uint64_t h = hash64<HK>(static_cast<uint64_t>(kc.x), seed);
-        const uint32_t cnt = static_cast<uint32_t>(min<int64_t>(kc.y, 0xffff));
-        atomicMax(&lwin[hot_slot(h)], (cnt << 16) | (i + 1));
-    }
-    __syncthreads();
-    for (uint32_t sl = threadIdx.x; sl < kHotSlots; sl += kBlock) {
-        const uint32_t w = lwin[sl];
-        int64_t key = 0;
-        uint8_t st = 0;
-        if (w) {
-            key = cand[(w & 0xffff) - 1].x;
-            const uint64_t h = hash64<HK>(static_cast<uint64_t>(key), seed);
-            st = np_lookup(tab, g.nb, np_home_r(h, g), key) ? 2 : 1;
-        }
-        img_keys[sl] = key;
-        img_state[sl] = st;
-    }
-}
-
-// k_np_probe with the direct-mapped hot-key LDS table in front: a probe key
-// equal to its slot's key is answered from the slot; the others read their
-// home bucket as before (ITEMS random reads in flight per thread, issued only
-// for the lanes that need them). Persistent grid: each workgroup copies the
-// image once.
-template <int HK, int ITEMS, int NT>
-__global__ __launch_bounds__(kBlock) void k_np_probe_hot(const longlong2* S, uint64_t nS, const NPBucket* tab,
-                                                         NPHome g, uint64_t seed, const int64_t* img_keys,
-                                                         const uint8_t* img_state, unsigned long long* count) {
-    __shared__ int64_t hkey[kHotSlots];
-    __shared__ uint8_t hst[kHotSlots];
-    __shared__ uint32_t red[kWaves];
-    {
-        const longlong2* src = reinterpret_cast<const longlong2*>(img_keys);
-        longlong2* dst = reinterpret_cast<longlong2*>(hkey);
-        for (uint32_t i = threadIdx.x; i < kHotSlots / 2; i += kBlock) dst[i] = src[i];
-        const uint4* s8 = reinterpret_cast<const uint4*>(img_state);
-        uint4* d8 = reinterpret_cast<uint4*>(hst);
-        for (uint32_t i = threadIdx.x; i < kHotSlots / 16; i += kBlock) d8[i] = s8[i];
-    }
-    __syncthreads();
-    const uint32_t nb = g.nb;
-    uint32_t hits = 0;
-    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kBlock * ITEMS;
-    for (uint64_t base = static_cast<uint64_t>(blockIdx.x) * kBlock * ITEMS; base < nS; base += stride) {
-        int64_t k[ITEMS];
-#pragma unroll
-        for (int j = 0; j < ITEMS; j++) {
-            const uint64_t idx = base + static_cast<uint64_t>(j) * kBlock + threadIdx.x;
-            if constexpr (NT > 0)
-                k[j] = idx < nS ? __builtin_nontemporal_load(&S[idx].x) : 0;
-            else
-                k[j] = idx < nS ? S[idx].x : 0;
-        }
-        uint32_t b[ITEMS];
-        bool cold[ITEMS];
-#pragma unroll
-        for (int j = 0; j < ITEMS; j++) {
-            const uint64_t idx = base + static_cast<uint64_t>(j) * kBlock + threadIdx.x;
-            const uint64_t h = hash64<HK>(static_cast<uint64_t>(k[j]), seed);
-            b[j] = np_home_r(h, g);
-            const uint32_t sl = hot_slot(h);
-            const uint32_t st = hst[sl];
-            const bool hot = st != 0 && hkey[sl] == k[j];
-            cold[j] = idx < nS && !hot;
-            hits += (idx < nS && hot && st == 2) ? 1u : 0u;
-        }
-        // the cold keys' home buckets, all requested before any is compared
-        longlong2 q[ITEMS][4];
-#pragma unroll
-        for (int j = 0; j < ITEMS; j++) {
-            if (cold[j]) {
-                const longlong2* bp = reinterpret_cast<const longlong2*>(tab + b[j]);
-#pragma unroll
-                for (int w = 0; w < 4; w++) q[j][w] = bp[w];
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < ITEMS; j++) {
-            if (cold[j]) {
-                const int64_t key = k[j];
-                const uint32_t fill = static_cast<uint32_t>(q[j][3].y);
-                const uint32_t c = fill < kNPSlots ? fill : kNPSlots;
-                const bool hit = (c > 0 && q[j][0].x == key) || (c > 1 && q[j][0].y == key) ||
-                                 (c > 2 && q[j][1].x == key) || (c > 3 && q[j][1].y == key) ||
-                                 (c > 4 && q[j][2].x == key) || (c > 5 && q[j][2].y == key) ||
-                                 (c > 6 && q[j][3].x == key);
-                if (hit)
-                    hits++;
-                else if (fill >= kNPSlots)
                     hits += np_lookup(tab, nb, b[j] + 1 == nb ? 0 : b[j] + 1, key) ? 1u : 0u;
             }
         }

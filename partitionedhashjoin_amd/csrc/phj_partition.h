@@ -22,6 +22,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "phj_hash.h"
 
 namespace phj {
@@ -86,6 +88,7 @@ constexpr uint32_t kTilesPerShard = 3072;
 __host__ __device__ constexpr size_t chunk_pool_word(uint32_t nb, uint32_t x) { return (static_cast<size_t>(kShards) * nb + 31) / 32 * 32 + 32 * x; }
 __host__ __device__ constexpr size_t chunk_ticket_word(uint32_t nb, uint32_t x) { return chunk_pool_word(nb, kShards + x); }
 __host__ __device__ constexpr size_t chunk_hint_word(uint32_t nb) { return chunk_pool_word(nb, 2 * kShards); }
+constexpr uint32_t kSinkGroups = 1024;   // k_chunk_codes: workgroups with their own sink words (PassArgs::sink)
 __host__ __device__ constexpr size_t chunk_state_bytes(uint32_t nb) { return chunk_hint_word(nb) * 4 + static_cast<size_t>(kShards) * nb * 8; }
 
 struct PassArgs {
@@ -127,6 +130,7 @@ struct PassArgs {
     uint32_t pool_stride;       // chunks of one shard's pool
     uint32_t nshards;           // chains per digit (<= kShards)
     uint32_t keys_only;         // chunked pass 1 for the counting probe: only the key column is written / read
+    unsigned long long* sink;   // k_chunk_codes: [grid][BLOCK] words the void claims / stores target (never read)
     DigitFn f;
 };
 
@@ -224,7 +228,7 @@ __device__ __forceinline__ uint32_t agg_rank_lds(uint32_t* C, uint32_t d, bool v
 }
 
 // Exclusive scan of one value per thread across a block of NW waves.
-template <int NW>
+template <int NW, bool TRAIL = true>
 __device__ __forceinline__ uint32_t block_exclusive_scan_t(uint32_t v, uint32_t* tmp,
                                                            uint32_t& total) {
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -243,7 +247,7 @@ __device__ __forceinline__ uint32_t block_exclusive_scan_t(uint32_t v, uint32_t*
         if (w < (int)wave) before += s;
         all += s;
     }
-    __syncthreads();
+    if constexpr (TRAIL) __syncthreads();   // TRAIL = false: the caller's next barriers order tmp's reuse
     total = all;
     return before + x - v;
 }
@@ -577,37 +581,36 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(PassArgs a) {
 // on a single per-digit counter row instead of the stable 64-lane match
 // ranking (nbits + 1 ballots per tuple). VAR bit 1: the sorted tile is held as
 // 16-B tuples (one ds_write_b128 / ds_read_b128 per tuple instead of two
-// 8-B column accesses). VAR bit 2 (the counting probe consumes the output,
-// HashJoin.hpp:295-301 reads only the key): keys only, loaded, sorted and
-// written (8 B per tuple out instead of 16; half the LDS, three workgroups
-// per CU). VAR bit 3 (with bit 2): the key is written as its hash code, which
-// the digit needed anyway, so the probe and its tables never hash again
-// (PHJ_P1_HCODE, phj_hash.h kHashed).
+// 8-B column accesses). The host launches VAR 3; the keys-only hash-code form
+// the counting probe consumes is k_chunk_codes below.
 template <int BLOCK, int ITEMS, int HK, int VAR = 0>
 __global__ __launch_bounds__(BLOCK)
-__attribute__((amdgpu_waves_per_eu(((VAR & 4) ? 3 : (BLOCK * ITEMS <= 4096 ? 2 : 1)) * BLOCK / 256)))   // what the LDS lets share a CU
+__attribute__((amdgpu_waves_per_eu((BLOCK * ITEMS <= 4096 ? 2 : 1) * BLOCK / 256)))   // what the LDS lets share a CU
 void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
     constexpr int NW = BLOCK / 64;
     constexpr int T = BLOCK * ITEMS;
-    constexpr bool ARANK = (VAR & 1) != 0, KO = (VAR & 4) != 0, LAOS = (VAR & 2) != 0 && !KO;
-    constexpr bool HC = KO && (VAR & 8) != 0;   // keys only, written as hash codes
+    constexpr bool ARANK = (VAR & 1) != 0, LAOS = (VAR & 2) != 0;
     // atomic ranking + one 16-B access per element: a digit's three write
     // offsets packed in one 16-B LDS entry (one ds_read_b128 per element in
     // the write loop), placed in the counter rows the atomic ranking leaves unused
-    constexpr bool PACK = ARANK && (LAOS || KO) && NW >= 8;
+    constexpr bool PACK = ARANK && LAOS && NW >= 8;
     constexpr int NWR = ARANK ? 1 : NW;   // counter rows
+    // atomic ranking: two counter rows used alternately, so a tile's row is
+    // zeroed while the previous one is still read and the loop needs four
+    // barriers per tile instead of seven
+    constexpr bool DB = ARANK;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t nb = a.nbins;
     int64_t* skey = reinterpret_cast<int64_t*>(smem);
     int64_t* spay = skey + T;
     longlong2* stup = reinterpret_cast<longlong2*>(smem);     // LAOS: [T] tuples over skey/spay
-    uint32_t* wcnt = reinterpret_cast<uint32_t*>(KO ? skey + T : spay + T);  // [NW][nb]
+    uint32_t* wcnt = reinterpret_cast<uint32_t*>(spay + T);  // [NW][nb]
     uint32_t* gofs = wcnt + NW * nb;                          // [nb] k <  dsplit: slot = gofs + k
     uint32_t* dstart = gofs + nb;                             // [nb] k >= dsplit: slot = dstart + k
     uint32_t* tmp = dstart + nb;                              // 16 words
     const SortedDigits sdig{tmp + 16, nb <= 256};             // [T]
     uint32_t* dsplit = static_cast<uint32_t*>(sdig.end(T));   // [nb]
-    uint4* wdesc = reinterpret_cast<uint4*>(wcnt + ((nb + 3u) & ~3u));   // PACK: [nb] {k < split: slot - k, else, split}
+    uint4* wdesc = reinterpret_cast<uint4*>(wcnt + (((DB ? 2u : 1u) * nb + 3u) & ~3u));   // PACK: [nb] {k < split: slot - k, else, split}
 
     const uint32_t x = blockIdx.x % a.nshards, slots = gridDim.x / a.nshards;
     const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -632,11 +635,7 @@ void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
 #pragma unroll
         for (int i = 0; i < ITEMS; i++) {
             const uint32_t ix = min(lo + wbase + i * 64 + lane, a.n - 1);
-            if constexpr (KO) {
-                pay[i] = 0;
-                if (a.nt_load) key[i] = __builtin_nontemporal_load(&rel[ix].x);
-                else key[i] = rel[ix].x;
-            } else if (a.nt_load) {
+            if (a.nt_load) {
                 typedef long long v2i __attribute__((ext_vector_type(2)));
                 const v2i v = __builtin_nontemporal_load(reinterpret_cast<const v2i*>(rel) + ix);
                 key[i] = v.x;
@@ -649,31 +648,30 @@ void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
         }
     };
     load(tile);
+    uint32_t par = 0;   // DB: this tile's counter row
+    if constexpr (DB) {
+        for (uint32_t i = tid; i < 2 * nb; i += BLOCK) wcnt[i] = 0;
+        __syncthreads();
+    }
 
     for (;;) {
         const uint32_t lo = tile * T, cnt = min(static_cast<uint32_t>(T), a.n - lo);
-        for (uint32_t i = tid; i < NWR * nb; i += BLOCK) wcnt[i] = 0;
-        __syncthreads();
+        if constexpr (!DB) {
+            for (uint32_t i = tid; i < NWR * nb; i += BLOCK) wcnt[i] = 0;
+            __syncthreads();
+        }
         uint32_t dig[ITEMS], rank[ITEMS];
-        uint32_t* my = wcnt + (ARANK ? 0u : wave * nb);
+        uint32_t* const crow = wcnt + par * nb;   // DB: this tile's counter row
+        uint32_t* my = DB ? crow : wcnt + (ARANK ? 0u : wave * nb);
+        const uint32_t next = tile + slots;
 #pragma unroll
         for (int i = 0; i < ITEMS; i++) {
             const uint32_t e = wbase + i * 64 + lane;
             const bool valid = e < cnt;
-            uint32_t d;
-            if constexpr (HC) {
-                // the key's hash code goes out in its place (phj_hash.h: kHashed)
-                const uint64_t h = hash64<HK>(static_cast<uint64_t>(key[i]), a.f.seed);
-                d = valid ? static_cast<uint32_t>(q_from_hash(h, a.f) >> a.f.shift) & a.f.dmask : 0u;
-                key[i] = static_cast<int64_t>(h);
-            } else {
-                d = valid ? digit_of<HK>(static_cast<uint64_t>(key[i]), a.f) : 0u;
-            }
+            const uint32_t d = valid ? digit_of<HK>(static_cast<uint64_t>(key[i]), a.f) : 0u;
             dig[i] = d;
             rank[i] = 0;
             if constexpr (ARANK) {
-                // measured: plain atomics beat the wave-aggregated agg_rank_lds
-                // here by 0.15 ms at 200M (C2 and C5 alike)
                 rank[i] = valid ? atomicAdd(&my[d], 1u) : 0u;
             } else {
                 const uint64_t peers = match_digit(d, valid, a.nbits);
@@ -690,18 +688,19 @@ void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
         uint32_t c = 0, ds = 0, v0 = 0;
         unsigned long long hint = 0;
         {
+            uint32_t* const rows = DB ? crow : wcnt;
             if (tid < nb) {
 #pragma unroll
-                for (int w = 0; w < NWR; w++) c += wcnt[w * nb + tid];
+                for (int w = 0; w < NWR; w++) c += rows[w * nb + tid];
             }
             uint32_t total;
-            uint32_t run = block_exclusive_scan_t<NW>(c, tmp, total);
+            uint32_t run = block_exclusive_scan_t<NW, !DB>(c, tmp, total);
             ds = run;
             if (tid < nb) {
 #pragma unroll
                 for (int w = 0; w < NWR; w++) {
-                    const uint32_t v = wcnt[w * nb + tid];
-                    wcnt[w * nb + tid] = run;
+                    const uint32_t v = rows[w * nb + tid];
+                    rows[w * nb + tid] = run;
                     run += v;
                 }
             }
@@ -722,9 +721,7 @@ void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
             const uint32_t e = wbase + i * 64 + lane;
             if (e < cnt) {
                 const uint32_t pos = my[dig[i]] + rank[i];
-                if constexpr (KO) {
-                    skey[pos] = key[i];
-                } else if constexpr (LAOS) {
+                if constexpr (LAOS) {
                     stup[pos] = make_longlong2(key[i], pay[i]);
                 } else {
                     skey[pos] = key[i];
@@ -733,9 +730,15 @@ void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
                 sdig.put(pos, dig[i]);
             }
         }
-        // the tile is in LDS: the next tile's loads and reservation go out
-        // behind the claims, into the same registers
-        const uint32_t next = tile + slots;
+        if constexpr (DB) {
+            // the next tile's row: its last readers (the previous tile's
+            // scatter) are behind this tile's barriers; the barrier below
+            // orders these zeros before the next tile's atomics
+            uint32_t* const other = wcnt + (par ^ 1u) * nb;
+            for (uint32_t i = tid; i < nb; i += BLOCK) other[i] = 0;
+        }
+        // the tile is in LDS: the next tile's loads go out behind the claims,
+        // into the same registers
         load(next < t_end ? next : tile);   // unconditional (a last one goes unused): exact vmcnt waits
         if (tid < nb && c) {
             const uint32_t d = tid;
@@ -793,10 +796,7 @@ void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
                     o = (k < dsplit[d] ? gofs[d] : dstart[d]) + k;
                 }
                 int64_t tk, tp;
-                if constexpr (KO) {
-                    a.out_keys[o] = skey[k];
-                    continue;
-                } else if constexpr (LAOS) {
+                if constexpr (LAOS) {
                     const longlong2 t = stup[k];
                     tk = t.x;
                     tp = t.y;
@@ -810,7 +810,209 @@ void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
         }
         if (next >= t_end) break;
         tile = next;
-        __syncthreads();   // LDS reads of this tile's stores before the next tile's counts
+        par ^= 1u;
+        // LDS reads of this tile's stores before the next tile's LDS writes:
+        // with DB the next tile's first LDS write to skey / wdesc / tmp comes
+        // after its ranking barrier
+        if constexpr (!DB) __syncthreads();
+    }
+}
+
+// LDS of k_chunk_codes: the sorted tile, two counter rows, the packed slot
+// descriptors and 32 words of scan / reservation state
+__host__ __device__ constexpr size_t chunk_codes_lds_bytes(int T, uint32_t nb) {
+    return static_cast<size_t>(T) * 8 + (static_cast<size_t>(2 * nb + 3) / 4 * 4 + 4 * static_cast<size_t>(nb)) * 4 + 128;
+}
+
+// Chunked pass 1, code form: the S side of the counting on-chip join
+// (HashJoin.hpp:295-301 reads only the key, so only the key's hash code goes
+// out: 8 B per tuple, phj_hash.h kHashed). Same chunk protocol and output as
+// k_scatter_chunked (VAR 3 there), laid out for the memory pipeline:
+//  - the next tile's loads go out right after this tile is hashed, so they are
+//    in flight through the ranking, the claims and the write-out;
+//  - every lane issues the same global operations on every path (see the
+//    sink words below): vmcnt retires in issue order and the compiler counts
+//    only what every path issues, so one skipped instruction would make the
+//    next tile's first wait a wait for this tile's stores as well;
+//  - two counter rows used alternately: four barriers per tile, not seven.
+// (Deferring the claims' resolution by a tile was measured 0.5 ms slower at
+// 200M: a chunk's owner then publishes its id a tile late and the runs that
+// continue the chunk wait for it.)
+template <int BLOCK, int ITEMS, int HK>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(2 * BLOCK / 256)))
+void k_chunk_codes(PassArgs a, uint32_t ntiles, uint32_t per) {
+    constexpr int NW = BLOCK / 64;
+    constexpr int T = BLOCK * ITEMS;
+    static_assert(NW <= 16, "scan words [0, NW) below the reservation words");
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t nb = a.nbins;   // host: nb <= BLOCK (digit d = thread d)
+    int64_t* sbuf = reinterpret_cast<int64_t*>(smem);                       // [T] sorted codes
+    uint32_t* wcnt = reinterpret_cast<uint32_t*>(sbuf + T);                 // [2][nb] counter rows
+    uint4* wdesc = reinterpret_cast<uint4*>(wcnt + (2 * nb + 3u) / 4 * 4);  // [nb] {k < split: slot - k, else, split}
+    uint32_t* tmp = reinterpret_cast<uint32_t*>(wdesc + nb);                // [0, NW) scan; 16, 17 reservations
+
+    const uint32_t x = blockIdx.x % a.nshards, slots = gridDim.x / a.nshards;
+    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const uint32_t t_end = min(ntiles, (x + 1) * per);
+    uint32_t tile = x * per + blockIdx.x / a.nshards;
+    if (tile >= t_end) return;
+    const uint32_t wbase = wave * 64 * ITEMS;
+    uint32_t* curs = a.chunk_cursor + static_cast<size_t>(x) * nb;   // this shard's chains
+    uint32_t* pool = a.chunk_cursor + chunk_pool_word(nb, x);
+    unsigned long long* hints = reinterpret_cast<unsigned long long*>(a.chunk_cursor + chunk_hint_word(nb)) + static_cast<size_t>(x) * nb;
+    const unsigned long long tag = static_cast<unsigned long long>(a.gen) << 32;
+    // a code's digit; pow2 = the plan's uniform power-of-two form (q = h & (P - 1),
+    // no refinement), hoisted out of the per-element loops
+    const bool pow2q = a.f.mode == 0 && a.f.sub_bits == 0;
+    auto code_digit = [&](uint64_t h, auto pow2) -> uint32_t {
+        if constexpr (decltype(pow2)::value) return static_cast<uint32_t>((h & (a.f.P - 1)) >> a.f.shift) & a.f.dmask;
+        else return static_cast<uint32_t>(q_from_hash(h, a.f) >> a.f.shift) & a.f.dmask;
+    };
+    // sink words: a lane without an element stores to its own word here
+    // instead of branching round the store
+    int64_t* const ssink = reinterpret_cast<int64_t*>(a.sink + static_cast<size_t>(blockIdx.x % kSinkGroups) * BLOCK + tid);
+
+    int64_t key[ITEMS];
+    const longlong2* rel = reinterpret_cast<const longlong2*>(a.in_keys);
+    auto load = [&](uint32_t t) {   // clamped: the same loads on every path
+        const uint32_t lo = t * T;
+#pragma unroll
+        for (int i = 0; i < ITEMS; i++) {
+            const uint32_t ix = min(lo + wbase + i * 64 + lane, a.n - 1);
+            if (a.nt_load) key[i] = __builtin_nontemporal_load(&rel[ix].x);
+            else key[i] = rel[ix].x;
+        }
+    };
+
+    for (uint32_t i = tid; i < 2 * nb; i += BLOCK) wcnt[i] = 0;
+    load(tile);
+    // the loop's entry mirrors its back edge (loads, then ITEMS stores), so the
+    // first waits need not assume an empty queue
+    {
+#pragma unroll
+        for (int i = 0; i < ITEMS; i++) {
+            __hip_atomic_store(ssink, 0ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __asm__ volatile("" ::: "memory");
+        }
+    }
+    __syncthreads();
+    uint32_t par = 0;   // this tile's counter row
+    for (;;) {
+        const uint32_t cnt = min(static_cast<uint32_t>(T), a.n - tile * T);
+        const uint32_t next = tile + slots;
+        uint32_t* const crow = wcnt + par * nb;
+        int64_t code[ITEMS];
+        uint32_t dig[ITEMS], rank[ITEMS];
+        auto hash_all = [&](auto pow2) {
+#pragma unroll
+            for (int i = 0; i < ITEMS; i++) {
+                const uint64_t h = hash64<HK>(static_cast<uint64_t>(key[i]), a.f.seed);
+                code[i] = static_cast<int64_t>(h);
+                dig[i] = wbase + i * 64 + lane < cnt ? code_digit(h, pow2) : 0u;
+            }
+        };
+        if (pow2q) hash_all(std::true_type{});
+        else hash_all(std::false_type{});
+        load(next < t_end ? next : tile);   // unconditional (a last one goes unused)
+        // one LDS atomic per code, back to back (an invalid lane adds 0 to
+        // digit 0; measured: plain atomics beat the wave-aggregated
+        // agg_rank_lds here by 0.15 ms at 200M)
+#pragma unroll
+        for (int i = 0; i < ITEMS; i++) rank[i] = atomicAdd(&crow[dig[i]], wbase + i * 64 + lane < cnt ? 1u : 0u);
+        __syncthreads();
+        // digit totals (d = tid) -> tile-local starts; claim the run in the chain
+        const uint32_t c = tid < nb ? crow[tid] : 0u;
+        uint32_t total;
+        const uint32_t ds = block_exclusive_scan_t<NW, false>(c, tmp, total);
+        if (tid < nb) crow[tid] = ds;
+        uint32_t v0 = 0;
+        unsigned long long hint = 0;
+        if (tid < nb && c) {   // waited for below, in this tile: a conditional issue costs no wait
+            v0 = atomicAdd(curs + tid, c);
+            hint = __hip_atomic_load(hints + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (tid == 0) {
+            // the tile's reserved pool chunks are static: shard x's pool keeps
+            // its first 2 * per chunks for its tiles, two each
+            tmp[16] = x * a.pool_stride + 2 * (tile - x * per);
+            tmp[17] = 0;
+        }
+        __syncthreads();
+        {
+            uint32_t base[ITEMS];
+#pragma unroll
+            for (int i = 0; i < ITEMS; i++) base[i] = crow[dig[i]];
+#pragma unroll
+            for (int i = 0; i < ITEMS; i++)
+                if (wbase + i * 64 + lane < cnt) sbuf[base[i] + rank[i]] = code[i];
+            // the next tile's counter row (its last reader, the previous
+            // tile's sort, is behind this tile's barriers)
+            uint32_t* const other = wcnt + (par ^ 1u) * nb;
+            for (uint32_t i = tid; i < nb; i += BLOCK) other[i] = 0;
+        }
+        // chain protocol (k_scatter_chunked): digit tid's run -> chunk ids -> wdesc[tid]
+        if (tid < nb && c) {
+            const uint32_t d = tid;
+            const uint32_t off = v0 % T, k0 = v0 / T, k1 = (v0 + c - 1) / T;
+            unsigned long long* tab = a.chunk_tab + (static_cast<size_t>(x) * nb + d) * a.maxch;
+            auto take = [&]() -> uint32_t {
+                const uint32_t r = atomicAdd(&tmp[17], 1u);
+                if (r < 2) return tmp[16] + r;
+                return x * a.pool_stride + 2 * per + atomicAdd(pool, 1u);
+            };
+            auto publish = [&](uint32_t k, uint32_t id) {
+                __hip_atomic_store(&tab[k], tag | id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                atomicMax(hints + d, (static_cast<unsigned long long>(k + 1) << 32) | id);
+            };
+            uint32_t id0 = 0, id1 = 0;
+            if (off == 0) {
+                id0 = take();
+                publish(k0, id0);
+            }
+            if (k1 != k0) {
+                id1 = take();
+                publish(k1, id1);
+            }
+            if (off != 0) {
+                if ((hint >> 32) == k0 + 1ull) {
+                    id0 = static_cast<uint32_t>(hint);
+                } else {
+                    unsigned long long v;
+                    while (((v = __hip_atomic_load(&tab[k0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) != a.gen)
+                        __builtin_amdgcn_s_sleep(2);
+                    id0 = static_cast<uint32_t>(v);
+                }
+            }
+            // sorted element k of digit d goes to chain slot v0 + (k - ds)
+            const uint32_t split = ds + (T - off);
+            wdesc[d] = make_uint4(id0 * T + off - ds, id1 * T - split, split, 0u);
+        }
+        __syncthreads();
+        // sorted element k: code, digit, slot, all LDS reads of the ITEMS
+        // elements in flight together; a lane past the tile stores to its sink
+        auto write_out = [&](auto pow2) {
+            int64_t v[ITEMS];
+            uint32_t o[ITEMS];
+#pragma unroll
+            for (int i = 0; i < ITEMS; i++) v[i] = sbuf[i * BLOCK + tid];
+#pragma unroll
+            for (int i = 0; i < ITEMS; i++) {
+                const uint32_t k = i * BLOCK + tid;
+                const uint4 w = wdesc[code_digit(static_cast<uint64_t>(v[i]), pow2)];
+                o[i] = (k < w.z ? w.x : w.y) + k;
+            }
+#pragma unroll
+            for (int i = 0; i < ITEMS; i++) *(i * BLOCK + tid < cnt ? a.out_keys + o[i] : ssink) = v[i];
+        };
+        if (pow2q) write_out(std::true_type{});
+        else write_out(std::false_type{});
+        // the claim's registers stay live past the write-out: else they are
+        // reused there, and a lane that issued no claim would first wait for
+        // everything in flight (the compiler cannot tell which lanes did)
+        __asm__ volatile("" ::"v"(v0), "v"(hint));
+        if (next >= t_end) return;
+        tile = next;
+        par ^= 1u;
     }
 }
 

@@ -19,8 +19,8 @@
 //                     table of its final partition
 //
 // Table of a final partition p: an open-addressed array of codes in 2-slot
-// (16-B) buckets, cap = the smallest power of two >= 1.5 * |R_p| slots (load
-// <= 2/3), home bucket (c >> 24) & (buckets - 1), linear probing over buckets
+// (16-B) buckets, cap = the smallest power of two >= 2 |R_p| slots (load
+// <= 1/2; >= 1.5 |R_p| beyond one wave's LDS slice, ht_cap), home bucket (c >> 24) & (buckets - 1), linear probing over buckets
 // with wrap-around, a bucket's slots filled in order, duplicates stored once
 // (the count is a semi-join, a set test). There is no occupancy word and no
 // key value is reserved: an empty slot holds E_p, a code of ANOTHER
@@ -46,6 +46,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "phj_hash.h"
 #include "phj_partition.h"
 
@@ -54,12 +56,22 @@ namespace phj {
 constexpr int kHtSegs = 16;             // build segments (ranks) per join
 constexpr uint32_t kHtBucketShift = 24; // home bucket = (c >> 24) & (buckets - 1): clear of every partition bit
 
-__host__ __device__ __forceinline__ uint32_t ht_cap(uint32_t m) {
-    // slots: the smallest power of two >= 1.5 m, at least one 2-slot bucket
-    const uint32_t want = m + (m + 1) / 2;
+__host__ __device__ __forceinline__ uint32_t ht_cap_for(uint32_t want) {
     uint32_t c = 2;
     while (c < want) c <<= 1;
     return c;
+}
+
+constexpr uint32_t kHtLcap = 512;    // k_ht_fill: LDS table slots per wave
+
+// Slots of a partition's table: the smallest power of two >= 2 m (load <=
+// 1/2) while that fits one wave's LDS slice, else >= 1.5 m (load <= 2/3); at
+// least one 2-slot bucket. Always < 4 m + 2 (the closed-form layout's bound).
+// Measured (C2): load <= 1/2 cuts the probe's walks (a full home bucket
+// without a match) from ~7 % to ~1-2 % of the keys, 0.86 -> 0.78 ms.
+__host__ __device__ __forceinline__ uint32_t ht_cap(uint32_t m) {
+    const uint32_t wide = ht_cap_for(2 * m);
+    return wide <= kHtLcap ? wide : ht_cap_for(m + (m + 1) / 2);
 }
 
 // E_p: e1 (a code outside partition 0) for partition 0, else code 0
@@ -165,7 +177,6 @@ __global__ __launch_bounds__(BLOCK) void k_scatter_codes(PassArgs a) {
 // the codes of kHtPpw consecutive partitions from every segment, each wave
 // builds a partition's table in its LDS slice and writes it out).
 // ---------------------------------------------------------------------------
-constexpr uint32_t kHtLcap = 512;    // k_ht_fill: LDS table slots per wave
 constexpr uint32_t kHtPpw = 8;       // k_ht_fill: partitions per workgroup (two per wave)
 
 // R pass 2 over one relation's pass-1 output (codes contiguous per d1).
@@ -460,6 +471,42 @@ __host__ __device__ constexpr size_t probe_ht_lds_bytes(int T, uint32_t nb) {
     return static_cast<size_t>(T + 2) * 8 + static_cast<size_t>(nb) * 2 * 12 + 64;
 }
 
+// Exclusive scan of nb digit counts C[0, nb) in place by one wave; returns the
+// total on every lane.
+__device__ __forceinline__ uint32_t wave_scan_counts(uint32_t* C, uint32_t nb, uint32_t lane) {
+    if (nb == 256) {   // the common 8-bit d2: one 16-B LDS read per lane
+        const uint4 q = reinterpret_cast<uint4*>(C)[lane];
+        const uint32_t local = q.x + q.y + q.z + q.w;
+        uint32_t x = local;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= static_cast<uint32_t>(o)) x += y;
+        }
+        const uint32_t r0 = x - local;
+        reinterpret_cast<uint4*>(C)[lane] = make_uint4(r0, r0 + q.x, r0 + q.x + q.y, r0 + q.x + q.y + q.z);
+        return __shfl(x, 63, 64);
+    }
+    const uint32_t per = (nb + 63) / 64, d0 = lane * per;
+    uint32_t local = 0;
+    for (uint32_t j = 0; j < per; j++)
+        if (d0 + j < nb) local += C[d0 + j];
+    uint32_t x = local;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= static_cast<uint32_t>(o)) x += y;
+    }
+    uint32_t run = x - local;
+    for (uint32_t j = 0; j < per; j++)
+        if (d0 + j < nb) {
+            const uint32_t c = C[d0 + j];
+            C[d0 + j] = run;
+            run += c;
+        }
+    return __shfl(x, 63, 64);
+}
+
 // FORM bit 0 (kProbeRadix): the radix digit of a code is a plain bit field,
 // d2 = (c >> shift) & dmask (no h % P, no sub-partition bits); bit 1
 // (kProbeChunked): the input is the chunked keys-only pass 1 (a code column,
@@ -510,10 +557,13 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
                 lo = L.lo;
                 c = L.hi - L.lo;
             }
+            // unconditional loads (clamped: a tile holds >= 1 code), no select
+            // on a loaded value
 #pragma unroll
             for (int i = 0; i < ITEMS; i++) {
                 const uint32_t e = wbase + i * 64 + lane;
-                key[i] = e < c ? (soa ? a.in_keys[lo + e] : rel[lo + e].x) : 0;
+                const uint32_t ix = lo + min(e, c - 1u);
+                key[i] = soa ? a.in_keys[ix] : rel[ix].x;
                 m |= e < c ? (1u << i) : 0u;
             }
         };
@@ -538,54 +588,25 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
                 rank[i] = agg_rank(C, dig[i], (vm >> i) & 1u);
             }
             __syncthreads();   // B1
+            uint32_t cnt;
+            uint32_t pos[ITEMS];
             if (wave == 0) {   // exclusive scan of the counts by one wave
-                if (nb == 256) {   // the common 8-bit d2: one 16-B LDS read per lane
-                    uint4 q = reinterpret_cast<uint4*>(C)[lane];
-                    const uint32_t local = q.x + q.y + q.z + q.w;
-                    uint32_t x = local;
-#pragma unroll
-                    for (int o = 1; o < 64; o <<= 1) {
-                        const uint32_t y = __shfl_up(x, o, 64);
-                        if (lane >= static_cast<uint32_t>(o)) x += y;
-                    }
-                    const uint32_t r0 = x - local;
-                    reinterpret_cast<uint4*>(C)[lane] = make_uint4(r0, r0 + q.x, r0 + q.x + q.y, r0 + q.x + q.y + q.z);
-                    if (lane == 63) tot_s = x;
-                } else {
-                    const uint32_t per = (nb + 63) / 64, d0 = lane * per;
-                    uint32_t local = 0;
-                    for (uint32_t j = 0; j < per; j++)
-                        if (d0 + j < nb) local += C[d0 + j];
-                    uint32_t x = local;
-#pragma unroll
-                    for (int o = 1; o < 64; o <<= 1) {
-                        const uint32_t y = __shfl_up(x, o, 64);
-                        if (lane >= static_cast<uint32_t>(o)) x += y;
-                    }
-                    uint32_t run = x - local;
-                    for (uint32_t j = 0; j < per; j++)
-                        if (d0 + j < nb) {
-                            const uint32_t c = C[d0 + j];
-                            C[d0 + j] = run;
-                            run += c;
-                        }
-                    if (lane == 63) tot_s = x;
-                }
+                const uint32_t t = wave_scan_counts(C, nb, lane);
+                if (lane == 0) tot_s = t;
             }
             __syncthreads();   // B2
-            const uint32_t cnt = tot_s;
-            {   // branch-free: the counter reads all go out before the writes
-                uint32_t pos[ITEMS];
+            cnt = tot_s;
 #pragma unroll
-                for (int i = 0; i < ITEMS; i++) pos[i] = C[dig[i]];
+            for (int i = 0; i < ITEMS; i++) pos[i] = C[dig[i]] + rank[i];
+
+            // branch-free: slot T takes invalid lanes' writes (a sink)
 #pragma unroll
-                for (int i = 0; i < ITEMS; i++) skey[((vm >> i) & 1u) ? pos[i] + rank[i] : static_cast<uint32_t>(T)] = key[i];   // slot T: a sink
-            }
+            for (int i = 0; i < ITEMS; i++) skey[((vm >> i) & 1u) ? pos[i] : static_cast<uint32_t>(T)] = key[i];
             const uint32_t next = tile + g8;
             const bool more = next < t_hi;
             uint32_t nvm = 0, nd1 = d1;
+            // the next tile's codes, counter row and descriptors
             if (more) load(next, nvm, nd1);
-            // the next tile's counter row and descriptors
             const uint32_t ob = buf ^ 1u;
             for (uint32_t d = tid; d < nb; d += BLOCK) cntb[ob * nb + d] = 0;
             if (more && sd[ob] != nd1) {
@@ -594,19 +615,15 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
             }
             __syncthreads();   // B3
             // probe: all items' home buckets in flight at once, then the walks
-            // of every item still pending advance together, one bucket a round
             const uint64_t e0 = d1 == 0 ? pa.e1 : 0ull;   // E of partition (d1, d2): e1 only for partition 0
             const ulonglong2* tab2 = reinterpret_cast<const ulonglong2*>(pa.table);
             ulonglong2 v[ITEMS];
 #pragma unroll
-            for (int i = 0; i < ITEMS; i++) {
+            for (int i = 0; i < ITEMS; i++) {   // unconditional: an unused lane reads code 0's bucket
                 const uint32_t k = i * BLOCK + tid;
-                v[i] = make_ulonglong2(0, 0);
-                if (k < cnt) {
-                    const uint64_t c = static_cast<uint64_t>(skey[k]);
-                    const uint2 ds = D[d2_of(c)];
-                    v[i] = tab2[(ds.x >> 1) + (static_cast<uint32_t>(c >> kHtBucketShift) & ds.y)];
-                }
+                const uint64_t c = k < cnt ? static_cast<uint64_t>(skey[k]) : 0ull;
+                const uint2 ds = D[d2_of(c)];
+                v[i] = tab2[(ds.x >> 1) + (static_cast<uint32_t>(c >> kHtBucketShift) & ds.y)];
             }
 #pragma unroll
             for (int i = 0; i < ITEMS; i++) {
@@ -691,48 +708,79 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
     const uint32_t tid = threadIdx.x;
     uint32_t hits = 0;
     const uint64_t step = static_cast<uint64_t>(gridDim.x) * 256 * ITEMS;
-    for (uint64_t base = static_cast<uint64_t>(blockIdx.x) * 256 * ITEMS; base < nS; base += step) {
-        uint64_t c[ITEMS];
+    // the probe loop is instantiated per layout: a descriptor load that the
+    // uniform layout does not need, speculated by the compiler, put a wait for
+    // every earlier load in front of each item's bucket read (the items' reads
+    // then went out one at a time)
+    auto run = [&](auto UNI) {
+        constexpr bool UNIFORM = decltype(UNI)::value;
+        for (uint64_t base = static_cast<uint64_t>(blockIdx.x) * 256 * ITEMS; base < nS; base += step) {
+            uint64_t c[ITEMS];
 #pragma unroll
-        for (int i = 0; i < ITEMS; i++) {   // S streams past the caches' allocate (it is read once)
-            const uint64_t ix = min(base + i * 256 + tid, nS - 1);
-            c[i] = static_cast<uint64_t>(__builtin_nontemporal_load(&S[ix].x));
-        }
-        uint32_t bb[ITEMS], bm[ITEMS], bk[ITEMS];
-        ulonglong2 v[ITEMS];
-#pragma unroll
-        for (int i = 0; i < ITEMS; i++) {
-            c[i] = hash64<HK>(c[i], seed);
-            const uint32_t p = static_cast<uint32_t>(c[i]) & (P - 1);
-            if (uniform) {
-                bb[i] = p * nbk;
-                bm[i] = nbk - 1;
-            } else {
-                const uint2 ds = desc[p];
-                bb[i] = ds.x >> 1;
-                bm[i] = ds.y;
+            for (int i = 0; i < ITEMS; i++) {   // S streams past the caches' allocate (it is read once)
+                const uint64_t ix = min(base + i * 256 + tid, nS - 1);
+                c[i] = static_cast<uint64_t>(__builtin_nontemporal_load(&S[ix].x));
             }
-            bk[i] = static_cast<uint32_t>(c[i] >> kHtBucketShift) & bm[i];
-            v[i] = tab2[bb[i] + bk[i]];
-        }
+            uint32_t bb[ITEMS], bm[ITEMS], bk[ITEMS];
+            ulonglong2 v[ITEMS];
+            if constexpr (!UNIFORM) {   // every descriptor requested before any bucket
+                uint2 ds[ITEMS];
 #pragma unroll
-        for (int i = 0; i < ITEMS; i++) {
-            if (base + i * 256 + tid < nS) {
-                const uint64_t e = ht_empty(static_cast<uint32_t>(c[i]) & (P - 1), e1);
-                bool hit = v[i].x == c[i] || v[i].y == c[i];
-                if (!hit && v[i].y != e) {   // home bucket full, no match: walk on
-                    uint32_t b = bk[i];
-                    for (;;) {
-                        b = (b + 1) & bm[i];
-                        const ulonglong2 w = tab2[bb[i] + b];
-                        hit = w.x == c[i] || w.y == c[i];
-                        if (hit || w.y == e) break;
-                    }
+                for (int i = 0; i < ITEMS; i++) {
+                    c[i] = hash64<HK>(c[i], seed);
+                    ds[i] = desc[static_cast<uint32_t>(c[i]) & (P - 1)];
                 }
-                hits += hit ? 1u : 0u;
+#pragma unroll
+                for (int i = 0; i < ITEMS; i++) {
+                    bb[i] = ds[i].x >> 1;
+                    bm[i] = ds[i].y;
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < ITEMS; i++) {
+                    c[i] = hash64<HK>(c[i], seed);
+                    bb[i] = (static_cast<uint32_t>(c[i]) & (P - 1)) * nbk;
+                    bm[i] = nbk - 1;
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < ITEMS; i++) {
+                bk[i] = static_cast<uint32_t>(c[i] >> kHtBucketShift) & bm[i];
+                v[i] = tab2[bb[i] + bk[i]];
+            }
+            // branch-free (a short-circuit || let the compiler split the last
+            // item's 16-B read into two dependent 8-B reads)
+            uint32_t pend = 0;   // bit i: item i's home bucket is full without a match
+#pragma unroll
+            for (int i = 0; i < ITEMS; i++) {
+                const uint32_t valid = base + i * 256 + tid < nS ? 1u : 0u;
+                const uint64_t e = ht_empty(static_cast<uint32_t>(c[i]) & (P - 1), e1);
+                const uint32_t hit = static_cast<uint32_t>(v[i].x == c[i]) | static_cast<uint32_t>(v[i].y == c[i]);
+                hits += hit & valid;
+                pend |= (valid & (hit ^ 1u) & static_cast<uint32_t>(v[i].y != e)) << i;
+            }
+            // the walks: every pending item's next bucket in flight at once (loads
+            // unconditional: a settled item re-reads its last bucket)
+            while (pend) {
+#pragma unroll
+                for (int i = 0; i < ITEMS; i++) {
+                    if ((pend >> i) & 1u) bk[i] = (bk[i] + 1) & bm[i];
+                    v[i] = tab2[bb[i] + bk[i]];
+                }
+#pragma unroll
+                for (int i = 0; i < ITEMS; i++) {
+                    const uint32_t pi = (pend >> i) & 1u;
+                    const uint64_t e = ht_empty(static_cast<uint32_t>(c[i]) & (P - 1), e1);
+                    const uint32_t hit = static_cast<uint32_t>(v[i].x == c[i]) | static_cast<uint32_t>(v[i].y == c[i]);
+                    const uint32_t done = pi & (hit | static_cast<uint32_t>(v[i].y == e));
+                    hits += done & hit;
+                    pend &= ~(done << i);
+                }
             }
         }
-    }
+    };
+    if (uniform) run(std::true_type{});
+    else run(std::false_type{});
     __shared__ uint32_t red[4];
     uint32_t x = hits;
 #pragma unroll

@@ -30,7 +30,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 FAMILIES = [
     (re.compile(r"^R\.p2\.scatter$"), re.compile(r"phj::k_ht_p2")),
     (re.compile(r"\.hist$"), re.compile(r"phj::k_hist")),
-    (re.compile(r"\.scatter$"), re.compile(r"phj::k_scatter")),
+    (re.compile(r"\.scatter$"), re.compile(r"phj::k_(scatter|chunk_codes)")),
     (re.compile(r"^build$"), re.compile(r"phj::k_(build_small|ht_fill|join_fused)")),
     (re.compile(r"^probe$"), re.compile(r"phj::k_(probe|join_fused)")),
     (re.compile(r"^np\.build$"), re.compile(r"phj::k_(np_build(?!_overflow)|ht_fill)")),

@@ -5,7 +5,7 @@ counter group, each a child process; run from a process that has not touched
 the GPU). Prints one JSON line per variant: {kernel: {counter: value}}.
 
   python scripts/pmc_kernel.py --config c4 --kernel np_probe \
-      --group TCC_HIT_sum,TCC_MISS_sum --variant PHJ_NP_HOT=0 --variant PHJ_NP_DIAG=2
+      --group TCC_HIT_sum,TCC_MISS_sum --variant PHJ_P1_WPC2=2 --variant PHJ_P1_WPC2=4
 """
 import argparse
 import json

@@ -127,7 +127,7 @@ def test_c1_nopartitioning_1m_16m(ctx):
 
 
 def test_full_size_probe_pass1_codes_match_oracle(ctx):
-    # the keys-only hash-code pass 1 (k_scatter_chunked VAR 13) that the
+    # the keys-only hash-code pass 1 (k_chunk_codes) that the
     # counting join consumes at full size, compared per pass-1 partition with
     # the oracle's stable partition of the same relation (the reference's
     # scatter, src/RadixCluster/HashJoin.hpp:394-412): bounds bit-exact, every

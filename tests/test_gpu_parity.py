@@ -410,13 +410,13 @@ def test_key_only_build_segments(params, env, monkeypatch):
             c.close()
 
 
-@pytest.mark.parametrize("region", ["0", "1"])
 @pytest.mark.parametrize("ratio", [0.0, 1.0])
-def test_nopart_region_build_overflow(region, ratio):
-    """NoPartitioning table built region by region in LDS (default) or with
-    device atomics (PHJ_NP_REGION=0): a key repeated 40K times fills its home
-    bucket's whole region and spills through the overflow list into the next
-    regions; the probe walks the same way. Both builds agree with the oracle."""
+def test_nopart_hot_build_key_overflow(ctx, ratio):
+    """A build key repeated 40K times: in the count's region code table it
+    fills one region's table far past its LDS slice (k_ht_fill's in-place
+    path); in the materialised join's 64-B bucket table, built region by
+    region in LDS, it spills through the overflow list into the next regions
+    and the probe walks the same way. Both agree with the oracle."""
     rng = np.random.default_rng(5)
     R = np.concatenate([np.full(40_000, 7, dtype=np.int64),
                         rng.integers(-200_000, 200_000, 300_000, dtype=np.int64)])
@@ -424,17 +424,9 @@ def test_nopart_region_build_overflow(region, ratio):
     S = rng.integers(-400_000, 400_000, 2_000_000, dtype=np.int64)
     S[::50] = 7
     expect = O.semijoin_count(O.as_relation(R), O.as_relation(S))
-    old = os.environ.get("PHJ_NP_REGION")
-    os.environ["PHJ_NP_REGION"] = region
-    try:
-        c = phj.Context(0)
-    finally:
-        if old is None:
-            del os.environ["PHJ_NP_REGION"]
-        else:
-            os.environ["PHJ_NP_REGION"] = old
-    with c:
-        c.upload(phj.SIDE_BUILD, O.as_relation(R))
-        c.upload(phj.SIDE_PROBE, O.as_relation(S))
-        for hk in (phj.HASH_XXH3, phj.HASH_MURMUR3):
-            assert c.join(phj.nopart_params(hash=hk, seed=SEED, table_ratio=ratio)).matches == expect
+    ctx.upload(phj.SIDE_BUILD, O.as_relation(R))
+    ctx.upload(phj.SIDE_PROBE, O.as_relation(S))
+    for hk in (phj.HASH_XXH3, phj.HASH_MURMUR3):
+        p = phj.nopart_params(hash=hk, seed=SEED, table_ratio=ratio)
+        assert ctx.join(p).matches == expect
+        assert ctx.join_materialize(p).matches == expect

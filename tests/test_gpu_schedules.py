@@ -3,21 +3,16 @@
 The tuning knobs (read from the environment when a context is created) pick
 between kernel schedules that must produce the same bytes: tile size
 (PHJ_TILE) and workgroup size (PHJ_BLOCK) of the histogram/scatter kernels,
-nontemporal stores (PHJ_NT), pass-1 output layout (PHJ_P1_AOS), the pass-2
-digit column (PHJ_DCOL), tile order
-(PHJ_XCD_REMAP), write-combining scatter (PHJ_WC, PHJ_WC_ITEMS, PHJ_WC_LW,
-PHJ_WC_WGS), the one-pass limit of hash % P (PHJ_ONEPASS_MAX), the join's
-sub-partitioning of large partitions (PHJ_SUBPART), the chunked pass 1 of
-unordered partitions (PHJ_P1_CHUNK) and its persistent workgroups per shard
-(PHJ_P1_SLOTS, PHJ_P1_WPC2), shard count (PHJ_P1_TPS, PHJ_P1_KO_TPS), size
-thresholds (PHJ_P1_MIN_TILES, PHJ_P1_KO_MIN_TILES) and tile ranking / LDS
-layout (PHJ_P1_VAR), the on-chip probe's input (PHJ_P2PROBE, PHJ_P1_KO,
-PHJ_P1_HCODE), fused LDS join vs HBM tables (PHJ_FUSED), the partitioned bucket
-tables vs CSR tables (PHJ_PTAB), the CSR probe schedule (PHJ_PROBE_WAVE,
-PHJ_PROBE_ITEMS) and the NoPartitioning probe (PHJ_NP_*). Every knob the
-context reads appears here (tests/test_tooling.py checks that). Each is
-checked against the oracle's stable partition (or, for the unordered layout,
-the same tuples in every partition) and semi-join count.
+nontemporal tuple loads (PHJ_NT_LOAD), the join's sub-partitioning of large
+partitions (PHJ_SUBPART), the chunked pass 1 of unordered partitions
+(PHJ_P1_CHUNK) and its persistent workgroups per shard (PHJ_P1_SLOTS,
+PHJ_P1_WPC2), shard count (PHJ_P1_TPS, PHJ_P1_KO_TPS) and size threshold
+(PHJ_P1_MIN_TILES), the on-chip probe (PHJ_P2PROBE), fused LDS join vs HBM
+tables (PHJ_FUSED), the partitioned bucket tables vs CSR tables (PHJ_PTAB) and
+the per-kernel timers (PHJ_TIMERS). Every knob the context reads appears here
+(tests/test_tooling.py checks that). Each is checked against the oracle's
+stable partition (or, for the unordered layout, the same tuples in every
+partition) and semi-join count.
 """
 import numpy as np
 import pytest
@@ -38,58 +33,24 @@ SCHEDULES = [
     {"PHJ_BLOCK": "512", "PHJ_TILE": "8192"},
     {"PHJ_BLOCK": "1024", "PHJ_TILE": "8192"},
     {"PHJ_BLOCK": "333"},                      # not compiled: falls back to 512 x 4096
-    {"PHJ_P1_AOS": "0"},
-    {"PHJ_P1_AOS": "0", "PHJ_DCOL": "0"},
-    {"PHJ_DCOL": "0"},
-    {"PHJ_XCD_REMAP": "0"},
-    {"PHJ_NT": "1"},
-    {"PHJ_WC": "1"},                                            # software write-combining scatter
-    {"PHJ_WC": "1", "PHJ_WC_ITEMS": "4", "PHJ_WC_LW": "16"},    # ... 4-item sub-tiles, 128-B lines
-    {"PHJ_WC": "1", "PHJ_WC_WGS": "64"},                        # ... few large super-tiles
-    {"PHJ_PROBE_ITEMS": "16", "PHJ_PROBE_WAVE": "0", "PHJ_FUSED": "0", "PHJ_PTAB": "0"},
-    {"PHJ_FUSED": "0", "PHJ_PTAB": "0", "PHJ_PROBE_WAVE": "0"},
-    {"PHJ_FUSED": "0", "PHJ_PTAB": "0", "PHJ_PROBE_WAVE": "2"},
     {"PHJ_FUSED": "0", "PHJ_PTAB": "0"},
     {"PHJ_FUSED": "0"},
     {"PHJ_FUSED": "0", "PHJ_PTAB": "2"},
-    {"PHJ_ONEPASS_MAX": "2048"},
     {"PHJ_SUBPART": "0"},
-    {"PHJ_R_AUX": "0"},
     {"PHJ_TIMERS": "0"},
-    {"PHJ_FUSED_KPL": "8"},
     {"PHJ_P1_CHUNK": "0"},                                      # on-chip probe over a stable pass 1 (raw keys)
     {"PHJ_P1_MIN_TILES": "0"},                                  # chunked pass 1 at every size
     {"PHJ_P1_MIN_TILES": "0", "PHJ_P1_SLOTS": "-1"},            # one tile per workgroup
     {"PHJ_P1_MIN_TILES": "0", "PHJ_P1_SLOTS": "3"},             # long persistent walks
     {"PHJ_P1_MIN_TILES": "0", "PHJ_P1_TPS": "4"},               # 16 shards on small relations
     {"PHJ_P1_MIN_TILES": "0", "PHJ_P1_TPS": "8", "PHJ_P1_SLOTS": "1"},  # 8 shards, one workgroup each
-    {"PHJ_FUSED_KPL": "2"},                                     # 2 S keys per lane, 6 waves/SIMD
     {"PHJ_NT_LOAD": "0"},                                       # no nontemporal tuple loads
     {"PHJ_NT_LOAD": "2", "PHJ_P1_MIN_TILES": "0"},              # nontemporal loads in both passes
-    # NoPartitioning: the count runs over region code tables by default
-    # (PHJ_NP_CT); PHJ_NP_CT=0 selects the 64-B key-bucket table, which the
-    # materialising join always uses, and its knobs
-    {"PHJ_NP_CT": "0"},                                         # NoPartitioning count over 64-B key buckets
-    {"PHJ_NP_CT": "0", "PHJ_NP_NT": "0"},                       # ... cached S loads
-    {"PHJ_NP_CT": "0", "PHJ_NP_NT": "2"},                       # ... nontemporal bucket loads too
-    {"PHJ_NP_CT": "0", "PHJ_NP_ITEMS": "8"},                    # ... 8 S keys per thread per round
-    {"PHJ_NP_CT": "0", "PHJ_NP_REGION": "0"},                   # ... device-atomic build
-    {"PHJ_NP_CT": "0", "PHJ_NP_HOT": "0"},                      # ... no hot-key LDS cache
-    {"PHJ_NP_CT": "0", "PHJ_NP_HOT_MIN": "0", "PHJ_NP_HOT_SAMPLES": "4096"},   # ... hot-key cache at every size
     {"PHJ_P2PROBE": "0"},                                       # radix: probe side's pass 2 through HBM
     {"PHJ_P2PROBE": "0", "PHJ_P1_MIN_TILES": "0"},              # ... after the chunked pass 1
     {"PHJ_P1_WPC2": "0"},                                       # keys-only pass 1 on every LDS slot
     {"PHJ_P1_WPC2": "1"},                                       # ... on half a workgroup per CU
-    {"PHJ_P1_HCODE": "0"},                                      # keys-only pass 1 writes raw keys (the probe hashes)
-    {"PHJ_P1_KO": "0", "PHJ_P1_MIN_TILES": "0"},                # chunked pass 1 writes whole tuples for the probe
     {"PHJ_P1_KO_TPS": "4"},                                     # keys-only pass 1: 16 shards on small relations
-    {"PHJ_P1_KO_MIN_TILES": "1000000"},                         # ... never chunked: stable pass 1 of tuples
-    {"PHJ_NP_CT": "0", "PHJ_NP_RATIO": "1.25"},                 # NoPartitioning 64-B bucket table ratio
-    {"PHJ_P1_MIN_TILES": "0", "PHJ_P1_VAR": "0"},               # chunked pass 1: stable ballot ranking
-    {"PHJ_P1_MIN_TILES": "0", "PHJ_P1_VAR": "1"},               # ... LDS-atomic ranking
-    {"PHJ_P1_MIN_TILES": "0", "PHJ_P1_VAR": "2"},               # ... tuple-wide LDS tile
-    {"PHJ_P1_MIN_TILES": "0", "PHJ_P1_VAR": "3"},               # ... both, packed write offsets
-    {"PHJ_P1_MIN_TILES": "0", "PHJ_P1_VAR": "3", "PHJ_BLOCK": "256", "PHJ_TILE": "4096"},  # ... 4 waves: no packing
 ]
 
 CASES = [((8, 8), 0, phj.HASH_MURMUR3), ((11, 0), 0, phj.HASH_XXH3), ((1, 0), 1000, phj.HASH_XXH3),
