@@ -96,8 +96,8 @@ struct SideState {
     DevBuf hist1, hist2, bounds1, tbase2, tseg2, bounds, partials;
     DevBuf dig;           // pass-2 digit column written by pass 1
     DevBuf ccur, ctab, tstart;   // chunked pass 1: digit cursors + pool counter, chunk table, pass-2 tile starts
-    DevBuf csink;                // ... code form: the void claims' / stores' sink words (never read)
-    uint32_t gen = 0;            // chunked pass 1: tag of the current chunk-table entries
+    DevBuf csink;                // ... code form: sink words of the stores past the tile (never read)
+    bool ctab_dirty = true;      // chunked pass 1: the chunk table may hold entries (clear before the next pass)
     bool hcoded = false;         // the last pass 1 wrote hash codes (keys only, PHJ_P1_HCODE)
     phj_partitioned view{};
     PassArgs p2{};               // p1_only: the pass-2 tile mapping over the pass-1 output
@@ -210,18 +210,23 @@ void free_buf(DevBuf& b) {
     b.bytes = 0;
 }
 
+hipEvent_t new_event() {
+    hipEvent_t e = nullptr;
+    // timing / same-device ordering only: no system-scope fence (a default
+    // event's system-scope writeback costs ~10 us per record); the first
+    // flag set the runtime accepts is used
+    const unsigned tries[3] = {hipEventDisableSystemFence, hipEventReleaseToDevice, hipEventDefault};
+    for (unsigned f : tries) {
+        if (hipEventCreateWithFlags(&e, f) == hipSuccess) break;
+        (void)hipGetLastError();
+        e = nullptr;
+    }
+    return e;
+}
+
 hipEvent_t next_event(phj_ctx* c) {
     if (c->evnext == c->evpool.size()) {
-        hipEvent_t e = nullptr;
-        // timing / same-device ordering only: no system-scope fence (a default
-        // event's system-scope writeback costs ~10 us per record); the first
-        // flag set the runtime accepts is used
-        const unsigned tries[3] = {hipEventDisableSystemFence, hipEventReleaseToDevice, hipEventDefault};
-        for (unsigned f : tries) {
-            if (hipEventCreateWithFlags(&e, f) == hipSuccess) break;
-            (void)hipGetLastError();
-            e = nullptr;
-        }
+        hipEvent_t e = new_event();
         if (!e) return nullptr;
         c->evpool.push_back(e);
     }
@@ -666,13 +671,14 @@ int partition_state(phj_ctx* c, SideState& S, const char* tag, const Plan& pl, b
         PHJ_TRY(ensure(c, S.ccur, chunk_state_bytes(pl.nb1)));
         if (ko) PHJ_TRY(ensure(c, S.csink, static_cast<size_t>(kSinkGroups) * tile_shape(c, pl.nb1).block * 8));
         PHJ_TRY(ensure(c, S.tstart, static_cast<size_t>(nt2max) * 8));   // tile_start, tile_cnt
-        // entries are tagged with the pass's generation: a fresh (zeroed, tag 0)
-        // table is never mistaken for a published chunk
+        // all zero between passes (kPublished): cleared when new, and when a
+        // pass that published entries never reached k_tile_chunks (an error)
         void* before = S.ctab.p;
         PHJ_TRY(ensure(c, S.ctab, static_cast<size_t>(nshards) * pl.nb1 * maxch * 8));
-        if (S.ctab.p != before) {
+        if (S.ctab.p != before) S.ctab_dirty = true;
+        if (S.ctab_dirty && !c->dry) {
             PHJ_HIP(c, hipMemsetAsync(S.ctab.p, 0, S.ctab.bytes, c->ks));
-            S.gen = 0;
+            S.ctab_dirty = false;
         }
     }
     if (c->dry) {   // scan scratch of both passes, then nothing is launched
@@ -708,11 +714,7 @@ int partition_state(phj_ctx* c, SideState& S, const char* tag, const Plan& pl, b
         a.maxch = maxch;
         a.pool_stride = pool_stride;
         a.nshards = nshards;
-        if (++S.gen == 0) {   // tags wrapped: clear the table (tag 0 is never published)
-            PHJ_HIP(c, hipMemsetAsync(S.ctab.p, 0, S.ctab.bytes, c->ks));
-            S.gen = 1;
-        }
-        a.gen = S.gen;
+        S.ctab_dirty = n > 0;   // until k_tile_chunks has cleared what pass 1 publishes
     }
     uint32_t* tb2 = pl.npass == 2 ? static_cast<uint32_t*>(S.tbase2.p) : nullptr;
     PHJ_TRY(launch_pass(c, pl.hk, true, p1_aos, a, nt1, std::string(tag) + ".p1", n, nt1 * pl.nb1));
@@ -747,9 +749,10 @@ int partition_state(phj_ctx* c, SideState& S, const char* tag, const Plan& pl, b
                 uint32_t* tc = ts + nt2max;
                 hipLaunchKernelGGL(k_tile_chunks, dim3((pl.nb1 * nshards + kWaves - 1) / kWaves), dim3(kBlock), 0, c->ks, tb2,
                                    static_cast<const uint32_t*>(S.ccur.p), pl.nb1, nshards,
-                                   static_cast<const unsigned long long*>(S.ctab.p), maxch, tile2,
+                                   static_cast<unsigned long long*>(S.ctab.p), maxch, tile2,
                                    static_cast<uint32_t*>(S.tseg2.p), ts, tc);
                 PHJ_LAUNCHED(c, "k_tile_chunks");
+                S.ctab_dirty = false;
                 b.tile_start = ts;
                 b.tile_cnt = tc;
             } else {   // stable layout: tile -> digit

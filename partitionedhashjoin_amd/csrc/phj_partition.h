@@ -84,6 +84,10 @@ __device__ __forceinline__ uint32_t digit_of(uint64_t key, const DigitFn& f) {
 // cursor line takes too many atomics, few enough that partial last chunks
 // stay a small share of the pass-2 tiles.
 constexpr uint32_t kShards = 16;
+// A published chunk-table entry (pool chunk ids start at 0). The table is all
+// zero between passes: k_tile_chunks clears every entry it reads, so no
+// per-pass tag has to reach the kernels (a captured step replays unchanged).
+constexpr unsigned long long kPublished = 1ull << 32;
 constexpr uint32_t kTilesPerShard = 3072;
 __host__ __device__ constexpr size_t chunk_pool_word(uint32_t nb, uint32_t x) { return (static_cast<size_t>(kShards) * nb + 31) / 32 * 32 + 32 * x; }
 __host__ __device__ constexpr size_t chunk_ticket_word(uint32_t nb, uint32_t x) { return chunk_pool_word(nb, kShards + x); }
@@ -112,7 +116,6 @@ struct PassArgs {
     void* out_dig;              // pass-1 scatter: writes the NEXT pass's digit per output slot
     const void* in_dig;         // pass-2 histogram: counts this column instead of hashing keys
     uint32_t dig2_mask;         // next pass's digit = q & dig2_mask
-    uint32_t gen;               // chunked pass 1: tag of this pass's chunk-table entries
     // Chunked pass 1 (no histogram pass): the output is a pool of T-tuple
     // chunks; every digit fills nshards chains of chunks (one per XCD, so the
     // atomic cursors and the chunks' partial lines stay in one L2), so a
@@ -123,14 +126,14 @@ struct PassArgs {
     // each), u64 hint per chain = max over its published chunks of
     // ((k + 1) << 32) | id
     uint32_t* chunk_cursor;
-    unsigned long long* chunk_tab;  // [kShards][nbins][maxch]: (gen << 32) | pool chunk id of a chain's k-th chunk
+    unsigned long long* chunk_tab;  // [kShards][nbins][maxch]: kPublished | pool chunk id of a chain's k-th chunk, 0 = not yet
     const uint32_t* tile_start; // segmented pass over a chunked input: first input slot of each tile ...
     const uint32_t* tile_cnt;   // ... and its tuple count
     uint32_t maxch;             // chunks of one chain (bound)
     uint32_t pool_stride;       // chunks of one shard's pool
     uint32_t nshards;           // chains per digit (<= kShards)
     uint32_t keys_only;         // chunked pass 1 for the counting probe: only the key column is written / read
-    unsigned long long* sink;   // k_chunk_codes: [grid][BLOCK] words the void claims / stores target (never read)
+    unsigned long long* sink;   // k_chunk_codes: [kSinkGroups][BLOCK] words the stores past the tile target (never read)
     DigitFn f;
 };
 
@@ -623,7 +626,6 @@ void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
     unsigned long long* hints = reinterpret_cast<unsigned long long*>(a.chunk_cursor + chunk_hint_word(nb)) + static_cast<size_t>(x) * nb;
     auto cur = [&](uint32_t d) { return curs + d; };
     auto hint_of = [&](uint32_t d) { return hints + d; };
-    const unsigned long long tag = static_cast<unsigned long long>(a.gen) << 32;
 
     // Every wave issues the same memory operations on every path (clamped
     // indices, zero adds) so the compiler's vmcnt bookkeeping stays exact and
@@ -750,7 +752,7 @@ void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
                 return x * a.pool_stride + 2 * per + atomicAdd(pool, 1u);
             };
             auto publish = [&](uint32_t k, uint32_t id) {
-                __hip_atomic_store(&tab[k], tag | id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&tab[k], kPublished | id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 atomicMax(hint_of(d), (static_cast<unsigned long long>(k + 1) << 32) | id);
             };
             uint32_t id0 = 0, id1 = 0;
@@ -767,7 +769,7 @@ void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
                     id0 = static_cast<uint32_t>(hint);
                 } else {
                     unsigned long long v;
-                    while (((v = __hip_atomic_load(&tab[k0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) != a.gen)
+                    while (((v = __hip_atomic_load(&tab[k0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) == 0)
                         __builtin_amdgcn_s_sleep(2);
                     id0 = static_cast<uint32_t>(v);
                 }
@@ -860,7 +862,6 @@ void k_chunk_codes(PassArgs a, uint32_t ntiles, uint32_t per) {
     uint32_t* curs = a.chunk_cursor + static_cast<size_t>(x) * nb;   // this shard's chains
     uint32_t* pool = a.chunk_cursor + chunk_pool_word(nb, x);
     unsigned long long* hints = reinterpret_cast<unsigned long long*>(a.chunk_cursor + chunk_hint_word(nb)) + static_cast<size_t>(x) * nb;
-    const unsigned long long tag = static_cast<unsigned long long>(a.gen) << 32;
     // a code's digit; pow2 = the plan's uniform power-of-two form (q = h & (P - 1),
     // no refinement), hoisted out of the per-element loops
     const bool pow2q = a.f.mode == 0 && a.f.sub_bits == 0;
@@ -961,7 +962,7 @@ void k_chunk_codes(PassArgs a, uint32_t ntiles, uint32_t per) {
                 return x * a.pool_stride + 2 * per + atomicAdd(pool, 1u);
             };
             auto publish = [&](uint32_t k, uint32_t id) {
-                __hip_atomic_store(&tab[k], tag | id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&tab[k], kPublished | id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 atomicMax(hints + d, (static_cast<unsigned long long>(k + 1) << 32) | id);
             };
             uint32_t id0 = 0, id1 = 0;
@@ -978,7 +979,7 @@ void k_chunk_codes(PassArgs a, uint32_t ntiles, uint32_t per) {
                     id0 = static_cast<uint32_t>(hint);
                 } else {
                     unsigned long long v;
-                    while (((v = __hip_atomic_load(&tab[k0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) != a.gen)
+                    while (((v = __hip_atomic_load(&tab[k0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) == 0)
                         __builtin_amdgcn_s_sleep(2);
                     id0 = static_cast<uint32_t>(v);
                 }
@@ -1189,7 +1190,7 @@ __global__ __launch_bounds__(kBlock) void k_tile_seg(const uint32_t* tile_base, 
 // the chain's chunks.
 __global__ __launch_bounds__(kBlock) void k_tile_chunks(const uint32_t* tile_base, const uint32_t* sizes,
                                                         uint32_t nseg, uint32_t nshards,
-                                                        const unsigned long long* chunk_tab, uint32_t maxch,
+                                                        unsigned long long* chunk_tab, uint32_t maxch,
                                                         uint32_t T, uint32_t* tile_seg, uint32_t* tile_start,
                                                         uint32_t* tile_cnt) {
     const uint32_t w = blockIdx.x * kWaves + (threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -1201,11 +1202,12 @@ __global__ __launch_bounds__(kBlock) void k_tile_chunks(const uint32_t* tile_bas
     for (int o = 32; o > 0; o >>= 1) before += __shfl_xor(before, o, 64);
     const uint32_t szx = sizes[x * nseg + s], nch = (szx + T - 1) / T;
     const uint32_t t0 = tile_base[s] + before;
-    const unsigned long long* tab = chunk_tab + (static_cast<size_t>(x) * nseg + s) * maxch;
+    unsigned long long* tab = chunk_tab + (static_cast<size_t>(x) * nseg + s) * maxch;
     for (uint32_t k = lane; k < nch; k += 64) {
         tile_seg[t0 + k] = s;
         tile_start[t0 + k] = static_cast<uint32_t>(tab[k]) * T;
         tile_cnt[t0 + k] = min(T, szx - k * T);
+        tab[k] = 0;   // the next pass starts from an all-zero table (kPublished)
     }
 }
 
