@@ -563,7 +563,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
             for (int i = 0; i < ITEMS; i++) {
                 const uint32_t e = wbase + i * 64 + lane;
                 const uint32_t ix = lo + min(e, c - 1u);
-                key[i] = soa ? a.in_keys[ix] : rel[ix].x;
+                // nontemporal: the code stream (read once) does not displace
+                // the d1 tables the XCD's L2 holds for the probes
+                key[i] = soa ? __builtin_nontemporal_load(a.in_keys + ix) : __builtin_nontemporal_load(&rel[ix].x);
                 m |= e < c ? (1u << i) : 0u;
             }
         };
