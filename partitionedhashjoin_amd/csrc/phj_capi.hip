@@ -487,6 +487,7 @@ int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const st
             const uint32_t per = (ntiles + a.nshards - 1) / a.nshards;
             const size_t lds = a.keys_only ? chunk_codes_lds_bytes(T, a.nbins) : sc_lds;
             const void* kfn = nullptr;
+            const int kblock = BLOCK;
             // keys only, written as hash codes (the on-chip probe): k_chunk_codes;
             // whole tuples: VAR 3, LDS-atomic ranking, 16-B LDS entries (phj_partition.h)
             if (a.keys_only)
@@ -503,7 +504,7 @@ int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const st
             if (hit != occ_cache.end() && hit->second.first == lds) {
                 occ = hit->second.second;
             } else {
-                if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kfn, BLOCK, lds) != hipSuccess || occ < 1) occ = 1;
+                if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kfn, kblock, lds) != hipSuccess || occ < 1) occ = 1;
                 occ_cache[kfn] = {lds, occ};
             }
             const uint32_t fit = std::max<uint32_t>(1, std::min<uint32_t>(static_cast<uint32_t>(occ), static_cast<uint32_t>(160 * 1024 / lds)));
@@ -519,7 +520,7 @@ int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const st
             if (c->tune.p1_slots < 0) slots = per;   // one tile per workgroup
             PassArgs ak = a;
             void* kargs[] = {&ak, const_cast<uint32_t*>(&ntiles), const_cast<uint32_t*>(&per)};
-            PHJ_HIP(c, hipLaunchKernel(kfn, dim3(slots * a.nshards), dim3(BLOCK), kargs, lds, c->ks));
+            PHJ_HIP(c, hipLaunchKernel(kfn, dim3(slots * a.nshards), dim3(kblock), kargs, lds, c->ks));
             PHJ_LAUNCHED(c, sname);
         } else {
             (void)grid;
@@ -673,9 +674,10 @@ int partition_state(phj_ctx* c, SideState& S, const char* tag, const Plan& pl, b
         PHJ_TRY(ensure(c, S.tstart, static_cast<size_t>(nt2max) * 8));   // tile_start, tile_cnt
         // all zero between passes (kPublished): cleared when new, and when a
         // pass that published entries never reached k_tile_chunks (an error)
-        void* before = S.ctab.p;
+        // (a reallocation can return the same address: compare the size)
+        const size_t before = S.ctab.bytes;
         PHJ_TRY(ensure(c, S.ctab, static_cast<size_t>(nshards) * pl.nb1 * maxch * 8));
-        if (S.ctab.p != before) S.ctab_dirty = true;
+        if (S.ctab.bytes != before) S.ctab_dirty = true;
         if (S.ctab_dirty && !c->dry) {
             PHJ_HIP(c, hipMemsetAsync(S.ctab.p, 0, S.ctab.bytes, c->ks));
             S.ctab_dirty = false;

@@ -314,6 +314,7 @@ __device__ __forceinline__ void store_next_digit(const PassArgs& a, uint32_t o, 
 // Per-tile digit histogram -> hist[(tb_s * nbins) + d * ntiles_s + tseg].
 template <int BLOCK, int ITEMS, bool AOS, int HK>
 __global__ __launch_bounds__(BLOCK) void k_hist(PassArgs a) {
+    __builtin_amdgcn_s_setprio(3);   // (R's chain beside S's persistent pass 1: issue first)
     constexpr int NW = BLOCK / 64;
     constexpr int T = BLOCK * ITEMS;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];

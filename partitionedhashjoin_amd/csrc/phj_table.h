@@ -95,6 +95,7 @@ __host__ __device__ constexpr size_t scatter_codes_lds_bytes(int T, uint32_t nb)
 
 template <int BLOCK, int ITEMS, int HK>
 __global__ __launch_bounds__(BLOCK) void k_scatter_codes(PassArgs a) {
+    __builtin_amdgcn_s_setprio(3);   // R's chain: issue ahead of the persistent S pass 1 sharing the SIMD
     constexpr int T = BLOCK * ITEMS;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t nb = a.nbins;
@@ -205,6 +206,7 @@ __host__ __device__ constexpr size_t ht_p2_lds_bytes(uint32_t nb2, bool keep) {
 
 template <bool KEEP>
 __global__ __launch_bounds__(kHtP2Block) void k_ht_p2(HtPass2Args a) {
+    __builtin_amdgcn_s_setprio(3);   // R's chain: issue ahead of the persistent S pass 1 sharing the SIMD
     constexpr uint32_t B = kHtP2Block, U = kHtP2Items;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint32_t* cnt = reinterpret_cast<uint32_t*>(smem);                 // [nb2] counts
@@ -317,6 +319,7 @@ __device__ __forceinline__ void ht_insert(uint64_t* tab, uint32_t bmask, uint64_
 // counts them.
 template <bool ONE>   // ONE: a single build segment (one device): element r is at codes[0] + start + r
 __global__ __launch_bounds__(256) void k_ht_fill(HtArgs a) {
+    __builtin_amdgcn_s_setprio(3);   // R's chain: issue ahead of the persistent S pass 1 sharing the SIMD
     // codes per lane: a partition that fits the slice at load <= 0.8 (the
     // uniform layout's bound; the radix layout's caps keep it <= 2/3)
     constexpr uint32_t CPL = kHtLcap * 4 / 5 / 64 + 1;
