@@ -152,6 +152,7 @@ struct phj_ctx {
     hipEvent_t last_ev = nullptr;      // the last event recorded (mark) ...
     hipStream_t last_ev_stream = nullptr;  // ... on this stream ...
     uint32_t since_ev = 0;             // ... and the kernels launched since
+    unsigned long long* count_host = nullptr;   // pinned: the count read back
 };
 
 namespace {
@@ -1190,11 +1191,18 @@ int probe_ht(phj_ctx* c, const Plan& pl, SideState& PS, bool clear = true) {
     return PHJ_OK;
 }
 
+// The count comes back through a pinned host word (a pageable destination is
+// staged by the runtime: a slower copy on the step's critical path).
 int get_count(phj_ctx* c, uint64_t* out) {
+    if (!c->count_host && hipHostMalloc(reinterpret_cast<void**>(&c->count_host), 16, hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        c->count_host = nullptr;
+    }
     unsigned long long h = 0;
-    PHJ_HIP(c, hipMemcpyAsync(&h, c->count.p, 8, hipMemcpyDeviceToHost, c->ks));
+    unsigned long long* dst = c->count_host ? c->count_host : &h;
+    PHJ_HIP(c, hipMemcpyAsync(dst, c->count.p, 8, hipMemcpyDeviceToHost, c->ks));
     PHJ_HIP(c, hipStreamSynchronize(c->ks));
-    *out = h;
+    *out = *dst;
     return PHJ_OK;
 }
 
@@ -1639,6 +1647,7 @@ void phj_ctx_destroy(phj_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     (void)hipStreamSynchronize(c->aux);
+    if (c->count_host) (void)hipHostFree(c->count_host);
     for (SideState& S : c->side) {
         for (DevBuf* b : {&S.owned, &S.kA, &S.pA, &S.kB, &S.pB, &S.hist1, &S.hist2, &S.bounds1, &S.tbase2,
                           &S.bounds, &S.partials, &S.tseg2, &S.dig, &S.ccur, &S.ctab, &S.tstart, &S.csink})

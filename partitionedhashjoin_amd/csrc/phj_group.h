@@ -385,7 +385,12 @@ int allreduce_count(Group& G, int i, const void* local_count, bool failed = fals
 
 int read_count(Group& G, int i, uint64_t* out) {
     phj_ctx* c = G.mem[i];
-    unsigned long long h[2] = {0, 0};
+    if (!c->count_host && hipHostMalloc(reinterpret_cast<void**>(&c->count_host), 16, hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        c->count_host = nullptr;
+    }
+    unsigned long long hs[2] = {0, 0};
+    unsigned long long* h = c->count_host ? c->count_host : hs;   // pinned when it could be allocated
     PHJ_HIP(c, hipMemcpyAsync(h, G.buf[i].cnt.p, 16, hipMemcpyDeviceToHost, c->ks));
     PHJ_HIP(c, hipStreamSynchronize(c->ks));
     if (G.kind == Xchg::kLocal) {
