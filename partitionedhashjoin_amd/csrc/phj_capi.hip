@@ -610,7 +610,8 @@ int launch_pass(phj_ctx* c, int hk, bool in_aos, bool out_aos, PassArgs a, uint3
 #undef PHJ_PASS_CASES
 }
 
-int partition_state(phj_ctx* c, SideState& S, const char* tag, const Plan& pl, bool p1_only) {
+int partition_state(phj_ctx* c, SideState& S, const char* tag, const Plan& pl, bool p1_only,
+                    unsigned long long* zero = nullptr) {
     c->scan_scratch = &S.partials;
     if (!S.rel && S.n > 0) return set_err(c, PHJ_ERR_STATE, "relation not bound");
     const uint64_t n64 = S.n;
@@ -723,7 +724,7 @@ int partition_state(phj_ctx* c, SideState& S, const char* tag, const Plan& pl, b
     PHJ_TRY(launch_pass(c, pl.hk, true, p1_aos, a, nt1, std::string(tag) + ".p1", n, nt1 * pl.nb1));
     if (chunked) {
         hipLaunchKernelGGL(k_pass1_finish_sizes, dim3(1), dim3(kFinBlock), 0, c->ks, a.chunk_cursor, pl.nb1, nshards, n, tile2,
-                           static_cast<uint32_t*>(S.bounds1.p), tb2);
+                           static_cast<uint32_t*>(S.bounds1.p), tb2, zero);
         PHJ_LAUNCHED(c, "k_pass1_finish_sizes");
     } else {
         hipLaunchKernelGGL(k_pass1_finish, dim3(1), dim3(kFinBlock), 0, c->ks, a.hist, nt1, pl.nb1, n,
@@ -798,8 +799,10 @@ int partition_state(phj_ctx* c, SideState& S, const char* tag, const Plan& pl, b
     return PHJ_OK;
 }
 
-int partition_side(phj_ctx* c, int s, const Plan& pl, bool p1_only = false) {
-    return partition_state(c, c->side[s], s == PHJ_SIDE_BUILD ? "R" : "S", pl, p1_only);
+// zero: a word the pass-1 bookkeeping clears (the on-chip probe's count),
+// or null
+int partition_side(phj_ctx* c, int s, const Plan& pl, bool p1_only = false, unsigned long long* zero = nullptr) {
+    return partition_state(c, c->side[s], s == PHJ_SIDE_BUILD ? "R" : "S", pl, p1_only, zero);
 }
 
 // Build over `nseg` partitioned build segments and probe the ctx's partitioned
@@ -1926,9 +1929,11 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
         // issued first, or run before S with S's pass 1 on every LDS slot, is
         // 0.05-0.1 ms slower; probing S in row ranges, each beside the next
         // range's pass 1, is 0.3 ms slower: DESIGN.md section 3)
+        PHJ_TRY(ensure(c, c->count, 16));
         PHJ_TRY(mark(c, &t0));
         PHJ_HIP(c, hipStreamWaitEvent(c->aux, t0, 0));
-        PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, pl, true));
+        // the code pass's bookkeeping kernel clears the count (hcoded)
+        PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, pl, true, static_cast<unsigned long long*>(c->count.p)));
         c->ks = c->aux;
         int rc = ensure(c, c->r_codes, std::max<uint64_t>(1, R.n) * 8);
         if (rc == PHJ_OK) rc = ensure(c, c->r_bounds, (static_cast<size_t>(pl.Ppad) + 1) * 4);
@@ -1948,7 +1953,7 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
         // algorithmic bytes: the pass-1 output read once (16-B tuples, or 8-B
         // codes after a keys-only pass 1); the tables are re-read from L2
         PHJ_TRY(timer_begin(c, "probe", S.n * (S.p2.keys_only ? 8 : 16)));
-        PHJ_TRY(probe_ht(c, pl, S));
+        PHJ_TRY(probe_ht(c, pl, S, !S.hcoded));
         PHJ_TRY(timer_end(c));
         PHJ_TRY(mark(c, &p1));
         uint64_t m = 0;

@@ -521,9 +521,11 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
     const bool s_early = !(G.rehearse && i > 0);
     if (rc == PHJ_OK && s_early) {
         c->ks = c->stream;
-        rc = partition_side(c, PHJ_SIDE_PROBE, pl, p2);
-        if (rc == PHJ_OK && p2) rc = ensure(c, c->count, 16);
-        if (rc == PHJ_OK && p2 && hipMemsetAsync(c->count.p, 0, 8, c->stream) != hipSuccess)
+        if (p2) rc = ensure(c, c->count, 16);
+        // the code pass's bookkeeping kernel clears the count (hcoded); else a memset
+        if (rc == PHJ_OK)
+            rc = partition_side(c, PHJ_SIDE_PROBE, pl, p2, p2 ? static_cast<unsigned long long*>(c->count.p) : nullptr);
+        if (rc == PHJ_OK && p2 && !c->side[PHJ_SIDE_PROBE].hcoded && hipMemsetAsync(c->count.p, 0, 8, c->stream) != hipSuccess)
             rc = set_err(c, PHJ_ERR_HIP, "count reset");
         if (rc == PHJ_OK && p2) rc = mark(c, &sdone);
         c->ks = c->aux;

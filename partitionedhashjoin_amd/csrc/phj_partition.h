@@ -1214,12 +1214,14 @@ __global__ __launch_bounds__(kBlock) void k_tile_chunks(const uint32_t* tile_bas
 
 // After a chunked pass 1: bounds1 = exclusive scan of the digit sizes (summed
 // over the shards: the segments' offsets in the pass-2 output) and
-// tile_base2 = exclusive scan of their chunk counts. One workgroup.
+// tile_base2 = exclusive scan of their chunk counts; `zero` (may be null) is
+// cleared. One workgroup.
 __global__ __launch_bounds__(kFinBlock) void k_pass1_finish_sizes(const uint32_t* sizes, uint32_t nb, uint32_t nshards,
                                                                   uint32_t n, uint32_t T, uint32_t* bounds1,
-                                                                  uint32_t* tile_base2) {
+                                                                  uint32_t* tile_base2, unsigned long long* zero) {
     __shared__ uint32_t wsum[2][kFinBlock / 64];
     const uint32_t tid = threadIdx.x;
+    if (zero && tid == 0) *zero = 0;   // the on-chip probe's count (one launch fewer before it)
     uint32_t cx = 0, cy = 0;
     for (uint32_t base = 0; base < nb; base += kFinBlock) {
         const uint32_t d = base + tid;
