@@ -98,7 +98,7 @@ struct SideState {
     DevBuf ccur, ctab, tstart;   // chunked pass 1: digit cursors + pool counter, chunk table, pass-2 tile starts
     DevBuf csink;                // ... code form: sink words of the stores past the tile (never read)
     bool ctab_dirty = true;      // chunked pass 1: the chunk table may hold entries (clear before the next pass)
-    bool hcoded = false;         // the last pass 1 wrote hash codes (keys only, PHJ_P1_HCODE)
+    bool hcoded = false;         // the last pass 1 wrote hash codes (keys only, k_chunk_codes)
     phj_partitioned view{};
     PassArgs p2{};               // p1_only: the pass-2 tile mapping over the pass-1 output
     uint32_t nt2 = 0;            // ... and its tile bound
@@ -646,7 +646,7 @@ int partition_state(phj_ctx* c, SideState& S, const char* tag, const Plan& pl, b
     const uint32_t tps = static_cast<uint32_t>(ko ? c->tune.p1_ko_tps : c->tune.p1_tps);
     while (nshards < kShards && static_cast<uint64_t>(nshards) * tps < nt1) nshards <<= 1;
     // pool of pass-1 chunks, one region per shard: a shard takes at most
-    // `per` tiles, each with two chunks reserved up front (k_scatter_chunked;
+    // `per` tiles, each with two chunks reserved up front (k_scatter_chunked, k_chunk_codes;
     // unused ones are never touched), then at most per + nb1 chunks for its
     // chains' other starts (each chain wastes at most one partial chunk)
     const uint32_t per = (nt1 + nshards - 1) / nshards;
@@ -1174,7 +1174,7 @@ int probe_ht(phj_ctx* c, const Plan& pl, SideState& PS, bool clear = true) {
     pa.nb2 = pl.nb2;
     constexpr int B = kProbeBlock, I = kProbeItems;
     const size_t lds = probe_ht_lds_bytes(B * I, pl.nb2);
-    // a keys-only pass 1 wrote codes (VAR 13); a stable pass 1 left whole tuples
+    // a keys-only pass 1 wrote codes (k_chunk_codes); a stable pass 1 left whole tuples
     // (the chunked pass-1 output is always codes; a radix plan's d2 is a bit field)
     const bool radix = pl.mode == 0 && pl.sub_bits == 0;
     const void* kfn = PS.hcoded ? (radix ? reinterpret_cast<const void*>(&k_probe_ht<B, I, kHashed, kProbeRadix | kProbeChunked>)

@@ -454,7 +454,7 @@ __global__ __launch_bounds__(256) void k_ht_fill(HtArgs a) {
 // Counters and descriptors are double-buffered, so the next tile's ranking may
 // start while slower waves still probe this one (its scatter waits behind the
 // next B1 / B2, which every wave reaches only after its probe).
-// HK = kHashed when the pass-1 output holds codes (VAR 13), else the key is
+// HK = kHashed when the pass-1 output holds codes (k_chunk_codes), else the key is
 // hashed here (a stable pass 1 of whole tuples).
 // ---------------------------------------------------------------------------
 struct HtProbeArgs {
