@@ -1931,9 +1931,11 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
         // range's pass 1, is 0.3 ms slower: DESIGN.md section 3)
         PHJ_TRY(ensure(c, c->count, 16));
         PHJ_TRY(mark(c, &t0));
-        PHJ_HIP(c, hipStreamWaitEvent(c->aux, t0, 0));
         // the code pass's bookkeeping kernel clears the count (hcoded)
         PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, pl, true, static_cast<unsigned long long*>(c->count.p)));
+        // R's chain waits for t0 (the previous step's probe read its tables);
+        // the wait is issued after S's pass 1 so that launch goes out first
+        PHJ_HIP(c, hipStreamWaitEvent(c->aux, t0, 0));
         c->ks = c->aux;
         int rc = ensure(c, c->r_codes, std::max<uint64_t>(1, R.n) * 8);
         if (rc == PHJ_OK) rc = ensure(c, c->r_bounds, (static_cast<size_t>(pl.Ppad) + 1) * 4);

@@ -496,7 +496,6 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
         rc = member_alloc_radix(G, i, pl, p2);
     }
     if (rc == PHJ_OK) rc = mark(c, &t0);
-    if (rc == PHJ_OK && hipStreamWaitEvent(c->aux, t0, 0) != hipSuccess) rc = set_err(c, PHJ_ERR_HIP, "wait t0");
     // R shard, pack and all-gather on the aux stream (S goes beside them);
     // a rehearsal's members > 0 pack their (unchanging) block once and from
     // then on only take part in the exchange, so member 0 has the GPU
@@ -530,6 +529,9 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
         if (rc == PHJ_OK && p2) rc = mark(c, &sdone);
         c->ks = c->aux;
     }
+    // R's chain (aux) waits for t0: the previous step's probe read its tables
+    // and exchange block (issued after S's pass 1, so that launch goes out first)
+    if (rc == PHJ_OK && hipStreamWaitEvent(c->aux, t0, 0) != hipSuccess) rc = set_err(c, PHJ_ERR_HIP, "wait t0");
     if (p2) {   // the R shard as codes in partition order, straight into the exchange block
         if (rc == PHJ_OK)
             rc = partition_build(c, pl, static_cast<int64_t*>(B.send.p),
