@@ -1,15 +1,10 @@
-#!/bin/bash
-# A/B the per-rank W rehearsal over tuning environments: scripts/ab_rehearse.sh "8" "ENV=.." "ENV=.." ...
 set -o pipefail
-mkdir -p gpurun_out
-worlds=$1; shift
-for v in "$@"; do
-  env $v timeout -k 10 200 python scripts/rehearse_world.py --worlds $worlds > gpurun_out/abr.jsonl 2> gpurun_out/abr.err || { echo "$v failed"; tail -5 gpurun_out/abr.err; exit 3; }
-  python - "$v" <<'PY'
-import json, sys
-for l in open("gpurun_out/abr.jsonl"):
-    d = json.loads(l); k = d["kernels_ms"]
-    print(f"{sys.argv[1] or 'default':24s} W={d['world']} {d['ms_per_step']:.4f} ms " +
-          " ".join(f"{n}={k[n]:.3f}" for n in k if n.startswith("S.")))
-PY
+cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests/test_gpu_multirank.py tests/test_gpu_fullsize_group.py -x -q --timeout 300 --timeout-method thread > gpurun_out/reh_tests.log 2>&1 || { echo tests failed; tail -20 gpurun_out/reh_tests.log; exit 1; }
+tail -2 gpurun_out/reh_tests.log
+for k in 1 2; do
+  PHJ_LIB=partitionedhashjoin_amd/libphj_hip_prev.so timeout -k 10 200 python scripts/rehearse_world.py --worlds 8 4 > gpurun_out/reh_prev$k.jsonl 2>/dev/null || exit 2
+  echo prev; cut -c1-90 gpurun_out/reh_prev$k.jsonl
+  timeout -k 10 200 python scripts/rehearse_world.py --worlds 8 4 > gpurun_out/reh_new$k.jsonl 2>/dev/null || exit 3
+  echo new; cut -c1-90 gpurun_out/reh_new$k.jsonl
 done
