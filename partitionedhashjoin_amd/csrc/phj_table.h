@@ -516,6 +516,9 @@ __device__ __forceinline__ uint32_t wave_scan_counts(uint32_t* C, uint32_t nb, u
 // tile t = chunk [tile_start[t], + tile_cnt[t])). Both drop the run-time mode
 // branches and the kernel-argument state they keep live.
 constexpr int kProbeRadix = 1, kProbeChunked = 2;
+#ifndef PHJ_PROBE_ABL
+#define PHJ_PROBE_ABL 0   // measurement builds only: 1 = no table reads, 2 = no d2 grouping
+#endif
 
 template <int BLOCK, int ITEMS, int HK, int FORM = 0>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void k_probe_ht(HtProbeArgs pa) {
@@ -590,11 +593,21 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
                 const uint64_t h = hash64<HK>(static_cast<uint64_t>(key[i]), pa.seed);
                 key[i] = static_cast<int64_t>(h);
                 dig[i] = d2_of(h);
-                rank[i] = agg_rank(C, dig[i], (vm >> i) & 1u);
+                if constexpr (PHJ_PROBE_ABL == 2) rank[i] = wbase + i * 64 + lane;
+                else rank[i] = agg_rank(C, dig[i], (vm >> i) & 1u);
             }
             __syncthreads();   // B1
             uint32_t cnt;
             uint32_t pos[ITEMS];
+            if constexpr (PHJ_PROBE_ABL == 2) {   // tile order: the valid codes are a prefix
+                if (tid == 0) tot_s = 0;
+                __syncthreads();
+                if (vm) atomicMax(&tot_s, wbase + (31 - __builtin_clz(vm)) * 64 + lane + 1);
+                __syncthreads();
+                cnt = tot_s;
+#pragma unroll
+                for (int i = 0; i < ITEMS; i++) pos[i] = rank[i];
+            } else {
             if (wave == 0) {   // exclusive scan of the counts by one wave
                 const uint32_t t = wave_scan_counts(C, nb, lane);
                 if (lane == 0) tot_s = t;
@@ -603,6 +616,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
             cnt = tot_s;
 #pragma unroll
             for (int i = 0; i < ITEMS; i++) pos[i] = C[dig[i]] + rank[i];
+            }
 
             // branch-free: slot T takes invalid lanes' writes (a sink)
 #pragma unroll
@@ -623,6 +637,14 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
             const uint64_t e0 = d1 == 0 ? pa.e1 : 0ull;   // E of partition (d1, d2): e1 only for partition 0
             const ulonglong2* tab2 = reinterpret_cast<const ulonglong2*>(pa.table);
             ulonglong2 v[ITEMS];
+            if constexpr (PHJ_PROBE_ABL == 1) {
+#pragma unroll
+                for (int i = 0; i < ITEMS; i++) {
+                    const uint32_t k = i * BLOCK + tid;
+                    const uint64_t c = k < cnt ? static_cast<uint64_t>(skey[k]) : 0ull;
+                    hits += (k < cnt && D[d2_of(c)].y != 0xdeadbeefu) ? 1u : 0u;
+                }
+            } else {
 #pragma unroll
             for (int i = 0; i < ITEMS; i++) {   // unconditional: an unused lane reads code 0's bucket
                 const uint32_t k = i * BLOCK + tid;
@@ -650,6 +672,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
                     }
                     hits += hit ? 1u : 0u;
                 }
+            }
             }
             if (!more) break;
             tile = next;

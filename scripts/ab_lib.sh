@@ -1,0 +1,10 @@
+#!/bin/bash
+# A/B the C2 bench over library builds: scripts/ab_lib.sh LIB1 LIB2 ... (e.g. measurement builds with -DPHJ_PROBE_ABL=N)
+set -o pipefail
+mkdir -p gpurun_out
+i=0
+for lib in "$@"; do
+  i=$((i+1))
+  PHJ_LIB=$lib timeout -k 10 150 python bench.py --no-cpu-baseline --no-traffic --verbose > gpurun_out/abl_$i.json 2> gpurun_out/abl_$i.err || { echo "$lib failed"; tail -5 gpurun_out/abl_$i.err; exit 9; }
+  python -c "import json,sys; d=json.load(open('gpurun_out/abl_$i.json')); k=d['kernels_ms']; print('$lib', round(d['ms_per_step'],3), d['correct'], {n: round(v,3) for n,v in k.items()})"
+done
