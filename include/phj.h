@@ -297,6 +297,16 @@ int phj_hash_keys(phj_ctx *ctx, int hash, uint64_t seed, const int64_t *keys, ui
 int phj_probe_pass1(phj_ctx *ctx, const phj_join_params *p, int64_t *keys, uint64_t n, uint32_t *bounds1,
                     uint32_t *nb1, int *codes);
 
+/* ---- test hook: a stale chunk table ----
+ * Replaces nothing in the reference. Fills the chunk table of `side`'s chunked
+ * pass 1 (the one the last chunked pass on that side used; if there is none
+ * yet, the one phj_join with params p would use) with `byte` and marks it
+ * clean, as a table left stale by an earlier pass would be. The chunked passes bound-check every
+ * chunk id and chain index they read back, so the next join returns
+ * PHJ_ERR_STATE (nothing is written through a stale entry) and clears the
+ * table; the join after it is exact again. Single-device ctx. */
+int phj_debug_poison_chunk_table(phj_ctx *ctx, int side, const phj_join_params *p, int byte);
+
 #ifdef __cplusplus
 }
 #endif

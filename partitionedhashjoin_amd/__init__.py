@@ -284,6 +284,11 @@ class Context:
                                             b1.ctypes.data_as(C.c_void_p), C.byref(nb1), C.byref(codes)))
         return out, b1[:nb1.value + 1].copy(), bool(codes.value)
 
+    def debug_poison_chunk_table(self, side: int, params: JoinParams, byte: int = 0xFF) -> None:
+        """Test hook (phj_debug_poison_chunk_table): leave `side`'s chunk table
+        as a stale one would be (every byte = `byte`, marked clean)."""
+        self._check(self._L.phj_debug_poison_chunk_table(self._h, side, C.byref(params), byte))
+
     def hash_keys(self, kind: int, seed: int, keys) -> np.ndarray:
         keys = np.ascontiguousarray(np.asarray(keys, dtype=np.int64))
         out = np.zeros(keys.shape[0], dtype=np.uint64)

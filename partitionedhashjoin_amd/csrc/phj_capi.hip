@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "../../include/phj.h"
+#include "phj_cluster.h"
 #include "phj_join.h"
 #include "phj_mat.h"
 #include "phj_partition.h"
@@ -39,7 +40,8 @@ struct DevBuf {
 };
 
 // Launch-shape knobs (results never depend on them). Defaults are the tuned
-// values; PHJ_TILE_ITEMS / PHJ_P1_AOS / PHJ_XCD_REMAP override them for sweeps.
+// values; ctx_create_device reads their PHJ_* overrides (every one is run by
+// tests/test_gpu_schedules.py).
 struct Tuning {
     int tile = 4096;      // tile kernels: tuples per tile (2048, 4096 or 8192)
     int block = 512;      // threads per workgroup of the tile kernels (256, 512 or 1024; tile_shape)
@@ -55,6 +57,9 @@ struct Tuning {
     int p1_min_tiles = 32768;  // chunked pass 1: smallest relation (in 4096-tuple tiles, ~134M tuples)
     int p1_ko_tps = 1024;      // ... the keys-only form for the on-chip probe: tiles per shard (at every size)
     int p2probe = 1;      // radix join, 2 passes: the probe side's pass 2 on-chip (k_probe_ht)
+    int cluster = 1;      // radix join: LDS cluster tables (phj_cluster.h) when the build side's clusters fit
+    int cl_cap = static_cast<int>(kClCapMax);   // ... LDS table slots (8192: two workgroups per CU, 16384: one)
+    int cl_bits = 0;      // ... clusters = 2^cl_bits (0: the fewest >= 256 whose average fits the table)
 };
 
 int env_int(const char* name, int dflt) {
@@ -75,6 +80,7 @@ struct Plan {
     uint32_t sub_bits = 0, sub_shift = 0;   // phj_join: sub-partitions per partition (refine_plan)
     bool stable = false;  // PHJ_PART_STABLE: the reference's order inside each partition (not compared by ==)
     bool chained = false; // PHJ_TABLE_CHAINED: bucket-chained (CSR) tables in HBM (not compared by ==: tables only)
+    bool cluster = false; // phj_join: pass 1 = the LDS join's clusters (cluster_plan), the count path of phj_cluster.h
     bool operator==(const Plan& o) const {
         return hk == o.hk && seed == o.seed && mode == o.mode && P == o.P && npass == o.npass &&
                nb1 == o.nb1 && nb2 == o.nb2 && sub_bits == o.sub_bits && sub_shift == o.sub_shift;
@@ -99,6 +105,7 @@ struct SideState {
     DevBuf csink;                // ... code form: sink words of the stores past the tile (never read)
     bool ctab_dirty = true;      // chunked pass 1: the chunk table may hold entries (clear before the next pass)
     bool hcoded = false;         // the last pass 1 wrote hash codes (keys only, k_chunk_codes)
+    bool chunk_check = false;    // a chunked pass ran whose error word (chunk_err_word) nobody has read yet
     phj_partitioned view{};
     PassArgs p2{};               // p1_only: the pass-2 tile mapping over the pass-1 output
     uint32_t nt2 = 0;            // ... and its tile bound
@@ -416,6 +423,62 @@ void refine_plan_sub(const phj_ctx* c, Plan& pl, uint64_t nR) {
 
 void refine_plan(const phj_ctx* c, Plan& pl, uint64_t nR) { refine_plan_sub(c, pl, nR); }
 
+// The LDS join's plan (phj_cluster.h) from the requested one (make_plan):
+// pass 1 partitions into K = 2^k clusters, the top k bits of the partition
+// number q (refined by sub-partition bits when q has fewer than k bits: hash
+// bits just above the radix bits, or bits 40+ under h % P, as refine_plan_sub),
+// so every cluster is a union of whole requested partitions. K is the smallest
+// power of two >= 256 (chains enough for S's pass-1 cursors) whose average
+// cluster fills at most 0.8 of the LDS limit (the binomial spread of the
+// cluster sizes, ~3 % at 10M / 1024); larger build sides than 2048 clusters
+// hold take the code-table path. Returns false when the plan does not apply.
+bool cluster_plan(const phj_ctx* c, const Plan& base, uint64_t nR, Plan& pl) {
+    if (!c->tune.cluster || base.chained || nR == 0 || base.P == 0) return false;
+    const uint32_t cap = static_cast<uint32_t>(c->tune.cl_cap);
+    const double fit = 0.8 * cl_lim(cap);
+    uint32_t k = 8;
+    if (c->tune.cl_bits > 0) {
+        k = static_cast<uint32_t>(c->tune.cl_bits);
+    } else {
+        while (k < kMaxDigitBits && static_cast<double>(nR) / static_cast<double>(1u << k) > fit) k++;
+    }
+    if (k < 1 || k > static_cast<uint32_t>(kMaxDigitBits) || static_cast<double>(nR) / static_cast<double>(1u << k) > fit)
+        return false;
+    pl = base;
+    pl.cluster = true;
+    pl.sub_bits = 0;
+    pl.sub_shift = 0;
+    uint32_t bits;   // bits of the (refined) partition number
+    if (base.mode == 0) {
+        const uint32_t logP = ceil_log2(base.P);
+        if (logP < k) {
+            pl.sub_bits = k - logP;
+            pl.sub_shift = logP;
+        }
+        bits = std::max(logP, k);
+    } else {
+        uint32_t s = 0;
+        while ((base.P << s) < (1ull << k)) s++;
+        if (s) {
+            pl.sub_bits = s;
+            pl.sub_shift = 40;
+        }
+        bits = ceil_log2(base.P << s);
+    }
+    const uint64_t range = (base.mode == 0 ? (1ull << ceil_log2(base.P)) : base.P) << pl.sub_bits;
+    const uint32_t shift = bits - k;
+    pl.npass = 2;
+    pl.shift1 = shift;
+    pl.dmask1 = 0xffffffffu;
+    pl.nb1 = static_cast<uint32_t>((range + (1ull << shift) - 1) >> shift);
+    pl.bits1 = ceil_log2(pl.nb1);
+    pl.nb2 = 1u << shift;
+    pl.bits2 = shift;
+    pl.dmask2 = pl.nb2 - 1;
+    pl.Ppad = pl.nb1 * pl.nb2;
+    return pl.nb1 >= 2 && pl.nb1 <= static_cast<uint32_t>(kMaxBins);
+}
+
 DigitFn digit_fn(const Plan& pl, int pass) {
     DigitFn f{};
     f.seed = pl.seed;
@@ -444,6 +507,15 @@ uint64_t plan_empty0(const Plan& pl) {
     const DigitFn f = digit_fn(pl, 1);
     for (int b = 0; b < 64; b++)
         if (q_from_hash(1ull << b, f) != 0) return 1ull << b;
+    return 0;
+}
+
+// E of cluster 0 (phj_cluster.h): the lowest power of two outside cluster 0
+// (pass-1 digit 0); 0 when every code is in cluster 0.
+uint64_t cluster_empty0(const Plan& pl) {
+    const DigitFn f = digit_fn(pl, 1);
+    for (int b = 0; b < 64; b++)
+        if (((q_from_hash(1ull << b, f) >> f.shift) & f.dmask) != 0) return 1ull << b;
     return 0;
 }
 
@@ -491,10 +563,21 @@ int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const st
             const int kblock = BLOCK;
             // keys only, written as hash codes (the on-chip probe): k_chunk_codes;
             // whole tuples: VAR 3, LDS-atomic ranking, 16-B LDS entries (phj_partition.h)
-            if (a.keys_only)
-                kfn = hk == kMurmur3 ? reinterpret_cast<const void*>(&k_chunk_codes<BLOCK, ITEMS, kMurmur3>)
-                                     : reinterpret_cast<const void*>(&k_chunk_codes<BLOCK, ITEMS, kXXH3>);
-            else
+            // (more digits than threads: the cluster plans, 512 x 4096 only)
+            if (a.keys_only) {
+                if constexpr (BLOCK == 512 && ITEMS == 8) {
+                    if (a.nbins > 2 * BLOCK)
+                        kfn = hk == kMurmur3 ? reinterpret_cast<const void*>(&k_chunk_codes<BLOCK, ITEMS, kMurmur3, 4>)
+                                             : reinterpret_cast<const void*>(&k_chunk_codes<BLOCK, ITEMS, kXXH3, 4>);
+                    else if (a.nbins > BLOCK)
+                        kfn = hk == kMurmur3 ? reinterpret_cast<const void*>(&k_chunk_codes<BLOCK, ITEMS, kMurmur3, 2>)
+                                             : reinterpret_cast<const void*>(&k_chunk_codes<BLOCK, ITEMS, kXXH3, 2>);
+                }
+                if (!kfn && a.nbins > BLOCK) return set_err(c, PHJ_ERR_INVALID, "keys-only pass 1: more digits than threads");
+                if (!kfn)
+                    kfn = hk == kMurmur3 ? reinterpret_cast<const void*>(&k_chunk_codes<BLOCK, ITEMS, kMurmur3>)
+                                         : reinterpret_cast<const void*>(&k_chunk_codes<BLOCK, ITEMS, kXXH3>);
+            } else
                 kfn = hk == kMurmur3 ? reinterpret_cast<const void*>(&k_scatter_chunked<BLOCK, ITEMS, kMurmur3, 3>)
                                      : reinterpret_cast<const void*>(&k_scatter_chunked<BLOCK, ITEMS, kXXH3, 3>);
             // workgroups per CU: what the LDS and the kernel's registers allow
@@ -637,7 +720,8 @@ int partition_state(phj_ctx* c, SideState& S, const char* tag, const Plan& pl, b
     const bool ko = p1_only;
     const bool chunked = pl.npass == 2 && !pl.stable && c->tune.p1_chunk && (dcol || p1_only) && p1_aos && n > 0 &&
                          (ko || nt1 >= static_cast<uint32_t>(c->tune.p1_min_tiles)) &&
-                         tile == tile2 && pl.nb1 <= static_cast<uint32_t>(tile_shape(c, pl.nb1).block) &&
+                         tile == tile2 &&
+                         pl.nb1 <= static_cast<uint32_t>(tile_shape(c, pl.nb1).block) * (ko && tile_shape(c, pl.nb1).block == 512 && tile == 4096 ? 4u : 1u) &&
                          tile / tile_shape(c, pl.nb1).block <= 8 &&   // registers: the next tile is prefetched
                          (3 * (static_cast<uint64_t>(n) / tile + kShards) + kShards * pl.nb1) * tile < (1ull << 32);
     S.hcoded = chunked && ko;   // k_chunk_codes
@@ -719,6 +803,7 @@ int partition_state(phj_ctx* c, SideState& S, const char* tag, const Plan& pl, b
         a.pool_stride = pool_stride;
         a.nshards = nshards;
         S.ctab_dirty = n > 0;   // until k_tile_chunks has cleared what pass 1 publishes
+        S.chunk_check = n > 0;
     }
     uint32_t* tb2 = pl.npass == 2 ? static_cast<uint32_t*>(S.tbase2.p) : nullptr;
     PHJ_TRY(launch_pass(c, pl.hk, true, p1_aos, a, nt1, std::string(tag) + ".p1", n, nt1 * pl.nb1));
@@ -752,8 +837,8 @@ int partition_state(phj_ctx* c, SideState& S, const char* tag, const Plan& pl, b
                 uint32_t* ts = static_cast<uint32_t*>(S.tstart.p);
                 uint32_t* tc = ts + nt2max;
                 hipLaunchKernelGGL(k_tile_chunks, dim3((pl.nb1 * nshards + kWaves - 1) / kWaves), dim3(kBlock), 0, c->ks, tb2,
-                                   static_cast<const uint32_t*>(S.ccur.p), pl.nb1, nshards,
-                                   static_cast<unsigned long long*>(S.ctab.p), maxch, tile2,
+                                   static_cast<uint32_t*>(S.ccur.p), pl.nb1, nshards,
+                                   static_cast<unsigned long long*>(S.ctab.p), maxch, pool_stride, tile2,
                                    static_cast<uint32_t*>(S.tseg2.p), ts, tc);
                 PHJ_LAUNCHED(c, "k_tile_chunks");
                 S.ctab_dirty = false;
@@ -1052,6 +1137,8 @@ int build_and_probe(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned*
 // 512 x 4096 tiles), then pass 2 into final partition order (k_ht_p2, one
 // workgroup per pass-1 digit). `out` receives |R| codes, `bounds` the P + 1 partition
 // bounds: one build segment of build_ht (they may point into an exchange block).
+// A cluster plan (pl.cluster, phj_cluster.h) stops after pass 1: `out` = the
+// codes contiguous per cluster, `bounds` = the nb1 + 1 cluster bounds.
 int partition_build(phj_ctx* c, const Plan& pl, int64_t* out, uint32_t* bounds) {
     SideState& S = c->side[PHJ_SIDE_BUILD];
     c->scan_scratch = &S.partials;
@@ -1061,16 +1148,16 @@ int partition_build(phj_ctx* c, const Plan& pl, int64_t* out, uint32_t* bounds) 
     const uint32_t n = static_cast<uint32_t>(S.n), nb = pl.nb1, P = pl.Ppad;
     const uint32_t nt = (n + T - 1) / T, hlen = nt * nb;
     PHJ_TRY(ensure(c, S.hist1, std::max<size_t>(1, hlen) * 4));
-    PHJ_TRY(ensure(c, S.kA, std::max<size_t>(1, n) * 8));
+    if (!pl.cluster) PHJ_TRY(ensure(c, S.kA, std::max<size_t>(1, n) * 8));
     if (c->dry) return hlen ? scan_u32(c, nullptr, hlen, 1, hlen, c->scan_scratch) : PHJ_OK;
     if (n == 0) {
-        PHJ_HIP(c, hipMemsetAsync(bounds, 0, (static_cast<size_t>(P) + 1) * 4, c->ks));
+        PHJ_HIP(c, hipMemsetAsync(bounds, 0, (static_cast<size_t>(pl.cluster ? nb : P) + 1) * 4, c->ks));
         c->since_ev++;
         return PHJ_OK;
     }
     PassArgs a{};
     a.in_keys = reinterpret_cast<const int64_t*>(S.rel);
-    a.out_keys = static_cast<int64_t*>(S.kA.p);
+    a.out_keys = pl.cluster ? out : static_cast<int64_t*>(S.kA.p);
     a.hist = static_cast<uint32_t*>(S.hist1.p);
     a.nseg = 1;
     a.n = n;
@@ -1098,6 +1185,12 @@ int partition_build(phj_ctx* c, const Plan& pl, int64_t* out, uint32_t* bounds) 
         hipLaunchKernelGGL((k_scatter_codes<BLOCK, ITEMS, kXXH3>), dim3(grid), dim3(BLOCK), slds, c->ks, a);
     PHJ_LAUNCHED(c, "k_scatter_codes");
     PHJ_TRY(timer_end(c));
+    if (pl.cluster) {   // the cluster bounds from the scanned histogram
+        hipLaunchKernelGGL(k_pass1_finish, dim3(1), dim3(kFinBlock), 0, c->ks, a.hist, nt, nb, n, static_cast<uint32_t>(T),
+                           bounds, static_cast<uint32_t*>(nullptr));
+        PHJ_LAUNCHED(c, "k_pass1_finish");
+        return PHJ_OK;
+    }
     HtPass2Args b{};
     b.codes = static_cast<const int64_t*>(S.kA.p);
     b.hist1 = a.hist;
@@ -1159,16 +1252,29 @@ bool use_p2probe(const phj_ctx* c, const Plan& pl, uint64_t nS, uint64_t nR) {
            4 * nR + 2ull * pl.Ppad < (1ull << 32) && plan_empty0(pl) != 0;
 }
 
+// phj_join takes the LDS join (phj_cluster.h) when the plan's clusters fit:
+// out = the cluster plan. Needs the keys-only chunked pass 1 (512 x 4096 tiles).
+bool use_cluster(const phj_ctx* c, const Plan& pl, uint64_t nS, uint64_t nR, Plan& out) {
+    (void)nS;
+    if (!c->tune.p1_chunk || pl.stable || tile_shape(c, 2048).tile != 4096 || tile_shape(c, 2048).block != 512) return false;
+    if (!cluster_plan(c, pl, nR, out)) return false;
+    return cluster_empty0(out) != 0 && 4 * nR + 2ull * out.nb1 < (1ull << 32);
+}
+
 // Probe a probe-side pass-1 output (partition_state p1_only) against the
 // tables of build_ht; the count lands in (clear) or is added to c->count.
 int probe_ht(phj_ctx* c, const Plan& pl, SideState& PS, bool clear = true) {
-    if (clear) PHJ_HIP(c, hipMemsetAsync(c->count.p, 0, 8, c->ks));
+    if (clear) PHJ_HIP(c, hipMemsetAsync(c->count.p, 0, 16, c->ks));
     if (PS.nt2 == 0) return PHJ_OK;
     HtProbeArgs pa{};
     pa.a = PS.p2;
     pa.desc = static_cast<const uint2*>(c->ht_desc.p);
     pa.table = static_cast<const uint64_t*>(c->ht_tab.p);
     pa.count = static_cast<unsigned long long*>(c->count.p);
+    if (PS.chunk_check) {   // its error word is folded into the count pair
+        pa.err = static_cast<const uint32_t*>(PS.ccur.p) + chunk_err_word(PS.plan.nb1);
+        PS.chunk_check = false;
+    }
     pa.seed = pl.seed;
     pa.e1 = plan_empty0(pl);
     pa.nb2 = pl.nb2;
@@ -1194,19 +1300,118 @@ int probe_ht(phj_ctx* c, const Plan& pl, SideState& PS, bool clear = true) {
     return PHJ_OK;
 }
 
+// A stale chunk table met by a chunked pass (phj_partition.h chunk_err_word):
+// the pass wrote nothing through it, and the join reports PHJ_ERR_STATE. Both
+// sides' tables are cleared before their next pass.
+int chunk_table_error(phj_ctx* c, uint32_t bits) {
+    for (SideState& S : c->side) {
+        S.ctab_dirty = true;
+        S.chunk_check = false;
+    }
+    return set_err(c, PHJ_ERR_STATE, "chunked pass 1 read a chunk-table entry out of range (stale table, error bits " +
+                                         std::to_string(bits) + "); nothing was written through it");
+}
+
+// The error words of chunked passes not folded into a count (a 4-B read back
+// per side; the default on-chip join folds S's into the count instead).
+int check_chunk_errors(phj_ctx* c) {
+    for (SideState& S : c->side) {
+        if (!S.chunk_check) continue;
+        S.chunk_check = false;
+        uint32_t e = 0;
+        PHJ_HIP(c, hipMemcpyAsync(&e, static_cast<const uint32_t*>(S.ccur.p) + chunk_err_word(S.plan.nb1), 4,
+                                  hipMemcpyDeviceToHost, c->ks));
+        PHJ_HIP(c, hipStreamSynchronize(c->ks));
+        if (e) return chunk_table_error(c, e);
+    }
+    return PHJ_OK;
+}
+
+// The LDS join over a cluster plan: the HBM tables of the clusters beyond the
+// LDS limit (k_cluster_big_fill, on the current launch stream: R's chain),
+// then (probe_cluster, on the main stream) k_cluster_probe over the probe
+// side's pass-1 tiles. `nseg` build segments of codes contiguous per cluster
+// and nb1 + 1 bounds each; nR = their codes. The count pair is added to.
+ClusterArgs cluster_args(phj_ctx* c, const Plan& pl, int nseg, const int64_t* const* codes,
+                         const uint32_t* const* bounds) {
+    ClusterArgs a{};
+    for (int g = 0; g < nseg; g++) {
+        a.r_codes[g] = codes[g];
+        a.r_bounds[g] = bounds[g];
+    }
+    a.nseg = static_cast<uint32_t>(nseg);
+    a.nb1 = pl.nb1;
+    a.cap = static_cast<uint32_t>(c->tune.cl_cap);
+    a.lim = cl_lim(a.cap);
+    a.e1 = cluster_empty0(pl);
+    a.gtab = static_cast<uint64_t*>(c->ht_tab.p);
+    a.count = static_cast<unsigned long long*>(c->count.p);
+    return a;
+}
+
+int cluster_big_fill(phj_ctx* c, const Plan& pl, int nseg, const int64_t* const* codes, const uint32_t* const* bounds,
+                     uint64_t nR) {
+    if (nseg < 1 || nseg > kHtSegs) return set_err(c, PHJ_ERR_INVALID, "build segments must be in [1,16]");
+    const uint64_t slots = 4 * nR + 2ull * pl.nb1;
+    if (slots >= (1ull << 32)) return set_err(c, PHJ_ERR_RANGE, "build side too large for 32-bit table slots");
+    PHJ_TRY(ensure(c, c->ht_tab, slots * 8));
+    PHJ_TRY(ensure(c, c->count, 16));
+    if (c->dry) return PHJ_OK;
+    ClusterArgs a = cluster_args(c, pl, nseg, codes, bounds);
+    hipLaunchKernelGGL(k_cluster_big_fill, dim3(pl.nb1), dim3(256), 0, c->ks, a);
+    PHJ_LAUNCHED(c, "k_cluster_big_fill");
+    return PHJ_OK;
+}
+
+int probe_cluster(phj_ctx* c, const Plan& pl, SideState& PS, int nseg, const int64_t* const* codes,
+                  const uint32_t* const* bounds) {
+    if (c->dry || PS.nt2 == 0) return PHJ_OK;
+    if (!PS.hcoded) return set_err(c, PHJ_ERR_STATE, "the LDS join needs the keys-only pass 1 (codes)");
+    ClusterArgs a = cluster_args(c, pl, nseg, codes, bounds);
+    a.s_codes = PS.p2.in_keys;
+    a.tile_base = PS.p2.tile_base;
+    a.tile_seg = PS.p2.tile_seg;
+    a.tile_start = PS.p2.tile_start;
+    a.tile_cnt = PS.p2.tile_cnt;
+    if (PS.chunk_check) {   // its error word is folded into the count pair
+        a.err = static_cast<const uint32_t*>(PS.ccur.p) + chunk_err_word(PS.plan.nb1);
+        PS.chunk_check = false;
+    }
+    constexpr int B = kClBlock, I = kClItems;
+    const size_t lds = static_cast<size_t>(a.cap) * 8;
+    const void* kfn = reinterpret_cast<const void*>(&k_cluster_probe<B, I>);
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, B, lds) != hipSuccess || per_cu < 1) per_cu = 1;
+    per_cu = std::max(1, std::min<int>(per_cu, static_cast<int>(160 * 1024 / (lds + 256))));
+    // persistent, a multiple of 8 (XCD-grouped ranges), never many more than tiles
+    const uint32_t want = (PS.nt2 + 7) & ~7u;
+    const uint32_t grid = std::max<uint32_t>(8, std::min<uint32_t>(want, static_cast<uint32_t>(per_cu) * c->num_cus) & ~7u);
+    void* kargs[] = {&a};
+    PHJ_HIP(c, hipLaunchKernel(kfn, dim3(grid), dim3(B), kargs, lds, c->ks));
+    PHJ_LAUNCHED(c, "k_cluster_probe");
+    return PHJ_OK;
+}
+
 // The count comes back through a pinned host word (a pageable destination is
-// staged by the runtime: a slower copy on the step's critical path).
-int get_count(phj_ctx* c, uint64_t* out) {
+// staged by the runtime: a slower copy on the step's critical path). pair:
+// the on-chip probes' {count, failed}, failed set when S's pass 1 met a stale
+// chunk table (fold_pass1_error).
+int get_count(phj_ctx* c, uint64_t* out, bool pair = false) {
     if (!c->count_host && hipHostMalloc(reinterpret_cast<void**>(&c->count_host), 16, hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();
         c->count_host = nullptr;
     }
-    unsigned long long h = 0;
-    unsigned long long* dst = c->count_host ? c->count_host : &h;
-    PHJ_HIP(c, hipMemcpyAsync(dst, c->count.p, 8, hipMemcpyDeviceToHost, c->ks));
+    unsigned long long h[2] = {0, 0};
+    unsigned long long* dst = c->count_host ? c->count_host : h;
+    PHJ_HIP(c, hipMemcpyAsync(dst, c->count.p, pair ? 16 : 8, hipMemcpyDeviceToHost, c->ks));
     PHJ_HIP(c, hipStreamSynchronize(c->ks));
-    *out = *dst;
-    return PHJ_OK;
+    *out = dst[0];
+    if (pair && dst[1]) {
+        c->side[PHJ_SIDE_PROBE].chunk_check = true;   // read its word for the message
+        const int rc = check_chunk_errors(c);
+        return rc != PHJ_OK ? rc : chunk_table_error(c, 0);
+    }
+    return check_chunk_errors(c);
 }
 
 // The NoPartitioning count over region code tables (phj_table.h, k_np_probe_ct):
@@ -1533,6 +1738,9 @@ int ctx_create_device(int device, phj_ctx** out) {
     c->tune.subpart = env_int("PHJ_SUBPART", 1) != 0;
     c->tune.timers = env_int("PHJ_TIMERS", 1) != 0;
     c->tune.p1_chunk = env_int("PHJ_P1_CHUNK", 1) != 0;
+    c->tune.cluster = env_int("PHJ_CLUSTER", 1) != 0;
+    c->tune.cl_cap = env_int("PHJ_CL_CAP", static_cast<int>(kClCapMax)) == 8192 ? 8192 : static_cast<int>(kClCapMax);
+    c->tune.cl_bits = std::max(0, std::min(kMaxDigitBits, env_int("PHJ_CL_BITS", 0)));
     c->tune.p2probe = env_int("PHJ_P2PROBE", 1);
     c->tune.p1_slots = env_int("PHJ_P1_SLOTS", 0);
     c->tune.p1_wpc2 = std::max(0, env_int("PHJ_P1_WPC2", 2));
@@ -1921,8 +2129,56 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
     SideState& R = c->side[PHJ_SIDE_BUILD];
     SideState& S = c->side[PHJ_SIDE_PROBE];
     const uint32_t requested = pl.Ppad;   // reported; the join may sub-partition
-    refine_plan(c, pl, R.n);
     hipEvent_t t0, t1, tr, b0, b1, p1;
+    Plan cpl;
+    if (use_cluster(c, pl, S.n, R.n, cpl)) {
+        // the LDS join (phj_cluster.h): S's pass 1 into clusters (codes) on
+        // the main stream; R's pass 1 and the big clusters' HBM tables on the
+        // aux stream beside it; then the probe builds each cluster's table in
+        // LDS and probes S's codes against it
+        PHJ_TRY(ensure(c, c->count, 16));
+        PHJ_TRY(mark(c, &t0));
+        // the code pass's bookkeeping kernel clears the count pair (an empty
+        // S takes no chunked pass: a memset)
+        PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, cpl, true, static_cast<unsigned long long*>(c->count.p)));
+        if (!S.hcoded) PHJ_HIP(c, hipMemsetAsync(c->count.p, 0, 16, c->stream));
+        // R's chain waits for t0 (the previous step's probe read R's codes)
+        PHJ_HIP(c, hipStreamWaitEvent(c->aux, t0, 0));
+        c->ks = c->aux;
+        int rc = ensure(c, c->r_codes, std::max<uint64_t>(1, R.n) * 8);
+        if (rc == PHJ_OK) rc = ensure(c, c->r_bounds, (static_cast<size_t>(cpl.nb1) + 1) * 4);
+        const int64_t* rcodes = static_cast<const int64_t*>(c->r_codes.p);
+        const uint32_t* rbnd = static_cast<const uint32_t*>(c->r_bounds.p);
+        if (rc == PHJ_OK) rc = partition_build(c, cpl, static_cast<int64_t*>(c->r_codes.p), static_cast<uint32_t*>(c->r_bounds.p));
+        if (rc == PHJ_OK) rc = mark(c, &b0);
+        // algorithmic bytes: none at the balanced configurations (the LDS
+        // tables are built inside the probe); a big cluster's codes read and table written
+        if (rc == PHJ_OK) rc = timer_begin(c, "build", 0);
+        if (rc == PHJ_OK) rc = cluster_big_fill(c, cpl, 1, &rcodes, &rbnd, R.n);
+        if (rc == PHJ_OK) rc = timer_end(c);
+        if (rc == PHJ_OK) rc = mark(c, &tr);
+        c->ks = c->stream;
+        PHJ_TRY(rc);
+        PHJ_HIP(c, hipStreamWaitEvent(c->stream, tr, 0));
+        PHJ_TRY(mark(c, &t1));
+        // algorithmic bytes: S's codes read once, R's codes read by the workgroups that build their cluster
+        PHJ_TRY(timer_begin(c, "probe", (S.n + R.n) * 8));
+        PHJ_TRY(probe_cluster(c, cpl, S, 1, &rcodes, &rbnd));
+        PHJ_TRY(timer_end(c));
+        PHJ_TRY(mark(c, &p1));
+        uint64_t m = 0;
+        PHJ_TRY(get_count(c, &m, true));
+        r->matches = m;
+        r->partition_ms = elapsed(c, t0, t1);
+        r->build_ms = elapsed(c, b0, tr);
+        r->probe_ms = elapsed(c, t1, p1);
+        r->total_ms = elapsed(c, t0, p1);
+        r->num_partitions = requested;
+        // R: 16 read + 8 written (pass 1), 8 read (probe); S: 16 read + 8 written, 8 read
+        r->algorithmic_bytes = R.n * (24 + 8) + S.n * (24 + 8);
+        return fill_timers(c, r);
+    }
+    refine_plan(c, pl, R.n);
     if (use_p2probe(c, pl, S.n, R.n)) {
         // S: pass 1 only (its pass 2 runs inside the probe); R: pass 1 as codes
         // and its tables on the aux stream, beside S (measured: R's chain
@@ -1959,7 +2215,7 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
         PHJ_TRY(timer_end(c));
         PHJ_TRY(mark(c, &p1));
         uint64_t m = 0;
-        PHJ_TRY(get_count(c, &m));
+        PHJ_TRY(get_count(c, &m, true));
         r->matches = m;
         r->partition_ms = elapsed(c, t0, t1);
         r->build_ms = elapsed(c, b0, tr);
@@ -2018,8 +2274,18 @@ int phj_prepare(phj_ctx* c, const phj_join_params* p) {
         return join_nopart(c, p, &r);
     }
     if (p->algo != PHJ_ALGO_RADIX) return set_err(c, PHJ_ERR_INVALID, "Unrecognized join algorithm");
-    Plan pl;
+    Plan pl, cpl;
     PHJ_TRY(make_plan(c, p, pl));
+    if (use_cluster(c, pl, c->side[PHJ_SIDE_PROBE].n, c->side[PHJ_SIDE_BUILD].n, cpl)) {
+        const uint64_t nR = c->side[PHJ_SIDE_BUILD].n;
+        PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, cpl, true));
+        PHJ_TRY(ensure(c, c->r_codes, std::max<uint64_t>(1, nR) * 8));
+        PHJ_TRY(ensure(c, c->r_bounds, (static_cast<size_t>(cpl.nb1) + 1) * 4));
+        PHJ_TRY(partition_build(c, cpl, nullptr, nullptr));
+        PHJ_TRY(cluster_big_fill(c, cpl, 1, nullptr, nullptr, nR));
+        PHJ_HIP(c, hipStreamSynchronize(c->stream));
+        return PHJ_OK;
+    }
     refine_plan(c, pl, c->side[PHJ_SIDE_BUILD].n);
     if (use_p2probe(c, pl, c->side[PHJ_SIDE_PROBE].n, c->side[PHJ_SIDE_BUILD].n)) {
         const uint64_t nR = c->side[PHJ_SIDE_BUILD].n;
@@ -2076,7 +2342,10 @@ int phj_partitioned_download(phj_ctx* c, const phj_partitioned* v, int64_t* keys
         }
         return at.type == hipMemoryTypeDevice;
     };
-    if (!(on_device(keys) && on_device(payloads) && on_device(bounds))) PHJ_HIP(c, hipStreamSynchronize(c->ks));
+    if (!(on_device(keys) && on_device(payloads) && on_device(bounds))) {
+        PHJ_HIP(c, hipStreamSynchronize(c->ks));
+        PHJ_TRY(check_chunk_errors(c));   // a chunked pass that met a stale table wrote nothing through it
+    }
     return PHJ_OK;
 }
 
@@ -2143,11 +2412,15 @@ int phj_probe_pass1(phj_ctx* c, const phj_join_params* p, int64_t* keys, uint64_
     if (p->algo != PHJ_ALGO_RADIX) return set_err(c, PHJ_ERR_INVALID, "radix join parameters required");
     SideState& S = c->side[PHJ_SIDE_PROBE];
     if (n != S.n) return set_err(c, PHJ_ERR_INVALID, "n must be the probe relation's size");
-    Plan pl;
+    Plan pl, cpl;
     PHJ_TRY(make_plan(c, p, pl));
-    refine_plan(c, pl, c->side[PHJ_SIDE_BUILD].n);
-    if (!use_p2probe(c, pl, S.n, c->side[PHJ_SIDE_BUILD].n))
-        return set_err(c, PHJ_ERR_STATE, "these params do not take the on-chip probe");
+    if (use_cluster(c, pl, S.n, c->side[PHJ_SIDE_BUILD].n, cpl)) {
+        pl = cpl;   // phj_join's LDS join: pass 1 into its clusters
+    } else {
+        refine_plan(c, pl, c->side[PHJ_SIDE_BUILD].n);
+        if (!use_p2probe(c, pl, S.n, c->side[PHJ_SIDE_BUILD].n))
+            return set_err(c, PHJ_ERR_STATE, "these params do not take the on-chip probe");
+    }
     reset_timers(c);
     c->ks = c->stream;
     PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, pl, true));
@@ -2167,9 +2440,44 @@ int phj_probe_pass1(phj_ctx* c, const phj_join_params* p, int64_t* keys, uint64_
     PHJ_HIP(c, hipMemcpyAsync(bounds1, S.bounds1.p, (static_cast<size_t>(pl.nb1) + 1) * 4, hipMemcpyDeviceToHost, c->ks));
     if (n) PHJ_HIP(c, hipMemcpyAsync(keys, S.kB.p, n * 8, hipMemcpyDeviceToHost, c->ks));
     PHJ_HIP(c, hipStreamSynchronize(c->ks));
+    PHJ_TRY(check_chunk_errors(c));
     if (total != n) return set_err(c, PHJ_ERR_STATE, "pass-1 tiles hold " + std::to_string(total) + " keys, not " + std::to_string(n));
     *nb1 = pl.nb1;
     *codes = S.hcoded ? 1 : 0;
+    return PHJ_OK;
+}
+
+int phj_debug_poison_chunk_table(phj_ctx* c, int side, const phj_join_params* p, int byte) {
+    if (!c) return PHJ_ERR_INVALID;
+    PHJ_TRY(check_side(c, side));
+    if (c->group) return set_err(c, PHJ_ERR_STATE, "phj_debug_poison_chunk_table takes a single-device context");
+    if (!p || p->algo != PHJ_ALGO_RADIX) return set_err(c, PHJ_ERR_INVALID, "radix join parameters required");
+    (void)hipGetLastError();
+    PHJ_HIP(c, hipSetDevice(c->device));
+    Plan pl, cpl;
+    PHJ_TRY(make_plan(c, p, pl));
+    bool p1_only;
+    if (use_cluster(c, pl, c->side[PHJ_SIDE_PROBE].n, c->side[PHJ_SIDE_BUILD].n, cpl)) {
+        pl = cpl;
+        p1_only = side == PHJ_SIDE_PROBE;
+    } else {
+        refine_plan(c, pl, c->side[PHJ_SIDE_BUILD].n);
+        // the pass phj_join runs on this side: keys-only codes for the on-chip probe
+        p1_only = side == PHJ_SIDE_PROBE && use_p2probe(c, pl, c->side[PHJ_SIDE_PROBE].n, c->side[PHJ_SIDE_BUILD].n);
+    }
+    SideState& S = c->side[side];
+    if (!S.ctab.p) {   // no pass has allocated it yet: size it for phj_join's pass
+        struct DryScope {
+            phj_ctx* c;
+            ~DryScope() { c->dry = false; }
+        } scope{c};
+        c->dry = true;
+        PHJ_TRY(partition_state(c, S, side == PHJ_SIDE_BUILD ? "R" : "S", pl, p1_only));
+    }
+    if (!S.ctab.p) return set_err(c, PHJ_ERR_STATE, "these params take no chunked pass on this side");
+    PHJ_HIP(c, hipMemsetAsync(S.ctab.p, byte & 0xff, S.ctab.bytes, c->stream));
+    PHJ_HIP(c, hipStreamSynchronize(c->stream));
+    S.ctab_dirty = false;
     return PHJ_OK;
 }
 

@@ -360,8 +360,10 @@ int allgather_blocks(Group& G, int i, uint64_t elems, bool ok, bool receive = tr
 // main stream (B.cnt words 2-3 -> 0-1), so a member that failed after the
 // exchange makes every rank return an error; or (local) the host adds the
 // members' counts afterwards and the member threads carry the errors.
-// `failed`: this member has no valid count but still takes part.
-int allreduce_count(Group& G, int i, const void* local_count, bool failed = false) {
+// `failed`: this member has no valid count but still takes part. pair: the
+// local count is the on-chip probe's {count, failed} (fold_pass1_error), sent
+// as this rank's two words.
+int allreduce_count(Group& G, int i, const void* local_count, bool failed = false, bool pair = false) {
     phj_ctx* c = G.mem[i];
     MemberBufs& B = G.buf[i];
     if (G.kind == Xchg::kRccl) {
@@ -373,17 +375,17 @@ int allreduce_count(Group& G, int i, const void* local_count, bool failed = fals
         phj_count_contribution(0, failed ? 1 : 0, w);
         PHJ_HIP(c, hipMemsetAsync(d + 2, 0, 16, c->ks));
         if (failed) PHJ_HIP(c, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d + 3), static_cast<uint32_t>(w[1]), 1, c->ks));
-        else PHJ_HIP(c, hipMemcpyAsync(d + 2, local_count, 8, hipMemcpyDeviceToDevice, c->ks));
+        else PHJ_HIP(c, hipMemcpyAsync(d + 2, local_count, pair ? 16 : 8, hipMemcpyDeviceToDevice, c->ks));
         PHJ_NCCL(c, rccl().AllReduce(d + 2, d, 2, ncclUint64, ncclSum, G.comm[i], c->ks));
     } else {
         if (failed) return PHJ_OK;
-        PHJ_HIP(c, hipMemcpyAsync(B.cnt.p, local_count, 8, hipMemcpyDeviceToDevice, c->ks));
+        PHJ_HIP(c, hipMemcpyAsync(B.cnt.p, local_count, pair ? 16 : 8, hipMemcpyDeviceToDevice, c->ks));
     }
     c->since_ev++;
     return PHJ_OK;
 }
 
-int read_count(Group& G, int i, uint64_t* out) {
+int read_count(Group& G, int i, uint64_t* out, bool pair = false) {
     phj_ctx* c = G.mem[i];
     if (!c->count_host && hipHostMalloc(reinterpret_cast<void**>(&c->count_host), 16, hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();
@@ -395,6 +397,7 @@ int read_count(Group& G, int i, uint64_t* out) {
     PHJ_HIP(c, hipStreamSynchronize(c->ks));
     if (G.kind == Xchg::kLocal) {
         *out = h[0];
+        if (pair && h[1]) return chunk_table_error(c, 0);   // this member's probe folded its pass-1 error
         return PHJ_OK;
     }
     const uint64_t words[2] = {h[0], h[1]};
@@ -406,15 +409,17 @@ int read_count(Group& G, int i, uint64_t* out) {
 // The exchange block carries the pass-1 codes and digit bounds of the on-chip
 // join (R's pass 2 happens inside the table build), or the fully partitioned
 // keys and final bounds of the fused join.
+// A cluster plan (pl.cluster: the LDS join, phj_cluster.h) ships each rank's
+// R codes contiguous per cluster + the nb1 + 1 cluster bounds.
 bool member_p2(const Group& G, const phj_ctx* c, const Plan& pl) {
-    return use_p2probe(c, pl, c->side[PHJ_SIDE_PROBE].n, total(G.n[PHJ_SIDE_BUILD]));
+    return pl.cluster || use_p2probe(c, pl, c->side[PHJ_SIDE_PROBE].n, total(G.n[PHJ_SIDE_BUILD]));
 }
 
 PackLayout member_layout(const Group& G, const Plan& pl, bool p2) {
-    (void)p2;   // both forms ship codes / keys in final partition order + P + 1 bounds
+    (void)p2;   // every form ships codes / keys in partition (or cluster) order + bounds
     uint64_t maxn = 0;
     for (uint64_t x : G.n[PHJ_SIDE_BUILD]) maxn = std::max(maxn, x);
-    return pack_layout(maxn, pl.Ppad);
+    return pack_layout(maxn, pl.cluster ? pl.nb1 : pl.Ppad);
 }
 
 int member_alloc_radix(Group& G, int i, const Plan& pl, bool p2) {
@@ -462,7 +467,10 @@ int member_prepare_radix(Group& G, int i, const Plan& pl) {
     c->dry = true;
     PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, pl, p2));
     const PackLayout L = member_layout(G, pl, p2);
-    if (p2) {
+    if (pl.cluster) {
+        PHJ_TRY(partition_build(c, pl, nullptr, nullptr));
+        PHJ_TRY(cluster_big_fill(c, pl, G.world, nullptr, nullptr, total(G.n[PHJ_SIDE_BUILD])));
+    } else if (p2) {
         PHJ_TRY(partition_build(c, pl, nullptr, nullptr));
         PHJ_TRY(build_ht(c, pl, G.world, nullptr, nullptr, total(G.n[PHJ_SIDE_BUILD])));
     } else {
@@ -524,7 +532,7 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
         // the code pass's bookkeeping kernel clears the count (hcoded); else a memset
         if (rc == PHJ_OK)
             rc = partition_side(c, PHJ_SIDE_PROBE, pl, p2, p2 ? static_cast<unsigned long long*>(c->count.p) : nullptr);
-        if (rc == PHJ_OK && p2 && !c->side[PHJ_SIDE_PROBE].hcoded && hipMemsetAsync(c->count.p, 0, 8, c->stream) != hipSuccess)
+        if (rc == PHJ_OK && p2 && !c->side[PHJ_SIDE_PROBE].hcoded && hipMemsetAsync(c->count.p, 0, 16, c->stream) != hipSuccess)
             rc = set_err(c, PHJ_ERR_HIP, "count reset");
         if (rc == PHJ_OK && p2) rc = mark(c, &sdone);
         c->ks = c->aux;
@@ -559,8 +567,13 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
         const uint32_t* bnd[kHtSegs];
         gathered_codes(G, i, L, codes, bnd);
         const uint64_t nRall = total(G.n[PHJ_SIDE_BUILD]);
-        if (rc == PHJ_OK) rc = timer_begin(c, "build", nRall * 8 * 3);   // codes read, tables written
-        if (rc == PHJ_OK) rc = build_ht(c, pl, G.world, codes, bnd, nRall);
+        if (pl.cluster) {   // only the big clusters' HBM tables; the LDS tables are built in the probe
+            if (rc == PHJ_OK) rc = timer_begin(c, "build", 0);
+            if (rc == PHJ_OK) rc = cluster_big_fill(c, pl, G.world, codes, bnd, nRall);
+        } else {
+            if (rc == PHJ_OK) rc = timer_begin(c, "build", nRall * 8 * 3);   // codes read, tables written
+            if (rc == PHJ_OK) rc = build_ht(c, pl, G.world, codes, bnd, nRall);
+        }
         if (rc == PHJ_OK) rc = timer_end(c);
         if (rc == PHJ_OK) rc = mark(c, &b1);
     } else if (rc == PHJ_OK) {
@@ -583,7 +596,14 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
             PHJ_HIP(c, hipStreamWaitEvent(c->aux, sdone, 0));
             PHJ_TRY(mark(c, &t1));
             PHJ_TRY(timer_begin(c, "probe", c->side[PHJ_SIDE_PROBE].n * (c->side[PHJ_SIDE_PROBE].p2.keys_only ? 8 : 16)));
-            PHJ_TRY(probe_ht(c, pl, c->side[PHJ_SIDE_PROBE], false));
+            if (pl.cluster) {
+                const int64_t* codes[kHtSegs];
+                const uint32_t* bnd[kHtSegs];
+                gathered_codes(G, i, L, codes, bnd);
+                PHJ_TRY(probe_cluster(c, pl, c->side[PHJ_SIDE_PROBE], G.world, codes, bnd));
+            } else {
+                PHJ_TRY(probe_ht(c, pl, c->side[PHJ_SIDE_PROBE], false));
+            }
             PHJ_TRY(timer_end(c));
             PHJ_TRY(mark(c, &p1));
             c->last_fused = false;
@@ -596,7 +616,7 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
     if (rc == PHJ_OK) rc = join_local();
     // RCCL: a member that failed still takes part in the count all-reduce
     if (rc == PHJ_OK || G.kind == Xchg::kRccl) {
-        const int ra = allreduce_count(G, i, c->count.p, rc != PHJ_OK);
+        const int ra = allreduce_count(G, i, c->count.p, rc != PHJ_OK, p2);
         if (rc == PHJ_OK) rc = ra;
     }
     if (rc != PHJ_OK) {
@@ -605,7 +625,7 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
     }
     PHJ_TRY(mark(c, &te));
     uint64_t m = 0;
-    rc = read_count(G, i, &m);
+    rc = read_count(G, i, &m, p2);
     c->ks = c->stream;
     PHJ_TRY(rc);
     r->matches = m;
@@ -782,8 +802,11 @@ int group_join(phj_ctx* shell, const phj_join_params* p, phj_join_result* r, boo
     if (const int rc = make_plan(G.mem[0], p, pl); rc != PHJ_OK) return set_err(shell, rc, G.mem[0]->err);
     const uint32_t requested = pl.Ppad;
     // every rank plans for the GLOBAL build side (the gathered segments), so all
-    // ranks partition by the same function
-    refine_plan(G.mem[0], pl, total(G.n[PHJ_SIDE_BUILD]));
+    // ranks partition by the same function: the LDS join's clusters, or the
+    // code tables' refined plan
+    Plan cpl;
+    if (use_cluster(G.mem[0], pl, 0, total(G.n[PHJ_SIDE_BUILD]), cpl)) pl = cpl;
+    else refine_plan(G.mem[0], pl, total(G.n[PHJ_SIDE_BUILD]));
     if (dry) return for_members(shell, G, [&](int i) { return member_prepare_radix(G, i, pl); });
     PHJ_TRY(for_members(shell, G, [&](int i) { return member_radix(G, i, pl, &G.res[i]); }));
     merge_results(G, r);

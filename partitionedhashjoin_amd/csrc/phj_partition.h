@@ -90,7 +90,10 @@ constexpr uint32_t kShards = 16;
 constexpr unsigned long long kPublished = 1ull << 32;
 constexpr uint32_t kTilesPerShard = 3072;
 __host__ __device__ constexpr size_t chunk_pool_word(uint32_t nb, uint32_t x) { return (static_cast<size_t>(kShards) * nb + 31) / 32 * 32 + 32 * x; }
-__host__ __device__ constexpr size_t chunk_ticket_word(uint32_t nb, uint32_t x) { return chunk_pool_word(nb, kShards + x); }
+// the pass's error word: a chunk id or chain index read back out of range
+// (a stale chunk table) sets kChunkErr* bits here instead of writing through it
+__host__ __device__ constexpr size_t chunk_err_word(uint32_t nb) { return chunk_pool_word(nb, kShards); }
+constexpr uint32_t kChunkErrId = 1, kChunkErrIndex = 2, kChunkErrTable = 4;
 __host__ __device__ constexpr size_t chunk_hint_word(uint32_t nb) { return chunk_pool_word(nb, 2 * kShards); }
 constexpr uint32_t kSinkGroups = 1024;   // k_chunk_codes: workgroups with their own sink words (PassArgs::sink)
 __host__ __device__ constexpr size_t chunk_state_bytes(uint32_t nb) { return chunk_hint_word(nb) * 4 + static_cast<size_t>(kShards) * nb * 8; }
@@ -436,7 +439,7 @@ __global__ __launch_bounds__(256) void k_hist_col(PassArgs a) {
 // A chunked pass 1 adds one word per digit. At T = 4096, nb = 256, NW = 8
 // that is 80,960 B: still two workgroups per CU.
 __host__ __device__ constexpr size_t scatter_lds_bytes(int T, uint32_t nb, int NW = kWaves, bool chunked = false) {
-    return static_cast<size_t>(T) * (nb <= 256 ? 17 : 18) + static_cast<size_t>(nb) * 4 * (NW + (chunked ? 3 : 2)) + 64;
+    return static_cast<size_t>(T) * (nb <= 256 ? 17 : 18) + static_cast<size_t>(nb) * 4 * (NW + (chunked ? 3 : 2)) + (chunked ? 128 : 64);
 }
 
 // Sorted-digit array of the scatter kernels: u8 for nb <= 256, else u16.
@@ -611,8 +614,8 @@ void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
     uint32_t* wcnt = reinterpret_cast<uint32_t*>(spay + T);  // [NW][nb]
     uint32_t* gofs = wcnt + NW * nb;                          // [nb] k <  dsplit: slot = gofs + k
     uint32_t* dstart = gofs + nb;                             // [nb] k >= dsplit: slot = dstart + k
-    uint32_t* tmp = dstart + nb;                              // 16 words
-    const SortedDigits sdig{tmp + 16, nb <= 256};             // [T]
+    uint32_t* tmp = dstart + nb;                              // 32 words: [0, NW) scan, 16-17 reservations, 18 bad tile
+    const SortedDigits sdig{tmp + 32, nb <= 256};             // [T]
     uint32_t* dsplit = static_cast<uint32_t*>(sdig.end(T));   // [nb]
     uint4* wdesc = reinterpret_cast<uint4*>(wcnt + (((DB ? 2u : 1u) * nb + 3u) & ~3u));   // PACK: [nb] {k < split: slot - k, else, split}
 
@@ -624,6 +627,8 @@ void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
     const uint32_t wbase = wave * 64 * ITEMS;
     uint32_t* curs = a.chunk_cursor + static_cast<size_t>(x) * nb;   // this shard's chains
     uint32_t* pool = a.chunk_cursor + chunk_pool_word(nb, x);
+    uint32_t* errw = a.chunk_cursor + chunk_err_word(nb);
+    const uint32_t id_lo = x * a.pool_stride, id_hi = id_lo + a.pool_stride;   // shard x's pool chunks
     unsigned long long* hints = reinterpret_cast<unsigned long long*>(a.chunk_cursor + chunk_hint_word(nb)) + static_cast<size_t>(x) * nb;
     auto cur = [&](uint32_t d) { return curs + d; };
     auto hint_of = [&](uint32_t d) { return hints + d; };
@@ -714,8 +719,9 @@ void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
             if (tid == 0) {
                 // the tile's reserved pool chunks are static: shard x's pool keeps
                 // its first 2 * per chunks for its tiles, two each
-                tmp[12] = x * a.pool_stride + 2 * (tile - x * per);
-                tmp[13] = 0;
+                tmp[16] = id_lo + 2 * (tile - x * per);
+                tmp[17] = 0;
+                tmp[18] = 0;
             }
         }
         __syncthreads();
@@ -748,15 +754,16 @@ void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
             const uint32_t off = v0 % T, k0 = v0 / T, k1 = (v0 + c - 1) / T;
             unsigned long long* tab = a.chunk_tab + (static_cast<size_t>(x) * nb + d) * a.maxch;
             auto take = [&]() -> uint32_t {
-                const uint32_t r = atomicAdd(&tmp[13], 1u);
-                if (r < 2) return tmp[12] + r;
-                return x * a.pool_stride + 2 * per + atomicAdd(pool, 1u);
+                const uint32_t r = atomicAdd(&tmp[17], 1u);
+                if (r < 2) return tmp[16] + r;
+                return id_lo + 2 * per + atomicAdd(pool, 1u);
             };
             auto publish = [&](uint32_t k, uint32_t id) {
+                if (k >= a.maxch) return;   // flagged below
                 __hip_atomic_store(&tab[k], kPublished | id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 atomicMax(hint_of(d), (static_cast<unsigned long long>(k + 1) << 32) | id);
             };
-            uint32_t id0 = 0, id1 = 0;
+            uint32_t id0 = id_lo, id1 = id_lo;
             if (off == 0) {
                 id0 = take();
                 publish(k0, id0);
@@ -765,15 +772,21 @@ void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
                 id1 = take();
                 publish(k1, id1);
             }
+            uint32_t bad = k1 >= a.maxch ? kChunkErrIndex : 0u;
             if (off != 0) {
                 if ((hint >> 32) == k0 + 1ull) {
                     id0 = static_cast<uint32_t>(hint);
-                } else {
+                } else if (k0 < a.maxch) {
                     unsigned long long v;
                     while (((v = __hip_atomic_load(&tab[k0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) == 0)
                         __builtin_amdgcn_s_sleep(2);
                     id0 = static_cast<uint32_t>(v);
                 }
+            }
+            if (id0 < id_lo || id0 >= id_hi || id1 < id_lo || id1 >= id_hi) bad |= kChunkErrId;
+            if (bad) {   // a stale chunk table: no store of this tile goes through it
+                tmp[18] = 1;
+                atomicOr(errw, bad);
             }
             // sorted element k of digit d goes to chain slot v0 + (k - ds)
             const uint32_t split = ds + (T - off);
@@ -786,10 +799,11 @@ void k_scatter_chunked(PassArgs a, uint32_t ntiles, uint32_t per) {
             }
         }
         __syncthreads();
+        const uint32_t lim = tmp[18] ? 0u : cnt;
 #pragma unroll
         for (int i = 0; i < ITEMS; i++) {
             const uint32_t k = i * BLOCK + tid;
-            if (k < cnt) {
+            if (k < lim) {
                 const uint32_t d = sdig.get(k);
                 uint32_t o;
                 if constexpr (PACK) {
@@ -841,18 +855,24 @@ __host__ __device__ constexpr size_t chunk_codes_lds_bytes(int T, uint32_t nb) {
 // (Deferring the claims' resolution by a tile was measured 0.5 ms slower at
 // 200M: a chunk's owner then publishes its id a tile late and the runs that
 // continue the chunk wait for it.)
-template <int BLOCK, int ITEMS, int HK>
+//  - DPT digits per thread (nb <= DPT * BLOCK): thread t owns digits
+//    [t * DPT, (t + 1) * DPT) for the scan, the claims and the chain protocol
+//    (DPT > 1: the cluster plans of the LDS join, up to 2048 digits).
+// Chunk ids and chain indices read back from memory (hint, chunk table) or
+// taken from the pool are bound-checked: one out of range (a stale table)
+// sets the pass's error word and the tile's stores go to the sink words.
+template <int BLOCK, int ITEMS, int HK, int DPT = 1>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(2 * BLOCK / 256)))
 void k_chunk_codes(PassArgs a, uint32_t ntiles, uint32_t per) {
     constexpr int NW = BLOCK / 64;
     constexpr int T = BLOCK * ITEMS;
     static_assert(NW <= 16, "scan words [0, NW) below the reservation words");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const uint32_t nb = a.nbins;   // host: nb <= BLOCK (digit d = thread d)
+    const uint32_t nb = a.nbins;   // host: nb <= DPT * BLOCK
     int64_t* sbuf = reinterpret_cast<int64_t*>(smem);                       // [T] sorted codes
     uint32_t* wcnt = reinterpret_cast<uint32_t*>(sbuf + T);                 // [2][nb] counter rows
     uint4* wdesc = reinterpret_cast<uint4*>(wcnt + (2 * nb + 3u) / 4 * 4);  // [nb] {k < split: slot - k, else, split}
-    uint32_t* tmp = reinterpret_cast<uint32_t*>(wdesc + nb);                // [0, NW) scan; 16, 17 reservations
+    uint32_t* tmp = reinterpret_cast<uint32_t*>(wdesc + nb);                // [0, NW) scan; 16, 17 reservations; 18 bad tile
 
     const uint32_t x = blockIdx.x % a.nshards, slots = gridDim.x / a.nshards;
     const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -862,7 +882,9 @@ void k_chunk_codes(PassArgs a, uint32_t ntiles, uint32_t per) {
     const uint32_t wbase = wave * 64 * ITEMS;
     uint32_t* curs = a.chunk_cursor + static_cast<size_t>(x) * nb;   // this shard's chains
     uint32_t* pool = a.chunk_cursor + chunk_pool_word(nb, x);
+    uint32_t* errw = a.chunk_cursor + chunk_err_word(nb);
     unsigned long long* hints = reinterpret_cast<unsigned long long*>(a.chunk_cursor + chunk_hint_word(nb)) + static_cast<size_t>(x) * nb;
+    const uint32_t id_lo = x * a.pool_stride, id_hi = id_lo + a.pool_stride;   // shard x's pool chunks
     // a code's digit; pow2 = the plan's uniform power-of-two form (q = h & (P - 1),
     // no refinement), hoisted out of the per-element loops
     const bool pow2q = a.f.mode == 0 && a.f.sub_bits == 0;
@@ -922,22 +944,40 @@ void k_chunk_codes(PassArgs a, uint32_t ntiles, uint32_t per) {
 #pragma unroll
         for (int i = 0; i < ITEMS; i++) rank[i] = atomicAdd(&crow[dig[i]], wbase + i * 64 + lane < cnt ? 1u : 0u);
         __syncthreads();
-        // digit totals (d = tid) -> tile-local starts; claim the run in the chain
-        const uint32_t c = tid < nb ? crow[tid] : 0u;
+        // digit totals (thread tid: digits d0 .. d0 + DPT - 1) -> tile-local
+        // starts; claim the runs in the chains
+        const uint32_t d0 = tid * DPT;
+        uint32_t c[DPT], ds[DPT], v0[DPT];
+        unsigned long long hint[DPT];
+        uint32_t local = 0;
+#pragma unroll
+        for (int j = 0; j < DPT; j++) {
+            c[j] = d0 + j < nb ? crow[d0 + j] : 0u;
+            local += c[j];
+        }
         uint32_t total;
-        const uint32_t ds = block_exclusive_scan_t<NW, false>(c, tmp, total);
-        if (tid < nb) crow[tid] = ds;
-        uint32_t v0 = 0;
-        unsigned long long hint = 0;
-        if (tid < nb && c) {   // waited for below, in this tile: a conditional issue costs no wait
-            v0 = atomicAdd(curs + tid, c);
-            hint = __hip_atomic_load(hints + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t run = block_exclusive_scan_t<NW, false>(local, tmp, total);
+#pragma unroll
+        for (int j = 0; j < DPT; j++) {
+            ds[j] = run;
+            if (d0 + j < nb) crow[d0 + j] = run;
+            run += c[j];
+            v0[j] = 0;
+            hint[j] = 0;
+        }
+#pragma unroll
+        for (int j = 0; j < DPT; j++) {
+            if (c[j]) {   // waited for below, in this tile: a conditional issue costs no wait
+                v0[j] = atomicAdd(curs + d0 + j, c[j]);
+                hint[j] = __hip_atomic_load(hints + d0 + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
         if (tid == 0) {
             // the tile's reserved pool chunks are static: shard x's pool keeps
             // its first 2 * per chunks for its tiles, two each
-            tmp[16] = x * a.pool_stride + 2 * (tile - x * per);
+            tmp[16] = id_lo + 2 * (tile - x * per);
             tmp[17] = 0;
+            tmp[18] = 0;
         }
         __syncthreads();
         {
@@ -952,21 +992,25 @@ void k_chunk_codes(PassArgs a, uint32_t ntiles, uint32_t per) {
             uint32_t* const other = wcnt + (par ^ 1u) * nb;
             for (uint32_t i = tid; i < nb; i += BLOCK) other[i] = 0;
         }
-        // chain protocol (k_scatter_chunked): digit tid's run -> chunk ids -> wdesc[tid]
-        if (tid < nb && c) {
-            const uint32_t d = tid;
-            const uint32_t off = v0 % T, k0 = v0 / T, k1 = (v0 + c - 1) / T;
+        // chain protocol (k_scatter_chunked): digit d's run -> chunk ids -> wdesc[d]
+        uint32_t bad = 0;
+#pragma unroll
+        for (int j = 0; j < DPT; j++) {
+            if (!c[j]) continue;
+            const uint32_t d = d0 + j;
+            const uint32_t off = v0[j] % T, k0 = v0[j] / T, k1 = (v0[j] + c[j] - 1) / T;
             unsigned long long* tab = a.chunk_tab + (static_cast<size_t>(x) * nb + d) * a.maxch;
             auto take = [&]() -> uint32_t {
                 const uint32_t r = atomicAdd(&tmp[17], 1u);
                 if (r < 2) return tmp[16] + r;
-                return x * a.pool_stride + 2 * per + atomicAdd(pool, 1u);
+                return id_lo + 2 * per + atomicAdd(pool, 1u);
             };
             auto publish = [&](uint32_t k, uint32_t id) {
+                if (k >= a.maxch) return;   // flagged below
                 __hip_atomic_store(&tab[k], kPublished | id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 atomicMax(hints + d, (static_cast<unsigned long long>(k + 1) << 32) | id);
             };
-            uint32_t id0 = 0, id1 = 0;
+            uint32_t id0 = id_lo, id1 = id_lo;
             if (off == 0) {
                 id0 = take();
                 publish(k0, id0);
@@ -975,23 +1019,31 @@ void k_chunk_codes(PassArgs a, uint32_t ntiles, uint32_t per) {
                 id1 = take();
                 publish(k1, id1);
             }
+            if (k1 >= a.maxch) bad |= kChunkErrIndex;
             if (off != 0) {
-                if ((hint >> 32) == k0 + 1ull) {
-                    id0 = static_cast<uint32_t>(hint);
-                } else {
+                if ((hint[j] >> 32) == k0 + 1ull) {
+                    id0 = static_cast<uint32_t>(hint[j]);
+                } else if (k0 < a.maxch) {
                     unsigned long long v;
                     while (((v = __hip_atomic_load(&tab[k0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) == 0)
                         __builtin_amdgcn_s_sleep(2);
                     id0 = static_cast<uint32_t>(v);
                 }
             }
+            if (id0 < id_lo || id0 >= id_hi || id1 < id_lo || id1 >= id_hi) bad |= kChunkErrId;
             // sorted element k of digit d goes to chain slot v0 + (k - ds)
-            const uint32_t split = ds + (T - off);
-            wdesc[d] = make_uint4(id0 * T + off - ds, id1 * T - split, split, 0u);
+            const uint32_t split = ds[j] + (T - off);
+            wdesc[d] = make_uint4(id0 * T + off - ds[j], id1 * T - split, split, 0u);
+        }
+        if (bad) {
+            tmp[18] = 1;
+            atomicOr(errw, bad);
         }
         __syncthreads();
         // sorted element k: code, digit, slot, all LDS reads of the ITEMS
-        // elements in flight together; a lane past the tile stores to its sink
+        // elements in flight together; a lane past the tile (or every lane of
+        // a tile with an id out of range) stores to its sink
+        const uint32_t lim = tmp[18] ? 0u : cnt;
         auto write_out = [&](auto pow2) {
             int64_t v[ITEMS];
             uint32_t o[ITEMS];
@@ -1004,14 +1056,15 @@ void k_chunk_codes(PassArgs a, uint32_t ntiles, uint32_t per) {
                 o[i] = (k < w.z ? w.x : w.y) + k;
             }
 #pragma unroll
-            for (int i = 0; i < ITEMS; i++) *(i * BLOCK + tid < cnt ? a.out_keys + o[i] : ssink) = v[i];
+            for (int i = 0; i < ITEMS; i++) *(i * BLOCK + tid < lim ? a.out_keys + o[i] : ssink) = v[i];
         };
         if (pow2q) write_out(std::true_type{});
         else write_out(std::false_type{});
         // the claim's registers stay live past the write-out: else they are
         // reused there, and a lane that issued no claim would first wait for
         // everything in flight (the compiler cannot tell which lanes did)
-        __asm__ volatile("" ::"v"(v0), "v"(hint));
+#pragma unroll
+        for (int j = 0; j < DPT; j++) __asm__ volatile("" ::"v"(v0[j]), "v"(hint[j]));
         if (next >= t_end) return;
         tile = next;
         par ^= 1u;
@@ -1188,12 +1241,14 @@ __global__ __launch_bounds__(kBlock) void k_tile_seg(const uint32_t* tile_base, 
 // chains, shard by shard, chunk by chunk: tile_seg / tile_start (first slot) /
 // tile_cnt (tuples) of each. One wave per chain (segment s, shard x): lane x'
 // reads chain (s, x')'s size for the chain's first tile, then the lanes write
-// the chain's chunks.
-__global__ __launch_bounds__(kBlock) void k_tile_chunks(const uint32_t* tile_base, const uint32_t* sizes,
+// the chain's chunks. An entry that is not published or names a chunk outside
+// shard x's pool (a stale table) becomes an empty tile and sets the pass's
+// error word (the consumers read no slot through it).
+__global__ __launch_bounds__(kBlock) void k_tile_chunks(const uint32_t* tile_base, uint32_t* sizes,
                                                         uint32_t nseg, uint32_t nshards,
                                                         unsigned long long* chunk_tab, uint32_t maxch,
-                                                        uint32_t T, uint32_t* tile_seg, uint32_t* tile_start,
-                                                        uint32_t* tile_cnt) {
+                                                        uint32_t pool_stride, uint32_t T, uint32_t* tile_seg,
+                                                        uint32_t* tile_start, uint32_t* tile_cnt) {
     const uint32_t w = blockIdx.x * kWaves + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (w >= nseg * nshards) return;
     const uint32_t s = w / nshards, x = w - s * nshards;
@@ -1204,24 +1259,30 @@ __global__ __launch_bounds__(kBlock) void k_tile_chunks(const uint32_t* tile_bas
     const uint32_t szx = sizes[x * nseg + s], nch = (szx + T - 1) / T;
     const uint32_t t0 = tile_base[s] + before;
     unsigned long long* tab = chunk_tab + (static_cast<size_t>(x) * nseg + s) * maxch;
+    uint32_t bad = 0;
     for (uint32_t k = lane; k < nch; k += 64) {
+        const unsigned long long v = k < maxch ? tab[k] : 0ull;
+        const uint32_t id = static_cast<uint32_t>(v);
+        const bool ok = k < maxch && (v >> 32) == 1ull && id >= x * pool_stride && id < (x + 1) * pool_stride;
         tile_seg[t0 + k] = s;
-        tile_start[t0 + k] = static_cast<uint32_t>(tab[k]) * T;
-        tile_cnt[t0 + k] = min(T, szx - k * T);
-        tab[k] = 0;   // the next pass starts from an all-zero table (kPublished)
+        tile_start[t0 + k] = ok ? id * T : 0u;
+        tile_cnt[t0 + k] = ok ? min(T, szx - k * T) : 0u;
+        if (!ok) bad |= kChunkErrTable;
+        if (k < maxch) tab[k] = 0;   // the next pass starts from an all-zero table (kPublished)
     }
+    if (bad) atomicOr(sizes + chunk_err_word(nseg), bad);
 }
 
 // After a chunked pass 1: bounds1 = exclusive scan of the digit sizes (summed
 // over the shards: the segments' offsets in the pass-2 output) and
-// tile_base2 = exclusive scan of their chunk counts; `zero` (may be null) is
-// cleared. One workgroup.
+// tile_base2 = exclusive scan of their chunk counts; `zero` (may be null: two
+// words) is cleared. One workgroup.
 __global__ __launch_bounds__(kFinBlock) void k_pass1_finish_sizes(const uint32_t* sizes, uint32_t nb, uint32_t nshards,
                                                                   uint32_t n, uint32_t T, uint32_t* bounds1,
                                                                   uint32_t* tile_base2, unsigned long long* zero) {
     __shared__ uint32_t wsum[2][kFinBlock / 64];
     const uint32_t tid = threadIdx.x;
-    if (zero && tid == 0) *zero = 0;   // the on-chip probe's count (one launch fewer before it)
+    if (zero && tid < 2) zero[tid] = 0;   // the on-chip probe's {count, failed} (one launch fewer before it)
     uint32_t cx = 0, cy = 0;
     for (uint32_t base = 0; base < nb; base += kFinBlock) {
         const uint32_t d = base + tid;

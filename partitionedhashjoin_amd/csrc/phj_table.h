@@ -461,12 +461,20 @@ struct HtProbeArgs {
     PassArgs a;                  // the pass-2 tile mapping over the pass-1 output
     const uint2* desc;
     const uint64_t* table;
-    unsigned long long* count;
+    unsigned long long* count;   // {count, failed}: failed = 1 when the pass-1 error word is set
+    const uint32_t* err;         // S's pass-1 error word (chunk_err_word), or null
     uint64_t seed;
     uint64_t e1;                 // E_0 (ht_empty)
     uint32_t nb2;
     uint32_t pad;
 };
+
+// The chunked pass 1's error word folded into the count pair by the probe
+// (read after k_tile_chunks, which also reports into it).
+__device__ __forceinline__ void fold_pass1_error(const uint32_t* err, unsigned long long* count) {
+    if (err && blockIdx.x == 0 && threadIdx.x == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        atomicOr(count + 1, 1ull);
+}
 
 constexpr int kProbeBlock = 1024, kProbeItems = 4;   // 16 waves, 4 keys per lane: a 4096-key tile
 
@@ -516,9 +524,6 @@ __device__ __forceinline__ uint32_t wave_scan_counts(uint32_t* C, uint32_t nb, u
 // tile t = chunk [tile_start[t], + tile_cnt[t])). Both drop the run-time mode
 // branches and the kernel-argument state they keep live.
 constexpr int kProbeRadix = 1, kProbeChunked = 2;
-#ifndef PHJ_PROBE_ABL
-#define PHJ_PROBE_ABL 0   // measurement builds only: 1 = no table reads, 2 = no d2 grouping
-#endif
 
 template <int BLOCK, int ITEMS, int HK, int FORM = 0>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void k_probe_ht(HtProbeArgs pa) {
@@ -593,30 +598,18 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
                 const uint64_t h = hash64<HK>(static_cast<uint64_t>(key[i]), pa.seed);
                 key[i] = static_cast<int64_t>(h);
                 dig[i] = d2_of(h);
-                if constexpr (PHJ_PROBE_ABL == 2) rank[i] = wbase + i * 64 + lane;
-                else rank[i] = agg_rank(C, dig[i], (vm >> i) & 1u);
+                rank[i] = agg_rank(C, dig[i], (vm >> i) & 1u);
             }
             __syncthreads();   // B1
-            uint32_t cnt;
-            uint32_t pos[ITEMS];
-            if constexpr (PHJ_PROBE_ABL == 2) {   // tile order: the valid codes are a prefix
-                if (tid == 0) tot_s = 0;
-                __syncthreads();
-                if (vm) atomicMax(&tot_s, wbase + (31 - __builtin_clz(vm)) * 64 + lane + 1);
-                __syncthreads();
-                cnt = tot_s;
-#pragma unroll
-                for (int i = 0; i < ITEMS; i++) pos[i] = rank[i];
-            } else {
             if (wave == 0) {   // exclusive scan of the counts by one wave
                 const uint32_t t = wave_scan_counts(C, nb, lane);
                 if (lane == 0) tot_s = t;
             }
             __syncthreads();   // B2
-            cnt = tot_s;
+            const uint32_t cnt = tot_s;
+            uint32_t pos[ITEMS];
 #pragma unroll
             for (int i = 0; i < ITEMS; i++) pos[i] = C[dig[i]] + rank[i];
-            }
 
             // branch-free: slot T takes invalid lanes' writes (a sink)
 #pragma unroll
@@ -637,14 +630,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
             const uint64_t e0 = d1 == 0 ? pa.e1 : 0ull;   // E of partition (d1, d2): e1 only for partition 0
             const ulonglong2* tab2 = reinterpret_cast<const ulonglong2*>(pa.table);
             ulonglong2 v[ITEMS];
-            if constexpr (PHJ_PROBE_ABL == 1) {
-#pragma unroll
-                for (int i = 0; i < ITEMS; i++) {
-                    const uint32_t k = i * BLOCK + tid;
-                    const uint64_t c = k < cnt ? static_cast<uint64_t>(skey[k]) : 0ull;
-                    hits += (k < cnt && D[d2_of(c)].y != 0xdeadbeefu) ? 1u : 0u;
-                }
-            } else {
 #pragma unroll
             for (int i = 0; i < ITEMS; i++) {   // unconditional: an unused lane reads code 0's bucket
                 const uint32_t k = i * BLOCK + tid;
@@ -673,7 +658,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
                     hits += hit ? 1u : 0u;
                 }
             }
-            }
             if (!more) break;
             tile = next;
             vm = nvm;
@@ -691,6 +675,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
         for (int w = 0; w < BLOCK / 64; w++) t += red[w];
         if (t) atomicAdd(pa.count, t);
     }
+    fold_pass1_error(pa.err, pa.count);
 }
 
 // ---------------------------------------------------------------------------

@@ -1,5 +1,6 @@
 #!/bin/bash
-# A/B the C2 bench over library builds: scripts/ab_lib.sh LIB1 LIB2 ... (e.g. measurement builds with -DPHJ_PROBE_ABL=N)
+# A/B the C2 bench over library builds on one box: scripts/ab_lib.sh LIB1 LIB2 ...
+# (each LIB a libphj_hip.so built beforehand in-tree, e.g. from another commit; PHJ_LIB selects it)
 set -o pipefail
 mkdir -p gpurun_out
 i=0

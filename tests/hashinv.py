@@ -96,7 +96,7 @@ def preimage(kind_is_murmur3, code, seed):
 
 
 def table_edge_codes(num_partitions):
-    """Codes at the code tables' edges (csrc/phj_table.h): 0, 1 and 2^40 (the
+    """Codes at the code tables' edges (csrc/phj_table.h, csrc/phj_cluster.h): 0, 1 and 2^40 (the
     empty values E_p of every plan: E_p = 0 for p != 0, E_0 = 1, or 2^40 under
     h % 1), 2, 3, 2^64 - 1, and "bucket mates" of 0, 1 and 2^40: codes of the
     same final partition and the same home bucket ((c >> 24) & mask = 0),
@@ -110,4 +110,13 @@ def table_edge_codes(num_partitions):
     for b in (0, 1, 1 << 40):
         for t in ts:
             codes.add(b + ((m * t) << 50))
-    return sorted(codes)
+    # the LDS join's cluster tables (csrc/phj_cluster.h): E of cluster 0 is the
+    # plan's lowest power of two outside cluster 0 (2^(log2 P - k) for radix
+    # bits, 2^40.. under h % P with sub-partition bits): every power of two,
+    # and bucket mates of those a cluster plan can pick
+    for b in range(64):
+        codes.add(1 << b)
+    for b in list(range(0, 17)) + [40, 41, 42]:
+        for t in ts[:3]:
+            codes.add((1 << b) + ((m * t) << 50))
+    return sorted(c & M64 for c in codes)

@@ -430,3 +430,53 @@ def test_nopart_hot_build_key_overflow(ctx, ratio):
         p = phj.nopart_params(hash=hk, seed=SEED, table_ratio=ratio)
         assert ctx.join(p).matches == expect
         assert ctx.join_materialize(p).matches == expect
+
+
+# ---- the LDS join (csrc/phj_cluster.h): cluster tables in LDS, big clusters in HBM ----
+
+def _cluster_ctx(monkeypatch, **env):
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    return phj.Context(0)
+
+
+@pytest.mark.parametrize("env", [{}, {"PHJ_CL_CAP": "8192"}, {"PHJ_CL_BITS": "11"}, {"PHJ_CL_BITS": "9", "PHJ_CL_CAP": "8192"}],
+                         ids=["default", "cap8192", "bits11", "bits9-cap8192"])
+@pytest.mark.parametrize("name,params", [a for a in ALL_PARAMS if a[0].startswith("radix") and "chained" not in a[0]],
+                         ids=[a[0] for a in ALL_PARAMS if a[0].startswith("radix") and "chained" not in a[0]])
+def test_cluster_tables_lds_and_hbm(monkeypatch, env, name, params):
+    """A build side whose clusters fit the LDS table except one: a hot key
+    repeated beyond the LDS limit (its cluster's table goes to HBM,
+    k_cluster_big_fill), many keys with few repeats, the extremes and the
+    empty-value preimages of the plan; probes hit the hot cluster, the LDS
+    clusters and miss. Counted against the oracle's sort-and-search."""
+    c = _cluster_ctx(monkeypatch, **env)
+    try:
+        rng = np.random.default_rng(len(name) * 131 + len(env))
+        hk = params.hash
+        pre = [preimage(hk == phj.HASH_MURMUR3, x, params.hash_seed) for x in table_edge_codes(0)]
+        R = np.concatenate([np.full(20_000, 777, dtype=np.int64),
+                            rng.integers(-400_000, 400_000, 180_000, dtype=np.int64),
+                            np.array([0, -1, I64_MIN, I64_MAX] + pre[::2], dtype=np.int64)])
+        S = np.concatenate([np.full(30_000, 777, dtype=np.int64),
+                            rng.integers(-800_000, 800_000, 600_000, dtype=np.int64),
+                            np.array([0, -1, I64_MIN, I64_MAX, 5] + pre, dtype=np.int64)])
+        rng.shuffle(R)
+        rng.shuffle(S)
+        expect = O.semijoin_count_keys(R, S)
+        assert _gpu_count(c, R, S, params) == expect
+        assert c.join(params).matches == expect   # the buffers reused
+    finally:
+        c.close()
+
+
+def test_cluster_path_is_default_for_c2_shape(ctx):
+    """10M-scale build side at 8+8 radix bits: the join's pass 1 is the LDS
+    join's 1024 clusters (the probe-side pass-1 hook reports its digits)."""
+    nR, nS = 10_000_000, 4_000_000
+    ctx.generate_sequential(phj.SIDE_BUILD, nR, 1)
+    ctx.generate_zipf(phj.SIDE_PROBE, nS, 1.05, 1, nR, 5)
+    p = phj.radix_params((8, 8), hash=phj.HASH_MURMUR3, seed=SEED)
+    out, b1, codes = ctx.probe_pass1(p)
+    assert codes and b1.shape[0] == 1025
+    assert ctx.join(p).matches == nS

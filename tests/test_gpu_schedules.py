@@ -51,6 +51,10 @@ SCHEDULES = [
     {"PHJ_P1_WPC2": "0"},                                       # keys-only pass 1 on every LDS slot
     {"PHJ_P1_WPC2": "1"},                                       # ... on half a workgroup per CU
     {"PHJ_P1_KO_TPS": "4"},                                     # keys-only pass 1: 16 shards on small relations
+    {"PHJ_CLUSTER": "0"},                                       # radix count: code tables in HBM (k_probe_ht), not the LDS join
+    {"PHJ_CL_CAP": "8192"},                                     # LDS join: 64 KB tables, two workgroups per CU
+    {"PHJ_CL_BITS": "11"},                                      # LDS join: 2048 clusters (four digits per pass-1 thread)
+    {"PHJ_CL_BITS": "10", "PHJ_P1_KO_TPS": "4"},                # ... 1024 clusters over 16 shards
 ]
 
 CASES = [((8, 8), 0, phj.HASH_MURMUR3), ((11, 0), 0, phj.HASH_XXH3), ((1, 0), 1000, phj.HASH_XXH3),
