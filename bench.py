@@ -68,29 +68,29 @@ def probe_phase(per_step, nR, nS, ms_per_step):
     """The north star's probe-phase figure (target >= 60 % of the HBM roofline
     at 1 GPU). SURVEY.md §8(d) prices the probe phase at 16 B per R and per S
     tuple (3.36 GB at 10M⋈200M: >= 60 % means <= 0.70 ms), assuming one fused
-    build + probe kernel. Here the build (k_ht_fill, the `build` timer) runs on
-    the aux stream beside S's pass 1 and the critical path's probe phase is ONE
-    kernel, k_probe_ht: it reads S's pass-1 output (8-B hash codes) once and
-    probes the tables. The same byte count over three spans, so rounds compare
-    like for like:
-      frac_survey_def              - over k_probe_ht alone (the figure the target
-                                     is mapped to)
-      frac_survey_def_build_probe  - over build + probe kernel time summed (the
-                                     survey's fused kernel)
+    build + probe kernel. Here that is what the probe kernel is: k_cluster_probe
+    (csrc/phj_cluster.h) builds each cluster's table from R's codes in LDS and
+    probes S's pass-1 codes against it, in one launch (the `build` timer is
+    only the HBM tables of clusters beyond the LDS limit, none at C2; with
+    PHJ_CLUSTER=0 it is k_ht_fill beside S's pass 1 and the probe k_probe_ht).
+    The same byte count over three spans, so rounds compare like for like:
+      frac_survey_def              - over the probe timer alone (the figure the
+                                     target is mapped to)
+      frac_survey_def_build_probe  - over build + probe kernel time summed
       frac_survey_def_span         - over the step minus S's pass 1: the whole
                                      critical path after it (gaps, the count)
-    and frac_bytes_read: the bytes k_probe_ht reads by design (8 B per S key;
-    the tables are L2 hits) over its time."""
+    and frac_bytes_read: the bytes the probe reads by design (8 B per S code
+    and per R code) over its time."""
     if "probe" not in per_step:
         return None
     ms = per_step["probe"][0]
     if ms <= 0:
         return None
-    b_def, b_read = 16 * (nR + nS), 8 * nS
+    b_def, b_read = 16 * (nR + nS), 8 * (nS + nR)
     frac = lambda b, t: b / (t * 1e-3) / 1e9 / HBM_PEAK_GBS if t > 0 else None
     bp_ms = ms + per_step.get("build", (0.0, 0))[0]
     span_ms = ms_per_step - per_step.get("S.p1.scatter", (0.0, 0))[0]
-    return {"kernel": "k_probe_ht (probe timer alone)", "ms": ms, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+    return {"kernel": "probe timer (k_cluster_probe: LDS build + probe)", "ms": ms, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "target": "frac_survey_def >= 0.60",
             "bytes_survey_def": b_def, "achieved_survey_def": b_def / (ms * 1e-3) / 1e9,
             "frac_survey_def": frac(b_def, ms),

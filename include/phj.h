@@ -177,6 +177,16 @@ void phj_shard_range(uint64_t n, int rank, int world, uint64_t *lo, uint64_t *hi
  *    count, or PHJ_ERR_STATE when any rank failed. */
 void phj_exchange_layout(uint64_t max_shard, uint32_t num_partitions, uint64_t *codes_elems,
                          uint64_t *block_elems);
+/* The segment geometry phj_join's member step uses for radix params p and a
+ * global build side of total_build rows (default tuning): the block's codes
+ * are grouped by d(c) = (q(c) >> *shift), q = the plan's (sub-)partition
+ * number of code c (q = c & (P - 1) for radix bits; (c % P) << s | bits
+ * 40.. for h % P, s = *sub_bits; radix bits below the cluster width take
+ * *sub_bits hash bits just above them), with *num_segments + 1 bounds.
+ * *cluster = 1: the LDS join's clusters (phj_cluster.h), else the final
+ * partitions of the code tables. PHJ_ERR_INVALID for bad params. */
+int phj_exchange_geometry(const phj_join_params *p, uint64_t total_build, uint32_t *num_segments,
+                          uint32_t *shift, uint32_t *sub_bits, uint32_t *sub_shift, int *cluster);
 void phj_count_contribution(uint64_t count, int failed, uint64_t words[2]);
 int phj_count_verdict(const uint64_t words[2], uint64_t *matches);
 void phj_ctx_destroy(phj_ctx *ctx);
@@ -306,6 +316,22 @@ int phj_probe_pass1(phj_ctx *ctx, const phj_join_params *p, int64_t *keys, uint6
  * PHJ_ERR_STATE (nothing is written through a stale entry) and clears the
  * table; the join after it is exact again. Single-device ctx. */
 int phj_debug_poison_chunk_table(phj_ctx *ctx, int side, const phj_join_params *p, int byte);
+
+/* ---- test hook: a failing rank ----
+ * Replaces nothing in the reference. On a multi-device or rank context, local
+ * member `member` (-1: none) fails the next phj_join before the exchange. The
+ * protocol must still end cleanly: with the local exchange every member returns
+ * PHJ_ERR_STATE; over RCCL the failed rank sends a zeroed (valid, empty) block
+ * into the all-gather and {0, 1} into the count all-reduce, so every rank
+ * returns PHJ_ERR_STATE ("1 rank(s) failed") with no collective left waiting. */
+int phj_debug_fail_member(phj_ctx *ctx, int member);
+
+/* ---- test hook: the exchange block a member packed ----
+ * Replaces nothing in the reference. Copies local member `member`'s exchange
+ * block of the last radix phj_join (phj_exchange_layout's layout, `elems`
+ * int64) to host memory, so tests can compare the library's own pack with the
+ * protocol's definition. */
+int phj_debug_exchange_block(phj_ctx *ctx, int member, int64_t *out, uint64_t elems);
 
 #ifdef __cplusplus
 }

@@ -74,6 +74,19 @@ def exchange_layout(max_shard: int, num_partitions: int):
     return a.value, b.value
 
 
+def exchange_geometry(params: JoinParams, total_build: int):
+    """(num_segments, shift, sub_bits, sub_shift, cluster) of the member step's
+    exchange block for radix params and a global build side of total_build rows
+    (phj_exchange_geometry; host only, default tuning)."""
+    L = _capi.load()
+    n, sh, sb, ss, cl = C.c_uint32(), C.c_uint32(), C.c_uint32(), C.c_uint32(), C.c_int()
+    rc = L.phj_exchange_geometry(C.byref(params), total_build, C.byref(n), C.byref(sh), C.byref(sb), C.byref(ss),
+                                 C.byref(cl))
+    if rc != 0:
+        raise PhjError(rc, "phj_exchange_geometry: radix params required")
+    return n.value, sh.value, sb.value, ss.value, bool(cl.value)
+
+
 def count_contribution(count: int, failed: bool = False) -> np.ndarray:
     """The two uint64 words a rank adds to the count all-reduce (phj_count_contribution)."""
     L = _capi.load()
@@ -288,6 +301,18 @@ class Context:
         """Test hook (phj_debug_poison_chunk_table): leave `side`'s chunk table
         as a stale one would be (every byte = `byte`, marked clean)."""
         self._check(self._L.phj_debug_poison_chunk_table(self._h, side, C.byref(params), byte))
+
+    def debug_fail_member(self, member: int) -> None:
+        """Test hook (phj_debug_fail_member): local member `member` fails the
+        next join before the exchange (-1: none)."""
+        self._check(self._L.phj_debug_fail_member(self._h, member))
+
+    def debug_exchange_block(self, member: int, elems: int) -> np.ndarray:
+        """Test hook (phj_debug_exchange_block): local member `member`'s packed
+        exchange block of the last radix join (`elems` int64)."""
+        out = np.zeros(elems, dtype=np.int64)
+        self._check(self._L.phj_debug_exchange_block(self._h, member, out.ctypes.data_as(C.c_void_p), elems))
+        return out
 
     def hash_keys(self, kind: int, seed: int, keys) -> np.ndarray:
         keys = np.ascontiguousarray(np.asarray(keys, dtype=np.int64))

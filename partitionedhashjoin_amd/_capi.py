@@ -38,7 +38,7 @@ EXPORTED = [
     "phj_partitioned_download", "phj_hash_keys", "phj_timers_report", "phj_join_partitioned_async",
     "phj_prepare", "phj_join_materialize", "phj_joined_rows", "phj_joined_download",
     "phj_ctx_create_ex", "phj_ctx_create_device", "phj_comm_unique_id", "phj_ctx_create_rank",
-    "phj_ctx_info", "phj_shard_range", "phj_probe_pass1", "phj_debug_poison_chunk_table",
+    "phj_ctx_info", "phj_shard_range", "phj_probe_pass1", "phj_debug_poison_chunk_table", "phj_debug_fail_member", "phj_debug_exchange_block", "phj_exchange_geometry",
     "phj_exchange_layout", "phj_count_contribution", "phj_count_verdict",
 ]
 ABI_VERSION = 2
@@ -135,6 +135,9 @@ def load():
         "phj_hash_keys": (i, [P, i, u64, P, u64, P]),
         "phj_probe_pass1": (i, [P, P, P, u64, P, P, P]),
         "phj_debug_poison_chunk_table": (i, [P, i, P, i]),
+        "phj_debug_fail_member": (i, [P, i]),
+        "phj_debug_exchange_block": (i, [P, i, P, u64]),
+        "phj_exchange_geometry": (i, [P, u64, P, P, P, P, P]),
         "phj_timers_report": (i, [P, C.POINTER(JoinResult)]),
         "phj_join_partitioned_async": (i, [P, C.POINTER(JoinParams), i, C.POINTER(Partitioned), P]),
         "phj_prepare": (i, [P, C.POINTER(JoinParams)]),

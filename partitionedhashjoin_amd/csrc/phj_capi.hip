@@ -57,9 +57,11 @@ struct Tuning {
     int p1_min_tiles = 32768;  // chunked pass 1: smallest relation (in 4096-tuple tiles, ~134M tuples)
     int p1_ko_tps = 1024;      // ... the keys-only form for the on-chip probe: tiles per shard (at every size)
     int p2probe = 1;      // radix join, 2 passes: the probe side's pass 2 on-chip (k_probe_ht)
+    int p1_pipe = 0;      // keys-only pass 1: claims resolved a tile later over pre-allocated chunks (k_chunk_codes_pipe)
     int cluster = 1;      // radix join: LDS cluster tables (phj_cluster.h) when the build side's clusters fit
     int cl_cap = static_cast<int>(kClCapMax);   // ... LDS table slots (8192: two workgroups per CU, 16384: one)
     int cl_bits = 0;      // ... clusters = 2^cl_bits (0: the fewest >= 256 whose average fits the table)
+    int cl_pf = 2;        // ... probe: tiles of codes in flight ahead of the one probed (1-3)
 };
 
 int env_int(const char* name, int dflt) {
@@ -432,18 +434,7 @@ void refine_plan(const phj_ctx* c, Plan& pl, uint64_t nR) { refine_plan_sub(c, p
 // cluster fills at most 0.8 of the LDS limit (the binomial spread of the
 // cluster sizes, ~3 % at 10M / 1024); larger build sides than 2048 clusters
 // hold take the code-table path. Returns false when the plan does not apply.
-bool cluster_plan(const phj_ctx* c, const Plan& base, uint64_t nR, Plan& pl) {
-    if (!c->tune.cluster || base.chained || nR == 0 || base.P == 0) return false;
-    const uint32_t cap = static_cast<uint32_t>(c->tune.cl_cap);
-    const double fit = 0.8 * cl_lim(cap);
-    uint32_t k = 8;
-    if (c->tune.cl_bits > 0) {
-        k = static_cast<uint32_t>(c->tune.cl_bits);
-    } else {
-        while (k < kMaxDigitBits && static_cast<double>(nR) / static_cast<double>(1u << k) > fit) k++;
-    }
-    if (k < 1 || k > static_cast<uint32_t>(kMaxDigitBits) || static_cast<double>(nR) / static_cast<double>(1u << k) > fit)
-        return false;
+bool cluster_plan_k(const Plan& base, uint32_t k, Plan& pl) {
     pl = base;
     pl.cluster = true;
     pl.sub_bits = 0;
@@ -479,6 +470,18 @@ bool cluster_plan(const phj_ctx* c, const Plan& base, uint64_t nR, Plan& pl) {
     return pl.nb1 >= 2 && pl.nb1 <= static_cast<uint32_t>(kMaxBins);
 }
 
+bool cluster_plan(const phj_ctx* c, const Plan& base, uint64_t nR, Plan& pl) {
+    if (!c->tune.cluster || base.chained || nR == 0 || base.P == 0) return false;
+    const double fit = 0.8 * cl_lim(static_cast<uint32_t>(c->tune.cl_cap));
+    // h % P: the clusters are 2^shift consecutive refined partitions each, so
+    // there may be fewer than 2^k of them; every k is tried until they fit
+    const uint32_t k0 = c->tune.cl_bits > 0 ? static_cast<uint32_t>(c->tune.cl_bits) : 8;
+    const uint32_t k1 = c->tune.cl_bits > 0 ? k0 : static_cast<uint32_t>(kMaxDigitBits);
+    for (uint32_t k = k0; k <= k1; k++)
+        if (cluster_plan_k(base, k, pl) && static_cast<double>(nR) / static_cast<double>(pl.nb1) <= fit) return true;
+    return false;
+}
+
 DigitFn digit_fn(const Plan& pl, int pass) {
     DigitFn f{};
     f.seed = pl.seed;
@@ -496,6 +499,7 @@ DigitFn digit_fn(const Plan& pl, int pass) {
     }
     return f;
 }
+
 
 // E_0 of the plan's code tables (phj_table.h ht_empty): the lowest power of
 // two whose final partition is not 0. Code 0 is in partition 0 under every
@@ -558,13 +562,26 @@ int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const st
             // (two per CU at 81 KB of LDS), never more than the shard's tiles
             const uint32_t ntiles = static_cast<uint32_t>((n + T - 1) / T);
             const uint32_t per = (ntiles + a.nshards - 1) / a.nshards;
-            const size_t lds = a.keys_only ? chunk_codes_lds_bytes(T, a.nbins) : sc_lds;
+            const bool pipe = a.keys_only && c->tune.p1_pipe && BLOCK == 512 && ITEMS == 8;
+            const size_t lds = pipe ? chunk_pipe_lds_bytes(T, a.nbins) : a.keys_only ? chunk_codes_lds_bytes(T, a.nbins) : sc_lds;
             const void* kfn = nullptr;
             const int kblock = BLOCK;
             // keys only, written as hash codes (the on-chip probe): k_chunk_codes;
             // whole tuples: VAR 3, LDS-atomic ranking, 16-B LDS entries (phj_partition.h)
             // (more digits than threads: the cluster plans, 512 x 4096 only)
-            if (a.keys_only) {
+            if (a.keys_only && pipe) {
+                if constexpr (BLOCK == 512 && ITEMS == 8) {
+                    const int dpt = a.nbins > 2 * BLOCK ? 4 : a.nbins > BLOCK ? 2 : 1;
+                    if (hk == kMurmur3)
+                        kfn = dpt == 4 ? reinterpret_cast<const void*>(&k_chunk_codes_pipe<BLOCK, ITEMS, kMurmur3, 4>)
+                            : dpt == 2 ? reinterpret_cast<const void*>(&k_chunk_codes_pipe<BLOCK, ITEMS, kMurmur3, 2>)
+                                       : reinterpret_cast<const void*>(&k_chunk_codes_pipe<BLOCK, ITEMS, kMurmur3, 1>);
+                    else
+                        kfn = dpt == 4 ? reinterpret_cast<const void*>(&k_chunk_codes_pipe<BLOCK, ITEMS, kXXH3, 4>)
+                            : dpt == 2 ? reinterpret_cast<const void*>(&k_chunk_codes_pipe<BLOCK, ITEMS, kXXH3, 2>)
+                                       : reinterpret_cast<const void*>(&k_chunk_codes_pipe<BLOCK, ITEMS, kXXH3, 1>);
+                }
+            } else if (a.keys_only) {
                 if constexpr (BLOCK == 512 && ITEMS == 8) {
                     if (a.nbins > 2 * BLOCK)
                         kfn = hk == kMurmur3 ? reinterpret_cast<const void*>(&k_chunk_codes<BLOCK, ITEMS, kMurmur3, 4>)
@@ -723,7 +740,9 @@ int partition_state(phj_ctx* c, SideState& S, const char* tag, const Plan& pl, b
                          tile == tile2 &&
                          pl.nb1 <= static_cast<uint32_t>(tile_shape(c, pl.nb1).block) * (ko && tile_shape(c, pl.nb1).block == 512 && tile == 4096 ? 4u : 1u) &&
                          tile / tile_shape(c, pl.nb1).block <= 8 &&   // registers: the next tile is prefetched
-                         (3 * (static_cast<uint64_t>(n) / tile + kShards) + kShards * pl.nb1) * tile < (1ull << 32);
+                         (3 * (static_cast<uint64_t>(n) / tile + kShards) + kShards * pl.nb1) * tile < (1ull << 32) &&
+                         (!p1_only || !c->tune.p1_pipe || tile_shape(c, pl.nb1).block != 512 || tile != 4096 ||
+                          ((kPipeRes + 1) * (static_cast<uint64_t>(n) / tile + kShards) + kShards * (3ull * pl.nb1 + 1)) * tile < (1ull << 32));
     S.hcoded = chunked && ko;   // k_chunk_codes
     // chains per digit: ~kTilesPerShard tiles each, a power of two <= kShards
     uint32_t nshards = 1;
@@ -734,7 +753,9 @@ int partition_state(phj_ctx* c, SideState& S, const char* tag, const Plan& pl, b
     // unused ones are never touched), then at most per + nb1 chunks for its
     // chains' other starts (each chain wastes at most one partial chunk)
     const uint32_t per = (nt1 + nshards - 1) / nshards;
-    const uint32_t pool_stride = 3 * per + pl.nb1;
+    // (the pipelined code pass: 2 static chunks per chain, kPipeRes per tile, then its counter)
+    const bool pipe = ko && c->tune.p1_pipe && tile_shape(c, pl.nb1).block == 512 && tile == 4096;
+    const uint32_t pool_stride = pipe ? pipe_pool_stride(per, pl.nb1) : 3 * per + pl.nb1;
     const uint32_t maxch = per + 1;   // chunks of one chain (every tuple of a shard in one digit)
     const size_t slots1 = chunked ? static_cast<size_t>(nshards) * pool_stride * tile : n;
     // pass-2 tiles (bound): one partial tile per segment, or per chain when chunked
@@ -1256,8 +1277,13 @@ bool use_p2probe(const phj_ctx* c, const Plan& pl, uint64_t nS, uint64_t nR) {
 // out = the cluster plan. Needs the keys-only chunked pass 1 (512 x 4096 tiles).
 bool use_cluster(const phj_ctx* c, const Plan& pl, uint64_t nS, uint64_t nR, Plan& out) {
     (void)nS;
-    if (!c->tune.p1_chunk || pl.stable || tile_shape(c, 2048).tile != 4096 || tile_shape(c, 2048).block != 512) return false;
+    if (!c->tune.p1_chunk || pl.stable) return false;
     if (!cluster_plan(c, pl, nR, out)) return false;
+    // the chunked pass 1 runs on 512 x 4096 tiles for both of the plan's digit counts
+    for (uint32_t nb : {out.nb1, out.nb2}) {
+        const TileShape sh = tile_shape(c, nb);
+        if (sh.tile != 4096 || sh.block != 512) return false;
+    }
     return cluster_empty0(out) != 0 && 4 * nR + 2ull * out.nb1 < (1ull << 32);
 }
 
@@ -1379,7 +1405,9 @@ int probe_cluster(phj_ctx* c, const Plan& pl, SideState& PS, int nseg, const int
     }
     constexpr int B = kClBlock, I = kClItems;
     const size_t lds = static_cast<size_t>(a.cap) * 8;
-    const void* kfn = reinterpret_cast<const void*>(&k_cluster_probe<B, I>);
+    const void* kfn = c->tune.cl_pf == 1   ? reinterpret_cast<const void*>(&k_cluster_probe<B, I, 1>)
+                      : c->tune.cl_pf == 3 ? reinterpret_cast<const void*>(&k_cluster_probe<B, I, 3>)
+                                           : reinterpret_cast<const void*>(&k_cluster_probe<B, I, 2>);
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, B, lds) != hipSuccess || per_cu < 1) per_cu = 1;
     per_cu = std::max(1, std::min<int>(per_cu, static_cast<int>(160 * 1024 / (lds + 256))));
@@ -1739,8 +1767,10 @@ int ctx_create_device(int device, phj_ctx** out) {
     c->tune.timers = env_int("PHJ_TIMERS", 1) != 0;
     c->tune.p1_chunk = env_int("PHJ_P1_CHUNK", 1) != 0;
     c->tune.cluster = env_int("PHJ_CLUSTER", 1) != 0;
+    c->tune.p1_pipe = env_int("PHJ_P1_PIPE", 0) != 0;
     c->tune.cl_cap = env_int("PHJ_CL_CAP", static_cast<int>(kClCapMax)) == 8192 ? 8192 : static_cast<int>(kClCapMax);
     c->tune.cl_bits = std::max(0, std::min(kMaxDigitBits, env_int("PHJ_CL_BITS", 0)));
+    c->tune.cl_pf = std::max(1, std::min(3, env_int("PHJ_CL_PF", 2)));
     c->tune.p2probe = env_int("PHJ_P2PROBE", 1);
     c->tune.p1_slots = env_int("PHJ_P1_SLOTS", 0);
     c->tune.p1_wpc2 = std::max(0, env_int("PHJ_P1_WPC2", 2));
@@ -1835,6 +1865,23 @@ void phj_exchange_layout(uint64_t max_shard, uint32_t num_partitions, uint64_t* 
     const uint64_t cap = (max_shard + 63) / 64 * 64;   // both columns stay 16-B aligned in the gathered buffer
     if (codes_elems) *codes_elems = cap;
     if (block_elems) *block_elems = cap + (static_cast<uint64_t>(num_partitions) + 2) / 2;
+}
+
+int phj_exchange_geometry(const phj_join_params* p, uint64_t total_build, uint32_t* num_segments, uint32_t* shift,
+                          uint32_t* sub_bits, uint32_t* sub_shift, int* cluster) {
+    if (!p || p->algo != PHJ_ALGO_RADIX) return PHJ_ERR_INVALID;
+    phj_ctx tmp;   // default tuning (no device is touched)
+    Plan pl, cpl;
+    if (make_plan(&tmp, p, pl) != PHJ_OK) return PHJ_ERR_INVALID;
+    const bool cl = use_cluster(&tmp, pl, 0, total_build, cpl);
+    if (cl) pl = cpl;
+    else refine_plan(&tmp, pl, total_build);
+    if (num_segments) *num_segments = cl ? pl.nb1 : pl.Ppad;
+    if (shift) *shift = cl ? pl.shift1 : 0;
+    if (sub_bits) *sub_bits = pl.sub_bits;
+    if (sub_shift) *sub_shift = pl.sub_shift;
+    if (cluster) *cluster = cl ? 1 : 0;
+    return PHJ_OK;
 }
 
 void phj_count_contribution(uint64_t count, int failed, uint64_t* words) {
@@ -2478,6 +2525,27 @@ int phj_debug_poison_chunk_table(phj_ctx* c, int side, const phj_join_params* p,
     PHJ_HIP(c, hipMemsetAsync(S.ctab.p, byte & 0xff, S.ctab.bytes, c->stream));
     PHJ_HIP(c, hipStreamSynchronize(c->stream));
     S.ctab_dirty = false;
+    return PHJ_OK;
+}
+
+int phj_debug_fail_member(phj_ctx* c, int member) {
+    if (!c) return PHJ_ERR_INVALID;
+    if (!c->group) return set_err(c, PHJ_ERR_STATE, "phj_debug_fail_member takes a multi-device or rank context");
+    if (member < -1 || member >= c->group->nlocal()) return set_err(c, PHJ_ERR_INVALID, "no such local member");
+    c->group->fail_member = member;
+    return PHJ_OK;
+}
+
+int phj_debug_exchange_block(phj_ctx* c, int member, int64_t* out, uint64_t elems) {
+    if (!c || !out) return PHJ_ERR_INVALID;
+    if (!c->group) return set_err(c, PHJ_ERR_STATE, "phj_debug_exchange_block takes a multi-device or rank context");
+    Group& G = *c->group;
+    if (member < 0 || member >= G.nlocal()) return set_err(c, PHJ_ERR_INVALID, "no such local member");
+    const DevBuf& b = G.buf[member].send;
+    if (!b.p || b.bytes < elems * 8) return set_err(c, PHJ_ERR_STATE, "no exchange block of that size");
+    PHJ_HIP(c, hipSetDevice(G.mem[member]->device));
+    PHJ_HIP(c, hipStreamSynchronize(G.mem[member]->aux));
+    PHJ_HIP(c, hipMemcpy(out, b.p, elems * 8, hipMemcpyDeviceToHost));
     return PHJ_OK;
 }
 

@@ -137,8 +137,9 @@ __global__ __launch_bounds__(256) void k_cluster_big_fill(ClusterArgs a) {
     }
 }
 
-// The probe. LDS: the cluster table (cap slots) + a few words.
-template <int BLOCK, int ITEMS>
+// The probe. LDS: the cluster table (cap slots) + a few words. PF: tiles
+// whose codes are in flight ahead of the one probed (registers: PF * ITEMS codes).
+template <int BLOCK, int ITEMS, int PF = 1>
 __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
     constexpr int CPL = kClCapMax * 3 / 4 / BLOCK;   // R codes per lane at the limit
     extern __shared__ __attribute__((aligned(16))) uint64_t tab[];   // [cap]
@@ -155,8 +156,8 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
     const uint32_t t_hi = static_cast<uint32_t>(static_cast<uint64_t>(total) * (r8 + 1) / G);
     uint32_t hits = 0;
     if (t_lo < t_hi) {   // workgroup-uniform
-        int64_t key[ITEMS];
-        uint32_t vm = 0, d = 0;
+        int64_t key[PF + 1][ITEMS];   // [0] the tile probed, [1..PF] in flight
+        uint32_t vm[PF + 1], dq[PF + 1];
         // tile metadata 64 tiles at a time: lane i holds tile mb + i's {cluster,
         // first slot, codes} (vector loads, read out with readlane: a scalar
         // load per tile would make every later LDS wait -- lgkmcnt covers both
@@ -183,12 +184,18 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
                 m |= e < c ? (1u << i) : 0u;
             }
         };
-        load(t_lo, key, vm, d);
+#pragma unroll
+        for (int f = 0; f < PF; f++) {
+            vm[f] = 0;
+            dq[f] = 0;
+            if (t_lo + f < t_hi) load(t_lo + f, key[f], vm[f], dq[f]);
+        }
         uint32_t cur = 0xffffffffu, bmask = 0;
         bool big = false;
         uint64_t e = 0;
         const ulonglong2* tb = reinterpret_cast<const ulonglong2*>(tab);
         for (uint32_t t = t_lo;;) {
+            const uint32_t d = dq[0];
             if (d != cur) {   // workgroup-uniform: build cluster d's table
                 __syncthreads();   // every probe of the previous table is done
                 cl_runs(a, d, sseg, sptr, &sB);
@@ -228,20 +235,18 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
                 }
                 cur = d;
             }
-            const uint32_t nt = t + 1;
-            const bool more = nt < t_hi;
-            int64_t nkey[ITEMS];
-            uint32_t nvm = 0, nd = d;
-            if (more) load(nt, nkey, nvm, nd);
+            vm[PF] = 0;
+            dq[PF] = d;
+            if (t + PF < t_hi) load(t + PF, key[PF], vm[PF], dq[PF]);   // workgroup-uniform
             if (!big) {   // LDS: every item's home bucket read, then the walks
                 ulonglong2 v[ITEMS];
 #pragma unroll
-                for (int i = 0; i < ITEMS; i++) v[i] = tb[static_cast<uint32_t>(static_cast<uint64_t>(key[i]) >> kHtBucketShift) & bmask];
+                for (int i = 0; i < ITEMS; i++) v[i] = tb[static_cast<uint32_t>(static_cast<uint64_t>(key[0][i]) >> kHtBucketShift) & bmask];
 #pragma unroll
                 for (int i = 0; i < ITEMS; i++) {
-                    const uint64_t c = static_cast<uint64_t>(key[i]);
+                    const uint64_t c = static_cast<uint64_t>(key[0][i]);
                     bool hit = v[i].x == c || v[i].y == c;
-                    if ((vm >> i) & 1u) {
+                    if ((vm[0] >> i) & 1u) {
                         if (!hit && v[i].y != e) {
                             uint32_t b = static_cast<uint32_t>(c >> kHtBucketShift) & bmask;
                             for (;;) {
@@ -258,8 +263,8 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
                 const ulonglong2* g2 = reinterpret_cast<const ulonglong2*>(a.gtab + 4ull * sB + 2ull * d);
 #pragma unroll
                 for (int i = 0; i < ITEMS; i++) {
-                    if ((vm >> i) & 1u) {
-                        const uint64_t c = static_cast<uint64_t>(key[i]);
+                    if ((vm[0] >> i) & 1u) {
+                        const uint64_t c = static_cast<uint64_t>(key[0][i]);
                         uint32_t b = static_cast<uint32_t>(c >> kHtBucketShift) & bmask;
                         for (;;) {
                             const ulonglong2 w = g2[b];
@@ -273,12 +278,14 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
                     }
                 }
             }
-            if (!more) break;
+            if (++t >= t_hi) break;
 #pragma unroll
-            for (int i = 0; i < ITEMS; i++) key[i] = nkey[i];
-            vm = nvm;
-            d = nd;
-            t = nt;
+            for (int f = 0; f < PF; f++) {
+#pragma unroll
+                for (int i = 0; i < ITEMS; i++) key[f][i] = key[f + 1][i];
+                vm[f] = vm[f + 1];
+                dq[f] = dq[f + 1];
+            }
         }
     }
     uint32_t x = hits;

@@ -231,6 +231,7 @@ struct Group {
     std::vector<phj_join_result> res;   // per member, the last join
     std::atomic<int> failed{0};          // local exchange: a member failed before the barrier
     bool rehearse = false;               // PHJ_REHEARSE (local exchange): members > 0 only feed the exchange
+    int fail_member = -1;                // phj_debug_fail_member: this local member fails the next join before the exchange
     int nlocal() const { return static_cast<int>(mem.size()); }
 };
 
@@ -503,6 +504,7 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
         reset_timers(c);
         rc = member_alloc_radix(G, i, pl, p2);
     }
+    if (rc == PHJ_OK && G.fail_member == i) rc = set_err(c, PHJ_ERR_STATE, "injected failure (phj_debug_fail_member)");
     if (rc == PHJ_OK) rc = mark(c, &t0);
     // R shard, pack and all-gather on the aux stream (S goes beside them);
     // a rehearsal's members > 0 pack their (unchanging) block once and from
@@ -676,6 +678,7 @@ int member_nopart(Group& G, int i, const phj_join_params* p, phj_join_result* r,
     if (rc == PHJ_OK) rc = ensure(c, B.cnt, cnt_bytes(G));
     if (rc == PHJ_OK && !B.packed && hipEventCreateWithFlags(&B.packed, hipEventDisableTiming) != hipSuccess)
         rc = set_err(c, PHJ_ERR_HIP, "hipEventCreate");
+    if (rc == PHJ_OK && !dry && G.fail_member == i) rc = set_err(c, PHJ_ERR_STATE, "injected failure (phj_debug_fail_member)");
     auto* full = static_cast<phj_tuple*>(B.full.p);
     if (dry) {
         PHJ_TRY(rc);
@@ -786,6 +789,13 @@ int group_join(phj_ctx* shell, const phj_join_params* p, phj_join_result* r, boo
     Group& G = *shell->group;
     G.res.assign(G.nlocal(), phj_join_result{});
     G.failed.store(0);
+    struct FailOnce {   // an injected failure applies to one join
+        Group& G;
+        bool dry;
+        ~FailOnce() {
+            if (!dry) G.fail_member = -1;
+        }
+    } once{G, dry};
     if (p->algo == PHJ_ALGO_NO_PARTITIONING) {
         if (total(G.n[PHJ_SIDE_BUILD]) == 0)   // LinearProbing.hpp:295-299
             return set_err(shell, PHJ_ERR_INVALID,

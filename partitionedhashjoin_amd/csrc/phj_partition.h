@@ -1071,6 +1071,279 @@ void k_chunk_codes(PassArgs a, uint32_t ntiles, uint32_t per) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// Pipelined code pass (k_chunk_codes_pipe): k_chunk_codes with the claims of
+// tile t resolved in the next iteration, beside the hashing and ranking of
+// tile t + slots, so the cursor round trip is never waited for (one workgroup
+// per CU spent ~1.5 us of every ~7 us tile on it). That needs chunk ids known
+// before the runs that use them are resolved, so the chunks are
+// PRE-ALLOCATED: chunks 0 and 1 of chain (x, d) are static, and the run that
+// starts chunk j (the one holding its first slot) takes chunk j + 1's id and
+// publishes it, with the chain's hint {j, id_j, id_j+1}; a run in chunk k
+// finds id_k in the hint it loaded with its claim (hint chunk k or k - 1) and
+// else in the chunk table, published one chunk earlier. A run's resolution
+// waits only on claims strictly earlier in its chain (publishes first, then
+// waits), so it always ends.
+// Pool of shard x (pipe_pool_stride chunks): [0, 2 nb) chunks 0, 1 of each
+// chain; then kPipeRes chunks per tile of the shard (the ids its starting
+// runs take); then the shard's pool counter.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kPipeRes = 3;
+__host__ __device__ constexpr uint32_t pipe_pool_stride(uint32_t per, uint32_t nb) {
+    return 2 * nb + kPipeRes * per + per + nb + 1;
+}
+// hint word: chunk index j (20 bits) | id_j - pool base (22) | id_j+1 - pool base (22)
+__device__ __forceinline__ unsigned long long pipe_hint(uint32_t j, uint32_t rid, uint32_t rid1) {
+    return (static_cast<unsigned long long>(j) << 44) | (static_cast<unsigned long long>(rid) << 22) | rid1;
+}
+
+__host__ __device__ constexpr size_t chunk_pipe_lds_bytes(int T, uint32_t nb) {
+    return 2 * static_cast<size_t>(T) * 8 + (static_cast<size_t>(2 * nb + 3) / 4 * 4 + 2 * 4 * static_cast<size_t>(nb)) * 4 + 128;
+}
+
+template <int BLOCK, int ITEMS, int HK, int DPT = 1>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(BLOCK / 256)))   // one workgroup per CU (LDS): the registers of two
+void k_chunk_codes_pipe(PassArgs a, uint32_t ntiles, uint32_t per) {
+    constexpr int NW = BLOCK / 64;
+    constexpr int T = BLOCK * ITEMS;
+    static_assert(NW <= 16, "scan words [0, NW) below the reservation words");
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t nb = a.nbins;   // host: nb <= DPT * BLOCK
+    int64_t* sbuf = reinterpret_cast<int64_t*>(smem);                       // [2][T] sorted codes
+    uint32_t* wcnt = reinterpret_cast<uint32_t*>(sbuf + 2 * T);             // [2][nb] counter rows
+    uint4* wdesc = reinterpret_cast<uint4*>(wcnt + (2 * nb + 3u) / 4 * 4);  // [2][nb] {k < split: slot - k, else, split}
+    uint32_t* tmp = reinterpret_cast<uint32_t*>(wdesc + 2 * nb);            // [0, NW) scan; 16-19 reservations [2]; 20 bad tile
+
+    const uint32_t x = blockIdx.x % a.nshards, slots = gridDim.x / a.nshards;
+    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const uint32_t t_end = min(ntiles, (x + 1) * per);
+    uint32_t tile = x * per + blockIdx.x / a.nshards;
+    if (tile >= t_end) return;
+    const uint32_t wbase = wave * 64 * ITEMS;
+    uint32_t* curs = a.chunk_cursor + static_cast<size_t>(x) * nb;
+    uint32_t* pool = a.chunk_cursor + chunk_pool_word(nb, x);
+    uint32_t* errw = a.chunk_cursor + chunk_err_word(nb);
+    unsigned long long* hints = reinterpret_cast<unsigned long long*>(a.chunk_cursor + chunk_hint_word(nb)) + static_cast<size_t>(x) * nb;
+    const uint32_t id_lo = x * a.pool_stride, id_hi = id_lo + a.pool_stride;
+    const bool pow2q = a.f.mode == 0 && a.f.sub_bits == 0;
+    auto code_digit = [&](uint64_t h, auto pow2) -> uint32_t {
+        if constexpr (decltype(pow2)::value) return static_cast<uint32_t>((h & (a.f.P - 1)) >> a.f.shift) & a.f.dmask;
+        else return static_cast<uint32_t>(q_from_hash(h, a.f) >> a.f.shift) & a.f.dmask;
+    };
+    int64_t* const ssink = reinterpret_cast<int64_t*>(a.sink + static_cast<size_t>(blockIdx.x % kSinkGroups) * BLOCK + tid);
+
+    int64_t key[ITEMS];
+    const longlong2* rel = reinterpret_cast<const longlong2*>(a.in_keys);
+    auto load = [&](uint32_t t) {
+        const uint32_t lo = t * T;
+#pragma unroll
+        for (int i = 0; i < ITEMS; i++) {
+            const uint32_t ix = min(lo + wbase + i * 64 + lane, a.n - 1);
+            if (a.nt_load) key[i] = __builtin_nontemporal_load(&rel[ix].x);
+            else key[i] = rel[ix].x;
+        }
+    };
+
+    for (uint32_t i = tid; i < 2 * nb; i += BLOCK) wcnt[i] = 0;
+    load(tile);
+    {
+#pragma unroll
+        for (int i = 0; i < ITEMS; i++) {
+            __hip_atomic_store(ssink, 0ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __asm__ volatile("" ::: "memory");
+        }
+    }
+    __syncthreads();
+    // the previous tile's claims, resolved in this iteration
+    uint32_t pv0[DPT], pc[DPT], pds[DPT];
+    unsigned long long phint[DPT];
+#pragma unroll
+    for (int j = 0; j < DPT; j++) {
+        pv0[j] = 0;
+        pc[j] = 0;
+        pds[j] = 0;
+        phint[j] = 0;
+    }
+    bool have_prev = false;
+    uint32_t pcnt = 0, par = 0;
+    const uint32_t d0 = tid * DPT;
+    for (;;) {
+        const bool live = tile < t_end;   // workgroup-uniform; false: the drain of the last tile
+        uint32_t* const crow = wcnt + par * nb;
+        const uint32_t cnt = live ? min(static_cast<uint32_t>(T), a.n - tile * T) : 0u;
+        const uint32_t next = tile + slots;
+        int64_t code[ITEMS];
+        uint32_t dig[ITEMS], rank[ITEMS];
+        if (live) {
+            auto hash_all = [&](auto pow2) {
+#pragma unroll
+                for (int i = 0; i < ITEMS; i++) {
+                    const uint64_t h = hash64<HK>(static_cast<uint64_t>(key[i]), a.f.seed);
+                    code[i] = static_cast<int64_t>(h);
+                    dig[i] = wbase + i * 64 + lane < cnt ? code_digit(h, pow2) : 0u;
+                }
+            };
+            if (pow2q) hash_all(std::true_type{});
+            else hash_all(std::false_type{});
+            load(next < t_end ? next : tile);
+#pragma unroll
+            for (int i = 0; i < ITEMS; i++) rank[i] = atomicAdd(&crow[dig[i]], wbase + i * 64 + lane < cnt ? 1u : 0u);
+        }
+        __syncthreads();   // B1: ranks counted
+        uint32_t c[DPT], ds[DPT], v0[DPT];
+        unsigned long long hint[DPT];
+        {
+            uint32_t local = 0;
+#pragma unroll
+            for (int j = 0; j < DPT; j++) {
+                c[j] = live && d0 + j < nb ? crow[d0 + j] : 0u;
+                local += c[j];
+            }
+            uint32_t total;
+            uint32_t run = block_exclusive_scan_t<NW, false>(local, tmp, total);
+#pragma unroll
+            for (int j = 0; j < DPT; j++) {
+                ds[j] = run;
+                if (live && d0 + j < nb) crow[d0 + j] = run;
+                run += c[j];
+                v0[j] = 0;
+                hint[j] = 0;
+            }
+            if (live) {   // claims of every digit (0 adds too): resolved next iteration
+#pragma unroll
+                for (int j = 0; j < DPT; j++) {
+                    const uint32_t d = min(d0 + j, nb - 1);
+                    v0[j] = atomicAdd(curs + d, d0 + j < nb ? c[j] : 0u);
+                    hint[j] = __hip_atomic_load(hints + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            if (tid == 0) {
+                if (live) {
+                    tmp[16 + 2 * par] = id_lo + 2 * nb + kPipeRes * (tile - x * per);   // this tile's reserved chunks
+                    tmp[17 + 2 * par] = 0;
+                }
+                tmp[20] = 0;
+            }
+        }
+        __syncthreads();   // B2: tile-local starts, reservations
+        if (live) {
+            uint32_t base[ITEMS];
+#pragma unroll
+            for (int i = 0; i < ITEMS; i++) base[i] = crow[dig[i]];
+#pragma unroll
+            for (int i = 0; i < ITEMS; i++)
+                if (wbase + i * 64 + lane < cnt) sbuf[par * T + base[i] + rank[i]] = code[i];
+        }
+        const uint32_t pp = par ^ 1u;   // the previous tile's buffers
+        // the next tile's counter row: the previous tile's, no longer read
+        for (uint32_t i = tid; i < nb; i += BLOCK) wcnt[pp * nb + i] = 0;
+        if (have_prev) {
+            uint32_t bad = 0;
+            uint32_t st[DPT], nid[DPT];   // chunk this run starts (or ~0u) and the id it took for st + 1
+            // phase 1: publish (no waits)
+#pragma unroll
+            for (int j = 0; j < DPT; j++) {
+                st[j] = 0xffffffffu;
+                nid[j] = 0;
+                if (!pc[j]) continue;
+                const uint32_t d = d0 + j;
+                const uint32_t off = pv0[j] % T, k0 = pv0[j] / T, k1 = (pv0[j] + pc[j] - 1) / T;
+                if (off == 0) st[j] = k0;
+                else if (k1 != k0) st[j] = k1;
+                if (st[j] == 0xffffffffu) continue;
+                unsigned long long* tab = a.chunk_tab + (static_cast<size_t>(x) * nb + d) * a.maxch;
+                const uint32_t s0 = id_lo + 2 * d;   // static chunks 0, 1 of the chain
+                if (st[j] == 0) {
+                    nid[j] = s0 + 1;
+                    if (a.maxch >= 2) {
+                        __hip_atomic_store(&tab[0], kPublished | s0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(&tab[1], kPublished | (s0 + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    } else {
+                        bad |= kChunkErrIndex;
+                    }
+                } else {
+                    const uint32_t r = atomicAdd(&tmp[17 + 2 * pp], 1u);
+                    nid[j] = r < kPipeRes ? tmp[16 + 2 * pp] + r : id_lo + 2 * nb + kPipeRes * per + atomicAdd(pool, 1u);
+                    // (a chain's last possible chunk needs no successor)
+                    if (st[j] + 1 < a.maxch)
+                        __hip_atomic_store(&tab[st[j] + 1], kPublished | nid[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            // phase 2: resolve the ids of the chunks each run writes
+#pragma unroll
+            for (int j = 0; j < DPT; j++) {
+                if (!pc[j]) continue;
+                const uint32_t d = d0 + j;
+                const uint32_t off = pv0[j] % T, k0 = pv0[j] / T, k1 = (pv0[j] + pc[j] - 1) / T;
+                unsigned long long* tab = a.chunk_tab + (static_cast<size_t>(x) * nb + d) * a.maxch;
+                const uint32_t s0 = id_lo + 2 * d;
+                const uint32_t hk = static_cast<uint32_t>(phint[j] >> 44);
+                const uint32_t hid = phint[j] ? id_lo + (static_cast<uint32_t>(phint[j] >> 22) & 0x3fffffu) : s0;
+                const uint32_t hid1 = phint[j] ? id_lo + (static_cast<uint32_t>(phint[j]) & 0x3fffffu) : s0 + 1;
+                auto id_of = [&](uint32_t k) -> uint32_t {
+                    if (k == 0) return s0;
+                    if (k == 1) return s0 + 1;
+                    if (k == hk) return hid;
+                    if (k == hk + 1) return hid1;
+                    if (k >= a.maxch) {
+                        bad |= kChunkErrIndex;
+                        return id_lo;
+                    }
+                    unsigned long long v;
+                    while (((v = __hip_atomic_load(&tab[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) == 0)
+                        __builtin_amdgcn_s_sleep(2);
+                    return static_cast<uint32_t>(v);
+                };
+                const uint32_t id0 = id_of(k0);
+                const uint32_t id1 = k1 != k0 ? id_of(k1) : id0;
+                if (st[j] != 0xffffffffu && st[j] != 0) {
+                    const uint32_t ids = st[j] == k0 ? id0 : id1;
+                    atomicMax(hints + d, pipe_hint(st[j], ids - id_lo, nid[j] - id_lo));
+                }
+                if (id0 < id_lo || id0 >= id_hi || id1 < id_lo || id1 >= id_hi || nid[j] >= id_hi) bad |= kChunkErrId;
+                const uint32_t split = pds[j] + (T - off);
+                wdesc[pp * nb + d] = make_uint4(id0 * T + off - pds[j], id1 * T - split, split, 0u);
+            }
+            if (bad) {
+                tmp[20] = 1;
+                atomicOr(errw, bad);
+            }
+        }
+        __syncthreads();   // B3: the previous tile's slots, this tile sorted
+        if (have_prev) {
+            const uint32_t lim = tmp[20] ? 0u : pcnt;
+            auto write_out = [&](auto pow2) {
+                int64_t v[ITEMS];
+                uint32_t o[ITEMS];
+#pragma unroll
+                for (int i = 0; i < ITEMS; i++) v[i] = sbuf[pp * T + i * BLOCK + tid];
+#pragma unroll
+                for (int i = 0; i < ITEMS; i++) {
+                    const uint32_t k = i * BLOCK + tid;
+                    const uint4 w = wdesc[pp * nb + code_digit(static_cast<uint64_t>(v[i]), pow2)];
+                    o[i] = (k < w.z ? w.x : w.y) + k;
+                }
+#pragma unroll
+                for (int i = 0; i < ITEMS; i++) *(i * BLOCK + tid < lim ? a.out_keys + o[i] : ssink) = v[i];
+            };
+            if (pow2q) write_out(std::true_type{});
+            else write_out(std::false_type{});
+        }
+        if (!live) return;
+#pragma unroll
+        for (int j = 0; j < DPT; j++) {
+            pv0[j] = v0[j];
+            pc[j] = c[j];
+            pds[j] = ds[j];
+            phint[j] = hint[j];
+        }
+        pcnt = cnt;
+        have_prev = true;
+        tile = next;
+        par ^= 1u;
+    }
+}
+
 constexpr int kScanItems = 16;
 constexpr int kScanBlockElems = kBlock * kScanItems;  // 4096
 
@@ -1243,7 +1516,8 @@ __global__ __launch_bounds__(kBlock) void k_tile_seg(const uint32_t* tile_base, 
 // reads chain (s, x')'s size for the chain's first tile, then the lanes write
 // the chain's chunks. An entry that is not published or names a chunk outside
 // shard x's pool (a stale table) becomes an empty tile and sets the pass's
-// error word (the consumers read no slot through it).
+// error word (the consumers read no slot through it). Entry nch (the chunk
+// k_chunk_codes_pipe pre-allocates after a chain's last one) is cleared too.
 __global__ __launch_bounds__(kBlock) void k_tile_chunks(const uint32_t* tile_base, uint32_t* sizes,
                                                         uint32_t nseg, uint32_t nshards,
                                                         unsigned long long* chunk_tab, uint32_t maxch,
@@ -1270,6 +1544,8 @@ __global__ __launch_bounds__(kBlock) void k_tile_chunks(const uint32_t* tile_bas
         if (!ok) bad |= kChunkErrTable;
         if (k < maxch) tab[k] = 0;   // the next pass starts from an all-zero table (kPublished)
     }
+    // the pipelined pass pre-allocates the chunk after a chain's last one
+    if (lane == 0 && nch < maxch) tab[nch] = 0;
     if (bad) atomicOr(sizes + chunk_err_word(nseg), bad);
 }
 

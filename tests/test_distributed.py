@@ -8,9 +8,15 @@ which phj_group.h itself calls and these tests drive through the C ABI:
     partition order | zero padding | bounds[P + 1] (uint32);
   * phj_count_contribution / phj_count_verdict: the {count, failed} words of
     the count all-reduce and the global count (or PHJ_ERR_STATE) they give.
-Each rank's partitioned codes and its table probe come from the oracle (test
-infrastructure): this checks that blocks packed and read by the library's
-layout carry every rank's build side intact, that the reduction counts what
+Each rank's packed block is built by tests/exchange_proto.py from the oracle's
+hash codes by the library's rules (phj_exchange_geometry: the segments --
+the LDS join's clusters or the final partitions; phj_exchange_layout: the
+block), and its table probe is the oracle's (test infrastructure). So only
+the geometry, the layout arithmetic and the count reduction are the library's
+here; the library's own pack (the device step) is compared with the same
+restatement by tests/test_gpu_multirank.py::test_member_pack_matches_protocol.
+This checks that blocks packed and read by those rules carry every rank's
+build side intact, that the reduction counts what
 the reference counts (the semi-join, src/RadixCluster/HashJoin.hpp:295-301),
 and that one failed rank (an all-zero block, failed word 1) makes every rank
 report the failure while its block still reads as a valid empty segment.
@@ -26,6 +32,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import partitionedhashjoin_amd as phj
+import exchange_proto as X
 from oracle import oracle as O
 
 
@@ -35,38 +42,6 @@ def _tables(nR, nS, alpha, seed):
     return R, S
 
 
-def _geometry(p):
-    if p.num_partitions:
-        return int(p.num_partitions), False
-    return 1 << (p.radix_bits[0] + p.radix_bits[1]), True
-
-
-def _part_of_codes(codes, P, radix):
-    u = codes.view(np.uint64)
-    return (u & np.uint64(P - 1)) if radix else (u % np.uint64(P))
-
-
-def _pack(R_shard, params, codes_elems, block_elems):
-    """This rank's exchange block: R's codes in partition order, bounds after."""
-    P, radix = _geometry(params)
-    kind = O.HASH_MURMUR3 if params.hash == phj.HASH_MURMUR3 else O.HASH_XXH3
-    out, bounds = O.partition(R_shard, P, radix, kind, params.hash_seed, workers=1)
-    block = np.zeros(block_elems, dtype=np.int64)
-    block[:out.shape[0]] = O.hash_keys(kind, out[:, 0], params.hash_seed).view(np.int64)
-    block[codes_elems:].view(np.uint32)[:P + 1] = bounds.astype(np.uint32)
-    return block
-
-
-def _segments(recv, world, P, codes_elems, block_elems):
-    """The gathered blocks as build segments (codes, bounds), as phj_group.h reads them."""
-    segs = []
-    for g in range(world):
-        blk = recv[g * block_elems:(g + 1) * block_elems]
-        b = blk[codes_elems:].view(np.uint32)[:P + 1].astype(np.int64)
-        segs.append((blk[:b[P]], b))
-    return segs
-
-
 def _worker(rank, world, port, nR, nS, alpha, seed, bits, nparts, fail_rank, out):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -74,7 +49,7 @@ def _worker(rank, world, port, nR, nS, alpha, seed, bits, nparts, fail_rank, out
     try:
         R, S = _tables(nR, nS, alpha, seed)
         params = phj.radix_params(bits, num_partitions=nparts, hash=phj.HASH_MURMUR3, seed=1234)
-        P, radix = _geometry(params)
+        P, segment_of = X.geometry(params, nR)   # the library's segments: clusters or final partitions
         rlo, rhi = phj.shard_range(nR, rank, world)
         slo, shi = phj.shard_range(nS, rank, world)
         # every rank's real shard size first (phj_group.h exchange_sizes)
@@ -82,15 +57,15 @@ def _worker(rank, world, port, nR, nS, alpha, seed, bits, nparts, fail_rank, out
         dist.all_gather_into_tensor(sizes, torch.tensor([rhi - rlo], dtype=torch.int64))
         codes_elems, block_elems = phj.exchange_layout(int(sizes.max()), P)
         failed = rank == fail_rank
-        send = np.zeros(block_elems, dtype=np.int64) if failed else _pack(R[rlo:rhi], params, codes_elems, block_elems)
+        send = np.zeros(block_elems, dtype=np.int64) if failed else X.pack(R[rlo:rhi], params, nR, codes_elems, block_elems)
         recv = torch.zeros(world * block_elems, dtype=torch.int64)
         dist.all_gather_into_tensor(recv, torch.from_numpy(send))
-        segs = _segments(recv.numpy(), world, P, codes_elems, block_elems)
+        segs = X.segments(recv.numpy(), world, P, codes_elems, block_elems)
         for g, (codes, b) in enumerate(segs):
-            # partition-major with consistent bounds; a failed rank's block is empty
+            # segment-major with consistent bounds; a failed rank's block is empty
             assert b[0] == 0 and np.all(np.diff(b) >= 0)
             assert codes.shape[0] == (0 if g == fail_rank else int(sizes[g]))
-            assert np.array_equal(_part_of_codes(codes, P, radix).astype(np.int64), np.repeat(np.arange(P), np.diff(b)))
+            assert np.array_equal(segment_of(codes), np.repeat(np.arange(P), np.diff(b)))
         kind = O.HASH_MURMUR3
         build = np.concatenate([c for c, _ in segs])
         local = O.semijoin_count_keys(build, O.hash_keys(kind, S[slo:shi, 0], 1234).view(np.int64))

@@ -127,3 +127,66 @@ def test_rehearsal_member_zero_joins_its_shard(monkeypatch):
         p = phj.radix_params((8, 8), hash=phj.HASH_MURMUR3, seed=SEED)
         for _ in range(3):   # members > 0 pack once, then only take part in the exchange
             assert g.join(p).matches == expect
+
+
+PHJ_ERR_STATE = -4
+
+
+@pytest.mark.parametrize("name,p", PARAMS, ids=[a for a, _ in PARAMS])
+@pytest.mark.parametrize("world", [2, 3])
+def test_local_group_member_failure(world, name, p):
+    """A member that fails before the exchange (phj_debug_fail_member): every
+    member returns PHJ_ERR_STATE through the local exchange's barrier, no
+    fault, and the next join is exact."""
+    nR, nS, off = 200_003, 2_000_003, 1_000
+    with phj.Context(devices=[0] * world, flags=phj.CTX_LOCAL) as g:
+        expect = _generate(g, nR, nS, 1.05, off)
+        assert g.join(p).matches == expect
+        g.debug_fail_member(world - 1)
+        with pytest.raises(phj.PhjError) as e:
+            g.join(p)
+        assert e.value.code == PHJ_ERR_STATE
+        assert g.join(p).matches == expect
+
+
+@pytest.mark.parametrize("name,p", PARAMS, ids=[a for a, _ in PARAMS])
+def test_rccl_world_of_one_failed_rank(name, p):
+    """The RCCL failure branch on a world of one: the failed rank still takes
+    part in the all-gather with a zeroed block (a valid empty segment) and in
+    the count all-reduce with {0, 1}; the join returns PHJ_ERR_STATE, the
+    communicator stays usable, the next join is exact."""
+    nR, nS, off = 200_003, 2_000_003, 1_000
+    with phj.Context(devices=[0], flags=phj.CTX_EXCHANGE) as g:
+        expect = _generate(g, nR, nS, 1.05, off)
+        assert g.join(p).matches == expect
+        g.debug_fail_member(0)
+        with pytest.raises(phj.PhjError) as e:
+            g.join(p)
+        assert e.value.code == PHJ_ERR_STATE
+        assert g.join(p).matches == expect
+        assert g.join(p).matches == expect
+
+
+@pytest.mark.parametrize("name,p", PARAMS[:2], ids=[a for a, _ in PARAMS[:2]])
+@pytest.mark.parametrize("world", [2, 3])
+def test_member_pack_matches_protocol(world, name, p):
+    """The library's own exchange blocks (the device pack of each member,
+    phj_debug_exchange_block) against the protocol's restatement
+    (tests/exchange_proto.py, the same pack tests/test_distributed.py runs over
+    gloo): layout, bounds and each segment's codes."""
+    import exchange_proto as X
+    R, S = O.generate_tables(300_007, 2_000_003, 1.05, 13, threads=4)
+    R[:, 0] = R[:, 0] * 7919 - 3   # spread keys: no structure in the codes
+    nR = R.shape[0]
+    with phj.Context(devices=[0] * world, flags=phj.CTX_LOCAL) as g:
+        g.upload(phj.SIDE_BUILD, R)
+        g.upload(phj.SIDE_PROBE, S)
+        g.join(p)
+        nseg, _ = X.geometry(p, nR)
+        maxn = max(hi - lo for lo, hi in (shard_range(nR, r, world) for r in range(world)))
+        ce, be = phj.exchange_layout(maxn, nseg)
+        for r in range(world):
+            lo, hi = shard_range(nR, r, world)
+            want = X.pack(R[lo:hi], p, nR, ce, be)
+            got = g.debug_exchange_block(r, be)
+            assert X.same_block(got, want, nseg, ce), (r, name)
