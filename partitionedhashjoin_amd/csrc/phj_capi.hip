@@ -57,7 +57,7 @@ struct Tuning {
     int p1_min_tiles = 32768;  // chunked pass 1: smallest relation (in 4096-tuple tiles, ~134M tuples)
     int p1_ko_tps = 1024;      // ... the keys-only form for the on-chip probe: tiles per shard (at every size)
     int p2probe = 1;      // radix join, 2 passes: the probe side's pass 2 on-chip (k_probe_ht)
-    int p1_pipe = 0;      // keys-only pass 1: claims resolved a tile later over pre-allocated chunks (k_chunk_codes_pipe)
+    int p1_pipe = 1;      // keys-only pass 1: claims resolved a tile later over pre-allocated chunks (k_chunk_codes_pipe)
     int cluster = 1;      // radix join: LDS cluster tables (phj_cluster.h) when the build side's clusters fit
     int cl_cap = static_cast<int>(kClCapMax);   // ... LDS table slots (8192: two workgroups per CU, 16384: one)
     int cl_bits = 0;      // ... clusters = 2^cl_bits (0: the fewest >= 256 whose average fits the table)
@@ -1767,7 +1767,7 @@ int ctx_create_device(int device, phj_ctx** out) {
     c->tune.timers = env_int("PHJ_TIMERS", 1) != 0;
     c->tune.p1_chunk = env_int("PHJ_P1_CHUNK", 1) != 0;
     c->tune.cluster = env_int("PHJ_CLUSTER", 1) != 0;
-    c->tune.p1_pipe = env_int("PHJ_P1_PIPE", 0) != 0;
+    c->tune.p1_pipe = env_int("PHJ_P1_PIPE", 1) != 0;
     c->tune.cl_cap = env_int("PHJ_CL_CAP", static_cast<int>(kClCapMax)) == 8192 ? 8192 : static_cast<int>(kClCapMax);
     c->tune.cl_bits = std::max(0, std::min(kMaxDigitBits, env_int("PHJ_CL_BITS", 0)));
     c->tune.cl_pf = std::max(1, std::min(3, env_int("PHJ_CL_PF", 2)));

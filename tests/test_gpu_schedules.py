@@ -57,8 +57,8 @@ SCHEDULES = [
     {"PHJ_CL_BITS": "10", "PHJ_P1_KO_TPS": "4"},                # ... 1024 clusters over 16 shards
     {"PHJ_CL_PF": "1"},                                         # LDS join probe: one tile of codes in flight
     {"PHJ_CL_PF": "3"},                                         # ... three tiles
-    {"PHJ_P1_PIPE": "1"},                                       # keys-only pass 1 resolving its claims a tile later (pre-allocated chunks)
-    {"PHJ_P1_PIPE": "1", "PHJ_CL_BITS": "11"},                  # ... with four digits per thread
+    {"PHJ_P1_PIPE": "0"},                                       # keys-only pass 1 resolving its claims in the same tile
+    {"PHJ_P1_PIPE": "0", "PHJ_CL_BITS": "11"},                  # ... with four digits per thread
 ]
 
 CASES = [((8, 8), 0, phj.HASH_MURMUR3), ((11, 0), 0, phj.HASH_XXH3), ((1, 0), 1000, phj.HASH_XXH3),
