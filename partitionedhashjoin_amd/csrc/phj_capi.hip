@@ -61,7 +61,8 @@ struct Tuning {
     int cluster = 1;      // radix join: LDS cluster tables (phj_cluster.h) when the build side's clusters fit
     int cl_cap = static_cast<int>(kClCapMax);   // ... LDS table slots (8192: two workgroups per CU, 16384: one)
     int cl_bits = 0;      // ... clusters = 2^cl_bits (0: the fewest >= 256 whose average fits the table)
-    int cl_pf = 2;        // ... probe: tiles of codes in flight ahead of the one probed (1-3)
+    int cl_pf = 3;        // ... probe: register buffers of tile codes (1-3): PF - 1 tiles in flight beside the one probed
+    bool cl_pre = true;   // ... probe: the next cluster's R codes prefetched during this cluster's tiles
 };
 
 int env_int(const char* name, int dflt) {
@@ -162,6 +163,7 @@ struct phj_ctx {
     hipStream_t last_ev_stream = nullptr;  // ... on this stream ...
     uint32_t since_ev = 0;             // ... and the kernels launched since
     unsigned long long* count_host = nullptr;   // pinned: the count read back
+    unsigned long long* split_words = nullptr;  // the LDS probe's {build, probe} clocks (count buffer words 2-3), this join
 };
 
 namespace {
@@ -288,13 +290,15 @@ void reset_timers(phj_ctx* c) {
     c->timers.clear();
     c->evnext = 0;
     c->last_ev = nullptr;
+    c->split_words = nullptr;
     if (c->split.p) (void)hipMemsetAsync(c->split.p, 0, 16, c->ks);
 }
 
 // Build share of the fused join launches since the last reset (wave clocks).
 double fused_build_fraction(phj_ctx* c) {
     unsigned long long cyc[2] = {0, 0};
-    if (!c->split.p || hipMemcpyAsync(cyc, c->split.p, 16, hipMemcpyDeviceToHost, c->ks) != hipSuccess ||
+    const void* src = c->split_words ? static_cast<const void*>(c->split_words) : c->split.p;
+    if (!src || hipMemcpyAsync(cyc, src, 16, hipMemcpyDeviceToHost, c->ks) != hipSuccess ||
         hipStreamSynchronize(c->ks) != hipSuccess)
         return 0.5;
     const double t = static_cast<double>(cyc[0]) + static_cast<double>(cyc[1]);
@@ -829,7 +833,7 @@ int partition_state(phj_ctx* c, SideState& S, const char* tag, const Plan& pl, b
     uint32_t* tb2 = pl.npass == 2 ? static_cast<uint32_t*>(S.tbase2.p) : nullptr;
     PHJ_TRY(launch_pass(c, pl.hk, true, p1_aos, a, nt1, std::string(tag) + ".p1", n, nt1 * pl.nb1));
     if (chunked) {
-        hipLaunchKernelGGL(k_pass1_finish_sizes, dim3(1), dim3(kFinBlock), 0, c->ks, a.chunk_cursor, pl.nb1, nshards, n, tile2,
+        hipLaunchKernelGGL(k_pass1_finish_sizes, dim3(1), dim3(kFinSizesBlock), 0, c->ks, a.chunk_cursor, pl.nb1, nshards, n, tile2,
                            static_cast<uint32_t*>(S.bounds1.p), tb2, zero);
         PHJ_LAUNCHED(c, "k_pass1_finish_sizes");
     } else {
@@ -942,7 +946,7 @@ int build_and_probe(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned*
         // fused per-partition join with LDS tables: HashJoin.hpp:267-303
         const size_t nslots = nS / kFusedChunk + P + 1;
         PHJ_TRY(ensure(c, c->fitems, nslots * sizeof(FusedItem)));
-        PHJ_TRY(ensure(c, c->count, 16));
+        PHJ_TRY(ensure(c, c->count, 32));
         if (!c->split.p) {
             PHJ_TRY(ensure(c, c->split, 16));
             PHJ_HIP(c, hipMemsetAsync(c->split.p, 0, 16, c->ks));
@@ -993,7 +997,7 @@ int build_and_probe(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned*
         PHJ_TRY(ensure(c, c->np_tab, nbk_bound * sizeof(NPBucket)));
         PHJ_TRY(ensure(c, c->np_pays, nbk_bound * kNPSlots * 8));
         PHJ_TRY(ensure(c, c->prep, (static_cast<size_t>(P) + 1) * 4));
-        PHJ_TRY(ensure(c, c->count, 16));
+        PHJ_TRY(ensure(c, c->count, 32));
         PtabArgs ta{};
         ta.L = L;
         uint64_t off = 0;
@@ -1061,7 +1065,7 @@ int build_and_probe(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned*
     const uint32_t kChunk = wave_probe ? 64u * kProbeWaveKPL : kBlock * 8u;
     const size_t item_bound = P + (nS + kChunk - 1) / kChunk;
     PHJ_TRY(ensure(c, c->items, item_bound * sizeof(ProbeItem)));
-    PHJ_TRY(ensure(c, c->count, 16));
+    PHJ_TRY(ensure(c, c->count, 32));
     PHJ_TRY(ensure(c, c->biglist, static_cast<size_t>(P) * 4));
     uint32_t* prep = static_cast<uint32_t*>(c->prep.p);
     // LDS capacities from the expected partition size (larger partitions take
@@ -1243,7 +1247,7 @@ int build_ht(phj_ctx* c, const Plan& pl, int nseg, const int64_t* const* codes, 
     if (slots >= (1ull << 32)) return set_err(c, PHJ_ERR_RANGE, "build side too large for 32-bit table slots");
     PHJ_TRY(ensure(c, c->ht_tab, slots * 8));
     PHJ_TRY(ensure(c, c->ht_desc, static_cast<size_t>(P) * 8));
-    PHJ_TRY(ensure(c, c->count, 16));
+    PHJ_TRY(ensure(c, c->count, 32));
     if (c->dry) return PHJ_OK;
     HtArgs a{};
     for (int g = 0; g < nseg; g++) {
@@ -1381,7 +1385,7 @@ int cluster_big_fill(phj_ctx* c, const Plan& pl, int nseg, const int64_t* const*
     const uint64_t slots = 4 * nR + 2ull * pl.nb1;
     if (slots >= (1ull << 32)) return set_err(c, PHJ_ERR_RANGE, "build side too large for 32-bit table slots");
     PHJ_TRY(ensure(c, c->ht_tab, slots * 8));
-    PHJ_TRY(ensure(c, c->count, 16));
+    PHJ_TRY(ensure(c, c->count, 32));
     if (c->dry) return PHJ_OK;
     ClusterArgs a = cluster_args(c, pl, nseg, codes, bounds);
     hipLaunchKernelGGL(k_cluster_big_fill, dim3(pl.nb1), dim3(256), 0, c->ks, a);
@@ -1403,11 +1407,18 @@ int probe_cluster(phj_ctx* c, const Plan& pl, SideState& PS, int nseg, const int
         a.err = static_cast<const uint32_t*>(PS.ccur.p) + chunk_err_word(PS.plan.nb1);
         PS.chunk_check = false;
     }
+    // the clock split: words 2-3 of the count buffer, cleared with the count
+    // pair by the pass-1 bookkeeping kernel (no memset per join)
+    if (c->tune.timers) {
+        a.split = static_cast<unsigned long long*>(c->count.p) + 2;
+        c->split_words = a.split;
+    }
     constexpr int B = kClBlock, I = kClItems;
     const size_t lds = static_cast<size_t>(a.cap) * 8;
-    const void* kfn = c->tune.cl_pf == 1   ? reinterpret_cast<const void*>(&k_cluster_probe<B, I, 1>)
+    const void* kfn = !c->tune.cl_pre      ? reinterpret_cast<const void*>(&k_cluster_probe<B, I, 2, false>)
+                      : c->tune.cl_pf == 2 ? reinterpret_cast<const void*>(&k_cluster_probe<B, I, 2>)
                       : c->tune.cl_pf == 3 ? reinterpret_cast<const void*>(&k_cluster_probe<B, I, 3>)
-                                           : reinterpret_cast<const void*>(&k_cluster_probe<B, I, 2>);
+                                           : reinterpret_cast<const void*>(&k_cluster_probe<B, I, 1>);
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, B, lds) != hipSuccess || per_cu < 1) per_cu = 1;
     per_cu = std::max(1, std::min<int>(per_cu, static_cast<int>(160 * 1024 / (lds + 256))));
@@ -1417,6 +1428,12 @@ int probe_cluster(phj_ctx* c, const Plan& pl, SideState& PS, int nseg, const int
     void* kargs[] = {&a};
     PHJ_HIP(c, hipLaunchKernel(kfn, dim3(grid), dim3(B), kargs, lds, c->ks));
     PHJ_LAUNCHED(c, "k_cluster_probe");
+    // the big clusters' tiles against their HBM tables (workgroups of the
+    // other clusters return at once)
+    a.split = nullptr;
+    a.err = nullptr;
+    hipLaunchKernelGGL(k_cluster_probe_big, dim3(pl.nb1), dim3(256), 0, c->ks, a);
+    PHJ_LAUNCHED(c, "k_cluster_probe_big");
     return PHJ_OK;
 }
 
@@ -1463,7 +1480,7 @@ int join_nopart_ct(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
     PHJ_TRY(ensure(c, c->r_codes, std::max<uint64_t>(1, R.n) * 8));
     PHJ_TRY(ensure(c, c->r_bounds, (static_cast<size_t>(P) + 1) * 4));
     PHJ_TRY(ensure(c, c->np_uni, 16));
-    PHJ_TRY(ensure(c, c->count, 16));
+    PHJ_TRY(ensure(c, c->count, 32));
     const int64_t* rcodes = static_cast<const int64_t*>(c->r_codes.p);
     const uint32_t* rbnd = static_cast<const uint32_t*>(c->r_bounds.p);
     auto* uni = static_cast<uint32_t*>(c->np_uni.p);
@@ -1693,7 +1710,7 @@ int join_radix_mark(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
     const uint64_t nS = S.view.n;
     const size_t nslots = nS / kFusedChunk + P + 1;
     PHJ_TRY(ensure(c, c->fitems, nslots * sizeof(FusedItem)));
-    PHJ_TRY(ensure(c, c->count, 16));
+    PHJ_TRY(ensure(c, c->count, 32));
     PHJ_TRY(ensure(c, c->mat_mark, std::max<uint64_t>(1, nS) * 4));
     PHJ_HIP(c, hipMemsetAsync(c->count.p, 0, 8, c->ks));
     PHJ_HIP(c, hipMemsetAsync(c->mat_mark.p, 0xff, std::max<uint64_t>(1, nS) * 4, c->ks));
@@ -1770,7 +1787,8 @@ int ctx_create_device(int device, phj_ctx** out) {
     c->tune.p1_pipe = env_int("PHJ_P1_PIPE", 1) != 0;
     c->tune.cl_cap = env_int("PHJ_CL_CAP", static_cast<int>(kClCapMax)) == 8192 ? 8192 : static_cast<int>(kClCapMax);
     c->tune.cl_bits = std::max(0, std::min(kMaxDigitBits, env_int("PHJ_CL_BITS", 0)));
-    c->tune.cl_pf = std::max(1, std::min(3, env_int("PHJ_CL_PF", 2)));
+    c->tune.cl_pf = std::max(1, std::min(3, env_int("PHJ_CL_PF", 3)));
+    c->tune.cl_pre = env_int("PHJ_CL_PRE", 1) != 0;
     c->tune.p2probe = env_int("PHJ_P2PROBE", 1);
     c->tune.p1_slots = env_int("PHJ_P1_SLOTS", 0);
     c->tune.p1_wpc2 = std::max(0, env_int("PHJ_P1_WPC2", 2));
@@ -2183,12 +2201,12 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
         // the main stream; R's pass 1 and the big clusters' HBM tables on the
         // aux stream beside it; then the probe builds each cluster's table in
         // LDS and probes S's codes against it
-        PHJ_TRY(ensure(c, c->count, 16));
+        PHJ_TRY(ensure(c, c->count, 32));
         PHJ_TRY(mark(c, &t0));
         // the code pass's bookkeeping kernel clears the count pair (an empty
         // S takes no chunked pass: a memset)
         PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, cpl, true, static_cast<unsigned long long*>(c->count.p)));
-        if (!S.hcoded) PHJ_HIP(c, hipMemsetAsync(c->count.p, 0, 16, c->stream));
+        if (!S.hcoded) PHJ_HIP(c, hipMemsetAsync(c->count.p, 0, 32, c->stream));
         // R's chain waits for t0 (the previous step's probe read R's codes)
         PHJ_HIP(c, hipStreamWaitEvent(c->aux, t0, 0));
         c->ks = c->aux;
@@ -2198,9 +2216,9 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
         const uint32_t* rbnd = static_cast<const uint32_t*>(c->r_bounds.p);
         if (rc == PHJ_OK) rc = partition_build(c, cpl, static_cast<int64_t*>(c->r_codes.p), static_cast<uint32_t*>(c->r_bounds.p));
         if (rc == PHJ_OK) rc = mark(c, &b0);
-        // algorithmic bytes: none at the balanced configurations (the LDS
-        // tables are built inside the probe); a big cluster's codes read and table written
-        if (rc == PHJ_OK) rc = timer_begin(c, "build", 0);
+        // the HBM tables of clusters beyond the LDS limit (none at the
+        // balanced configurations; the LDS tables are built inside the probe)
+        if (rc == PHJ_OK) rc = timer_begin(c, "build.big", 0);
         if (rc == PHJ_OK) rc = cluster_big_fill(c, cpl, 1, &rcodes, &rbnd, R.n);
         if (rc == PHJ_OK) rc = timer_end(c);
         if (rc == PHJ_OK) rc = mark(c, &tr);
@@ -2208,17 +2226,21 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
         PHJ_TRY(rc);
         PHJ_HIP(c, hipStreamWaitEvent(c->stream, tr, 0));
         PHJ_TRY(mark(c, &t1));
-        // algorithmic bytes: S's codes read once, R's codes read by the workgroups that build their cluster
-        PHJ_TRY(timer_begin(c, "probe", (S.n + R.n) * 8));
+        // one launch, reported as "build" (the workgroups' table builds in LDS:
+        // R's codes read) and "probe" (S's codes read), split by the kernel's own clocks
+        PHJ_TRY(timer_begin_split(c, R.n * 8, S.n * 8));
         PHJ_TRY(probe_cluster(c, cpl, S, 1, &rcodes, &rbnd));
-        PHJ_TRY(timer_end(c));
+        PHJ_TRY(timer_end_split(c));
         PHJ_TRY(mark(c, &p1));
         uint64_t m = 0;
         PHJ_TRY(get_count(c, &m, true));
         r->matches = m;
         r->partition_ms = elapsed(c, t0, t1);
-        r->build_ms = elapsed(c, b0, tr);
-        r->probe_ms = elapsed(c, t1, p1);
+        {   // the probe launch split by its clocks (build = the LDS table builds + the big clusters' HBM tables)
+            const double t = elapsed(c, t1, p1), fb = c->tune.timers ? fused_build_fraction(c) : 0.0;
+            r->build_ms = elapsed(c, b0, tr) + t * fb;
+            r->probe_ms = t * (1.0 - fb);
+        }
         r->total_ms = elapsed(c, t0, p1);
         r->num_partitions = requested;
         // R: 16 read + 8 written (pass 1), 8 read (probe); S: 16 read + 8 written, 8 read
@@ -2232,7 +2254,7 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
         // issued first, or run before S with S's pass 1 on every LDS slot, is
         // 0.05-0.1 ms slower; probing S in row ranges, each beside the next
         // range's pass 1, is 0.3 ms slower: DESIGN.md section 3)
-        PHJ_TRY(ensure(c, c->count, 16));
+        PHJ_TRY(ensure(c, c->count, 32));
         PHJ_TRY(mark(c, &t0));
         // the code pass's bookkeeping kernel clears the count (hcoded)
         PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, pl, true, static_cast<unsigned long long*>(c->count.p)));
@@ -2341,7 +2363,7 @@ int phj_prepare(phj_ctx* c, const phj_join_params* p) {
         PHJ_TRY(ensure(c, c->r_bounds, (static_cast<size_t>(pl.Ppad) + 1) * 4));
         PHJ_TRY(partition_build(c, pl, nullptr, nullptr));
         PHJ_TRY(build_ht(c, pl, 1, nullptr, nullptr, nR));
-        PHJ_TRY(ensure(c, c->count, 16));
+        PHJ_TRY(ensure(c, c->count, 32));
         PHJ_HIP(c, hipStreamSynchronize(c->stream));
         return PHJ_OK;
     }

@@ -71,6 +71,7 @@ struct ClusterArgs {
     uint64_t* gtab;               // HBM tables of the big clusters
     unsigned long long* count;    // {count, failed}
     const uint32_t* err;          // S's pass-1 error word (fold_pass1_error), or null
+    unsigned long long* split;    // null, or {build, probe}: the workgroups' wall clocks spent building tables / probing
 };
 
 // Cluster d's runs over the segments: sseg[g] = codes before segment g (sseg[nseg] = m),
@@ -115,7 +116,9 @@ __device__ __forceinline__ uint32_t cl_seg_of(const uint32_t* sseg, uint32_t nse
 }
 
 // HBM tables of the clusters beyond the LDS limit: one workgroup per cluster,
-// the others return at once (none at the balanced configurations).
+// the others return at once (none at the balanced configurations). Their S
+// tiles are probed by k_cluster_probe_big after k_cluster_probe (which skips
+// them), so the main probe's loop issues the same global loads on every path.
 __global__ __launch_bounds__(256) void k_cluster_big_fill(ClusterArgs a) {
     __shared__ uint32_t sseg[kHtSegs + 1];
     __shared__ const int64_t* sptr[kHtSegs];
@@ -137,16 +140,65 @@ __global__ __launch_bounds__(256) void k_cluster_big_fill(ClusterArgs a) {
     }
 }
 
-// The probe. LDS: the cluster table (cap slots) + a few words. PF: tiles
-// whose codes are in flight ahead of the one probed (registers: PF * ITEMS codes).
-template <int BLOCK, int ITEMS, int PF = 1>
-__global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
-    constexpr int CPL = kClCapMax * 3 / 4 / BLOCK;   // R codes per lane at the limit
-    extern __shared__ __attribute__((aligned(16))) uint64_t tab[];   // [cap]
+// The S tiles of the big clusters against their HBM tables: one workgroup per
+// cluster (the others return at once), its tiles from the pass-1 tile list.
+__global__ __launch_bounds__(256) void k_cluster_probe_big(ClusterArgs a) {
     __shared__ uint32_t sseg[kHtSegs + 1];
     __shared__ const int64_t* sptr[kHtSegs];
     __shared__ uint32_t sB;
+    __shared__ uint32_t red[4];
+    const uint32_t d = blockIdx.x, tid = threadIdx.x;
+    cl_runs(a, d, sseg, sptr, &sB);
+    __syncthreads();
+    const uint32_t m = sseg[a.nseg];
+    if (m <= a.lim) return;   // workgroup-uniform
+    const uint64_t e = d == 0 ? a.e1 : 0ull;
+    const uint32_t bmask = cl_big_cap(m) / 2 - 1;
+    const ulonglong2* g2 = reinterpret_cast<const ulonglong2*>(a.gtab + 4ull * sB + 2ull * d);
+    uint32_t hits = 0;
+    for (uint32_t t = a.tile_base[d]; t < a.tile_base[d + 1]; t++) {
+        const uint32_t lo = a.tile_start[t], c = a.tile_cnt[t];
+        for (uint32_t i = tid; i < c; i += 256) {
+            const uint64_t cc = static_cast<uint64_t>(a.s_codes[lo + i]);
+            uint32_t b = static_cast<uint32_t>(cc >> kHtBucketShift) & bmask;
+            for (;;) {
+                const ulonglong2 w = g2[b];
+                if (w.x == cc || w.y == cc) {
+                    hits++;
+                    break;
+                }
+                if (w.y == e) break;
+                b = (b + 1) & bmask;
+            }
+        }
+    }
+    uint32_t x = hits;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_down(x, o, 64);
+    if ((tid & 63) == 0) red[tid >> 6] = x;
+    __syncthreads();
+    if (tid == 0) {
+        const unsigned long long s = static_cast<unsigned long long>(red[0]) + red[1] + red[2] + red[3];
+        if (s) atomicAdd(a.count, s);
+    }
+}
+
+// The probe. LDS: the cluster table (cap slots) + a few words. PF: tiles
+// whose codes are in flight ahead of the one probed (registers: PF * ITEMS codes).
+// PRE: while a cluster's tiles are probed, the NEXT cluster's R codes are
+// already loaded into registers (its runs staged in the other LDS run buffer
+// during this cluster's build), so a build waits on no memory; only the
+// first build of a workgroup, or a cluster its range skips, loads in place.
+template <int BLOCK, int ITEMS, int PF = 1, bool PRE = true>
+__global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
+    constexpr int CPL = kClCapMax * 3 / 4 / BLOCK;   // R codes per lane at the limit
+    extern __shared__ __attribute__((aligned(16))) uint64_t tab[];   // [cap]
+    __shared__ uint32_t sseg_[2][kHtSegs + 1];
+    __shared__ const int64_t* sptr_[2][kHtSegs];
+    __shared__ uint32_t sB_[2];
     __shared__ uint32_t red[BLOCK / 64];
+    constexpr uint32_t MR = 512;                 // tiles of metadata staged in LDS at a time
+    __shared__ uint32_t smeta[3][MR];            // {cluster, first slot, codes} of tiles mbase .. mbase + MR - 1
     const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const uint32_t total = a.tile_base[a.nb1];
     // workgroup -> a contiguous range of tiles; neighbouring ranges on one XCD
@@ -155,136 +207,199 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
     const uint32_t t_lo = static_cast<uint32_t>(static_cast<uint64_t>(total) * r8 / G);
     const uint32_t t_hi = static_cast<uint32_t>(static_cast<uint64_t>(total) * (r8 + 1) / G);
     uint32_t hits = 0;
+    const unsigned long long clk0 = wall_clock64();
+    unsigned long long clk_b = 0;   // wall clock in table builds (workgroup-uniform sections)
     if (t_lo < t_hi) {   // workgroup-uniform
-        int64_t key[PF + 1][ITEMS];   // [0] the tile probed, [1..PF] in flight
-        uint32_t vm[PF + 1], dq[PF + 1];
-        // tile metadata 64 tiles at a time: lane i holds tile mb + i's {cluster,
-        // first slot, codes} (vector loads, read out with readlane: a scalar
-        // load per tile would make every later LDS wait -- lgkmcnt covers both
-        // -- wait for it too)
-        uint32_t mb = 0, mseg = 0, mstart = 0, mcnt = 0;
-        auto meta = [&](uint32_t base) {
-            mb = base;
-            const uint32_t tt = min(base + lane, t_hi - 1);
-            mseg = a.tile_seg[tt];
-            mstart = a.tile_start[tt];
-            mcnt = a.tile_cnt[tt];
+        // PF register buffers of tile codes, used in turn (no register moves:
+        // a move of a register a load is still writing waits for that load).
+        // The step for tile t probes the codes in its buffer (requested PF
+        // steps earlier; tiles t + 1 .. t + PF - 1 stay in flight), then
+        // requests tile t + PF's codes into the buffer. Every global load of a step
+        // is issued on every path, in the same order (indices clamped; a tile
+        // past the range reads the last one's chunk with no valid lanes), so a
+        // wait covers only what was issued before the awaited load: vmcnt
+        // retires in issue order, and one conditional load made the compiler
+        // wait for everything in flight. The metadata loads are vector loads (a
+        // scalar load would be waited for by every LDS access: lgkmcnt counts both).
+        int64_t key[PF][ITEMS];
+        uint32_t vm[PF], dq[PF];
+        // tile metadata staged in LDS, MR tiles at a time (refilled behind a
+        // barrier every MR tiles): the loop's only global loads are then the
+        // tiles' codes and the builds' R codes, and an LDS read of metadata
+        // never waits for a global load
+        uint32_t mbase = 0xffffffffu;
+        auto stage = [&](uint32_t base) {   // workgroup-uniform
+            __syncthreads();
+            for (uint32_t i = tid; i < MR; i += BLOCK) {
+                const uint32_t ti = min(base + i, t_hi - 1);
+                smeta[0][i] = a.tile_seg[ti];
+                smeta[1][i] = a.tile_start[ti];
+                smeta[2][i] = a.tile_cnt[ti];
+            }
+            __builtin_amdgcn_s_waitcnt(0xF70);   // vmcnt(0): this path's loads done (see build)
+            __syncthreads();
+            mbase = base;
         };
-        meta(t_lo);
         auto load = [&](uint32_t t, int64_t* k, uint32_t& m, uint32_t& dd) {
-            if (t - mb >= 64) meta(t);
-            const int idx = static_cast<int>(t - mb);
-            dd = __builtin_amdgcn_readlane(mseg, idx);
-            const uint32_t lo = __builtin_amdgcn_readlane(mstart, idx), c = __builtin_amdgcn_readlane(mcnt, idx);
+            if (t - mbase >= MR && t < t_hi) stage(t);   // workgroup-uniform
+            const uint32_t j = min(t, t_hi - 1) - mbase;
+            dd = smeta[0][j];
+            const uint32_t lo = smeta[1][j];
+            const uint32_t c = t < t_hi ? smeta[2][j] : 0u;
             m = 0;
+            // 16-B loads, two codes per lane each: a tile is one pass-1 chunk of
+            // BLOCK * ITEMS allocated slots, read whole (the slots past its codes
+            // are masked off); element (i, h) = code 2 * (i / 2 * BLOCK + tid) + h
+            typedef long long v2i __attribute__((ext_vector_type(2)));
+            const v2i* src = reinterpret_cast<const v2i*>(a.s_codes + lo);
 #pragma unroll
-            for (int i = 0; i < ITEMS; i++) {   // clamped, unconditional (an empty tile reads slot lo + e)
-                const uint32_t e = i * BLOCK + tid;
-                k[i] = __builtin_nontemporal_load(a.s_codes + lo + min(e, c - 1u));
-                m |= e < c ? (1u << i) : 0u;
+            for (int i = 0; i < ITEMS; i += 2) {
+                const uint32_t e = 2 * ((i / 2) * BLOCK + tid);
+                const v2i v = __builtin_nontemporal_load(src + (i / 2) * BLOCK + tid);
+                k[i] = v.x;
+                k[i + 1] = v.y;
+                m |= (e < c ? (1u << i) : 0u) | (e + 1 < c ? (2u << i) : 0u);
             }
         };
+        stage(t_lo);
 #pragma unroll
-        for (int f = 0; f < PF; f++) {
-            vm[f] = 0;
-            dq[f] = 0;
-            if (t_lo + f < t_hi) load(t_lo + f, key[f], vm[f], dq[f]);
-        }
+        for (int f = 0; f < PF; f++) load(t_lo + f, key[f], vm[f], dq[f]);   // tiles t_lo .. t_lo + PF - 1
         uint32_t cur = 0xffffffffu, bmask = 0;
         bool big = false;
         uint64_t e = 0;
-        const ulonglong2* tb = reinterpret_cast<const ulonglong2*>(tab);
-        for (uint32_t t = t_lo;;) {
-            const uint32_t d = dq[0];
-            if (d != cur) {   // workgroup-uniform: build cluster d's table
-                __syncthreads();   // every probe of the previous table is done
-                cl_runs(a, d, sseg, sptr, &sB);
+        uint32_t pb = 0;                 // run buffer of the current cluster
+        uint32_t pre = 0xffffffffu;      // the cluster whose codes are in rn[] (PRE)
+        uint64_t rn[PRE ? CPL : 1];
+        const uint32_t d_last = a.tile_seg[t_hi - 1];   // the range's last cluster
+        // codes of the cluster whose runs are in buffer `buf` (m of them), requested at once
+        auto fetch = [&](uint32_t buf, uint32_t m, uint64_t* rc) {
+            const uint32_t* sseg = sseg_[buf];
+            const int64_t* const* sptr = sptr_[buf];
+            if (a.nseg == 1) {   // one build segment: element r at sptr[0] + r
+                const int64_t* src = sptr[0];
+#pragma unroll
+                for (int j = 0; j < CPL; j++) {
+                    const uint32_t r = j * BLOCK + tid;
+                    rc[j] = r < m ? static_cast<uint64_t>(src[r]) : 0ull;
+                }
+            } else {   // the segments' run ends in registers (broadcast reads), searched per element
+                uint32_t se[kHtSegs];
+#pragma unroll
+                for (int g = 0; g < kHtSegs; g++) se[g] = g < static_cast<int>(a.nseg) ? sseg[g + 1] : 0xffffffffu;
+#pragma unroll
+                for (int j = 0; j < CPL; j++) {
+                    const uint32_t r = j * BLOCK + tid;
+                    uint32_t g = 0;
+#pragma unroll
+                    for (int q = 0; q < kHtSegs; q++) g += r >= se[q] ? 1u : 0u;   // segments ending at or before r
+                    rc[j] = r < m ? static_cast<uint64_t>(sptr[min(g, a.nseg - 1)][r]) : 0ull;
+                }
+            }
+        };
+        // cluster d's table, in LDS (or the descriptor of its HBM table)
+        auto build = [&](uint32_t d) {
+            __syncthreads();   // every probe of the previous table is done
+            const unsigned long long cb = wall_clock64();
+            uint64_t rc[CPL];
+            if (PRE && pre == d) {   // runs staged in the other buffer, codes in registers
+                pb ^= 1u;
+#pragma unroll
+                for (int j = 0; j < CPL; j++) rc[j] = rn[PRE ? j : 0];
+            } else {
+                cl_runs(a, d, sseg_[pb], sptr_[pb], &sB_[pb]);
                 __syncthreads();
-                const uint32_t m = sseg[a.nseg];
-                e = d == 0 ? a.e1 : 0ull;
-                big = m > a.lim;
-                if (!big) {
-                    bmask = a.cap / 2 - 1;
-                    uint64_t rc[CPL];
+                const uint32_t m0 = sseg_[pb][a.nseg];
+                if (m0 <= a.lim) fetch(pb, m0, rc);
+            }
+            const uint32_t m = sseg_[pb][a.nseg];
+            e = d == 0 ? a.e1 : 0ull;
+            big = m > a.lim;
+            if (!big) {
+                bmask = a.cap / 2 - 1;
+                ulonglong2* t2 = reinterpret_cast<ulonglong2*>(tab);
+                for (uint32_t b = tid; b <= bmask; b += BLOCK) t2[b] = make_ulonglong2(e, e);
+            } else {
+                bmask = cl_big_cap(m) / 2 - 1;
+            }
+            // the next cluster's runs into the other buffer (read after the barrier)
+            const bool nxt = PRE && d < d_last;
+            if (nxt) cl_runs(a, d + 1, sseg_[pb ^ 1u], sptr_[pb ^ 1u], &sB_[pb ^ 1u]);
+            __syncthreads();   // cleared; the next runs staged
+            if (!big) {
 #pragma unroll
-                    for (int j = 0; j < CPL; j++) {   // every code of the run requested at once
-                        const uint32_t r = j * BLOCK + tid;
-                        rc[j] = 0;
-                        if (r < m) rc[j] = static_cast<uint64_t>(sptr[cl_seg_of(sseg, a.nseg, r)][r]);
-                    }
-                    ulonglong2* t2 = reinterpret_cast<ulonglong2*>(tab);
-                    for (uint32_t b = tid; b <= bmask; b += BLOCK) t2[b] = make_ulonglong2(e, e);
-                    __syncthreads();   // cleared
-#pragma unroll
-                    for (int j = 0; j < CPL; j++) {
-                        if (j * BLOCK + tid < m) {
-                            const uint64_t c = rc[j];
-                            uint32_t b = static_cast<uint32_t>(c >> kHtBucketShift) & bmask;
-                            for (;;) {
-                                const uint64_t o0 = atomicCAS(reinterpret_cast<unsigned long long*>(&tab[2 * b]), e, c);
-                                if (o0 == e || o0 == c) break;
-                                const uint64_t o1 = atomicCAS(reinterpret_cast<unsigned long long*>(&tab[2 * b + 1]), e, c);
-                                if (o1 == e || o1 == c) break;
-                                b = (b + 1) & bmask;
-                            }
+                for (int j = 0; j < CPL; j++) {
+                    if (j * BLOCK + tid < m) {
+                        const uint64_t c = rc[j];
+                        uint32_t b = static_cast<uint32_t>(c >> kHtBucketShift) & bmask;
+                        for (;;) {
+                            const uint64_t o0 = atomicCAS(reinterpret_cast<unsigned long long*>(&tab[2 * b]), e, c);
+                            if (o0 == e || o0 == c) break;
+                            const uint64_t o1 = atomicCAS(reinterpret_cast<unsigned long long*>(&tab[2 * b + 1]), e, c);
+                            if (o1 == e || o1 == c) break;
+                            b = (b + 1) & bmask;
                         }
                     }
-                    __syncthreads();   // built
-                } else {
-                    bmask = cl_big_cap(m) / 2 - 1;
                 }
-                cur = d;
             }
-            vm[PF] = 0;
-            dq[PF] = d;
-            if (t + PF < t_hi) load(t + PF, key[PF], vm[PF], dq[PF]);   // workgroup-uniform
+            // every load of the build path complete (s_waitcnt vmcnt(0)): else
+            // the compiler, merging this path with the no-build one, makes the
+            // next step wait for every load in flight on both
+            __builtin_amdgcn_s_waitcnt(0xF70);
+            pre = 0xffffffffu;
+            if constexpr (PRE) {   // the next cluster's codes: in flight during this cluster's tiles
+                if (nxt) {
+                    const uint32_t mn = sseg_[pb ^ 1u][a.nseg];
+                    if (mn <= a.lim) {
+                        fetch(pb ^ 1u, mn, rn);
+                        pre = d + 1;
+                    }
+                }
+            }
+            __syncthreads();   // built
+            cur = d;
+            clk_b += wall_clock64() - cb;
+        };
+        const ulonglong2* tb = reinterpret_cast<const ulonglong2*>(tab);
+        uint32_t t = t_lo;
+        // one tile: take its codes out of buffer f, refill the buffer, probe
+        auto step = [&](int f) -> bool {
+            const uint32_t cvm = vm[f], d = dq[f];
+            if (d != cur) build(d);   // workgroup-uniform
             if (!big) {   // LDS: every item's home bucket read, then the walks
                 ulonglong2 v[ITEMS];
 #pragma unroll
-                for (int i = 0; i < ITEMS; i++) v[i] = tb[static_cast<uint32_t>(static_cast<uint64_t>(key[0][i]) >> kHtBucketShift) & bmask];
+                for (int i = 0; i < ITEMS; i++) v[i] = tb[static_cast<uint32_t>(static_cast<uint64_t>(key[f][i]) >> kHtBucketShift) & bmask];
 #pragma unroll
                 for (int i = 0; i < ITEMS; i++) {
-                    const uint64_t c = static_cast<uint64_t>(key[0][i]);
-                    bool hit = v[i].x == c || v[i].y == c;
-                    if ((vm[0] >> i) & 1u) {
+                    const uint64_t cc = static_cast<uint64_t>(key[f][i]);
+                    bool hit = v[i].x == cc || v[i].y == cc;
+                    if ((cvm >> i) & 1u) {
                         if (!hit && v[i].y != e) {
-                            uint32_t b = static_cast<uint32_t>(c >> kHtBucketShift) & bmask;
+                            uint32_t b = static_cast<uint32_t>(cc >> kHtBucketShift) & bmask;
                             for (;;) {
                                 b = (b + 1) & bmask;
                                 const ulonglong2 w = tb[b];
-                                hit = w.x == c || w.y == c;
+                                hit = w.x == cc || w.y == cc;
                                 if (hit || w.y == e) break;
                             }
                         }
                         hits += hit ? 1u : 0u;
                     }
                 }
-            } else {   // HBM table of a big cluster
-                const ulonglong2* g2 = reinterpret_cast<const ulonglong2*>(a.gtab + 4ull * sB + 2ull * d);
-#pragma unroll
-                for (int i = 0; i < ITEMS; i++) {
-                    if ((vm[0] >> i) & 1u) {
-                        const uint64_t c = static_cast<uint64_t>(key[0][i]);
-                        uint32_t b = static_cast<uint32_t>(c >> kHtBucketShift) & bmask;
-                        for (;;) {
-                            const ulonglong2 w = g2[b];
-                            if (w.x == c || w.y == c) {
-                                hits++;
-                                break;
-                            }
-                            if (w.y == e) break;
-                            b = (b + 1) & bmask;
-                        }
-                    }
-                }
-            }
-            if (++t >= t_hi) break;
+            }   // (a big cluster's tiles: k_cluster_probe_big, no global load here)
+            // the buffer refilled only now, once its codes are consumed (a refill
+            // into other registers would put a move at the loop's back edge,
+            // which waits for the refill): tile t + PF's codes; tiles t + 1 ..
+            // t + PF - 1 were in flight during this tile's probe
+            load(t + PF, key[f], vm[f], dq[f]);
+            return ++t < t_hi;
+        };
+        bool more = true;
+        while (more) {
 #pragma unroll
             for (int f = 0; f < PF; f++) {
-#pragma unroll
-                for (int i = 0; i < ITEMS; i++) key[f][i] = key[f + 1][i];
-                vm[f] = vm[f + 1];
-                dq[f] = dq[f + 1];
+                more = step(f);
+                if (!more) break;
             }
         }
     }
@@ -297,6 +412,11 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
         unsigned long long s = 0;
         for (int w = 0; w < BLOCK / 64; w++) s += red[w];
         if (s) atomicAdd(a.count, s);
+        if (a.split) {
+            const unsigned long long all = wall_clock64() - clk0;
+            atomicAdd(&a.split[0], clk_b);
+            atomicAdd(&a.split[1], all - clk_b);
+        }
     }
     fold_pass1_error(a.err, a.count);
 }

@@ -530,11 +530,11 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
     const bool s_early = !(G.rehearse && i > 0);
     if (rc == PHJ_OK && s_early) {
         c->ks = c->stream;
-        if (p2) rc = ensure(c, c->count, 16);
+        if (p2) rc = ensure(c, c->count, 32);
         // the code pass's bookkeeping kernel clears the count (hcoded); else a memset
         if (rc == PHJ_OK)
             rc = partition_side(c, PHJ_SIDE_PROBE, pl, p2, p2 ? static_cast<unsigned long long*>(c->count.p) : nullptr);
-        if (rc == PHJ_OK && p2 && !c->side[PHJ_SIDE_PROBE].hcoded && hipMemsetAsync(c->count.p, 0, 16, c->stream) != hipSuccess)
+        if (rc == PHJ_OK && p2 && !c->side[PHJ_SIDE_PROBE].hcoded && hipMemsetAsync(c->count.p, 0, 32, c->stream) != hipSuccess)
             rc = set_err(c, PHJ_ERR_HIP, "count reset");
         if (rc == PHJ_OK && p2) rc = mark(c, &sdone);
         c->ks = c->aux;
@@ -570,7 +570,7 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
         gathered_codes(G, i, L, codes, bnd);
         const uint64_t nRall = total(G.n[PHJ_SIDE_BUILD]);
         if (pl.cluster) {   // only the big clusters' HBM tables; the LDS tables are built in the probe
-            if (rc == PHJ_OK) rc = timer_begin(c, "build", 0);
+            if (rc == PHJ_OK) rc = timer_begin(c, "build.big", 0);
             if (rc == PHJ_OK) rc = cluster_big_fill(c, pl, G.world, codes, bnd, nRall);
         } else {
             if (rc == PHJ_OK) rc = timer_begin(c, "build", nRall * 8 * 3);   // codes read, tables written
@@ -597,16 +597,18 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
             c->ks = c->aux;
             PHJ_HIP(c, hipStreamWaitEvent(c->aux, sdone, 0));
             PHJ_TRY(mark(c, &t1));
-            PHJ_TRY(timer_begin(c, "probe", c->side[PHJ_SIDE_PROBE].n * (c->side[PHJ_SIDE_PROBE].p2.keys_only ? 8 : 16)));
-            if (pl.cluster) {
+            if (pl.cluster) {   // one launch: "build" (LDS tables) / "probe" by its clocks
                 const int64_t* codes[kHtSegs];
                 const uint32_t* bnd[kHtSegs];
                 gathered_codes(G, i, L, codes, bnd);
+                PHJ_TRY(timer_begin_split(c, total(G.n[PHJ_SIDE_BUILD]) * 8, c->side[PHJ_SIDE_PROBE].n * 8));
                 PHJ_TRY(probe_cluster(c, pl, c->side[PHJ_SIDE_PROBE], G.world, codes, bnd));
+                PHJ_TRY(timer_end_split(c));
             } else {
+                PHJ_TRY(timer_begin(c, "probe", c->side[PHJ_SIDE_PROBE].n * (c->side[PHJ_SIDE_PROBE].p2.keys_only ? 8 : 16)));
                 PHJ_TRY(probe_ht(c, pl, c->side[PHJ_SIDE_PROBE], false));
+                PHJ_TRY(timer_end(c));
             }
-            PHJ_TRY(timer_end(c));
             PHJ_TRY(mark(c, &p1));
             c->last_fused = false;
             return PHJ_OK;
@@ -634,6 +636,11 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
     r->partition_ms = elapsed(c, t0, t1);
     r->build_ms = elapsed(c, b0, b1);
     r->probe_ms = p2 ? elapsed(c, t1, p1) : elapsed(c, b1, p1);
+    if (pl.cluster && c->tune.timers) {   // the LDS probe launch split by its clocks
+        const double t = elapsed(c, t1, p1), fb = fused_build_fraction(c);
+        r->build_ms += t * fb;
+        r->probe_ms = t * (1.0 - fb);
+    }
     if (!p2 && c->last_fused) {
         const double t = elapsed(c, b0, p1), fb = fused_build_fraction(c);
         r->build_ms = t * fb;

@@ -1456,6 +1456,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_apply(ScanArgs s) {
 constexpr uint32_t kFinBlock = 256;
 
 // Exclusive scan over the block with a running carry (kFinBlock threads).
+template <uint32_t NT = kFinBlock>
 __device__ __forceinline__ uint32_t fin_block_scan(uint32_t v, uint32_t* wsum, uint32_t& total) {
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t x = v;
@@ -1468,7 +1469,7 @@ __device__ __forceinline__ uint32_t fin_block_scan(uint32_t v, uint32_t* wsum, u
     __syncthreads();
     uint32_t before = 0, all = 0;
 #pragma unroll
-    for (uint32_t w = 0; w < kFinBlock / 64; w++) {
+    for (uint32_t w = 0; w < NT / 64; w++) {
         const uint32_t t = wsum[w];
         if (w < wave) before += t;
         all += t;
@@ -1551,28 +1552,31 @@ __global__ __launch_bounds__(kBlock) void k_tile_chunks(const uint32_t* tile_bas
 
 // After a chunked pass 1: bounds1 = exclusive scan of the digit sizes (summed
 // over the shards: the segments' offsets in the pass-2 output) and
-// tile_base2 = exclusive scan of their chunk counts; `zero` (may be null: two
+// tile_base2 = exclusive scan of their chunk counts; `zero` (may be null: four
 // words) is cleared. One workgroup.
-__global__ __launch_bounds__(kFinBlock) void k_pass1_finish_sizes(const uint32_t* sizes, uint32_t nb, uint32_t nshards,
-                                                                  uint32_t n, uint32_t T, uint32_t* bounds1,
-                                                                  uint32_t* tile_base2, unsigned long long* zero) {
-    __shared__ uint32_t wsum[2][kFinBlock / 64];
+constexpr uint32_t kFinSizesBlock = 1024;   // one digit per thread at 1024 clusters: one round of shard loads
+__global__ __launch_bounds__(kFinSizesBlock) void k_pass1_finish_sizes(const uint32_t* sizes, uint32_t nb, uint32_t nshards,
+                                                                       uint32_t n, uint32_t T, uint32_t* bounds1,
+                                                                       uint32_t* tile_base2, unsigned long long* zero) {
+    constexpr uint32_t B = kFinSizesBlock;
+    __shared__ uint32_t wsum[2][B / 64];
     const uint32_t tid = threadIdx.x;
-    if (zero && tid < 2) zero[tid] = 0;   // the on-chip probe's {count, failed} (one launch fewer before it)
+    if (zero && tid < 4) zero[tid] = 0;   // the on-chip probe's {count, failed} and its clock split (one launch fewer before it)
     uint32_t cx = 0, cy = 0;
-    for (uint32_t base = 0; base < nb; base += kFinBlock) {
+    for (uint32_t base = 0; base < nb; base += B) {
         const uint32_t d = base + tid;
+        uint32_t z[kShards];
+#pragma unroll
+        for (uint32_t x = 0; x < kShards; x++) z[x] = d < nb && x < nshards ? sizes[x * nb + d] : 0u;   // all in flight
         uint32_t v = 0, t = 0;
-        if (d < nb) {
-            for (uint32_t x = 0; x < nshards; x++) {
-                const uint32_t z = sizes[x * nb + d];
-                v += z;
-                t += (z + T - 1) / T;
-            }
+#pragma unroll
+        for (uint32_t x = 0; x < kShards; x++) {
+            v += z[x];
+            t += (z[x] + T - 1) / T;
         }
         uint32_t ax, ay;
-        const uint32_t ex = fin_block_scan(v, wsum[0], ax);
-        const uint32_t ey = fin_block_scan(t, wsum[1], ay);
+        const uint32_t ex = fin_block_scan<B>(v, wsum[0], ax);
+        const uint32_t ey = fin_block_scan<B>(t, wsum[1], ay);
         if (d < nb) {
             bounds1[d] = cx + ex;
             tile_base2[d] = cy + ey;

@@ -31,8 +31,9 @@ FAMILIES = [
     (re.compile(r"^R\.p2\.scatter$"), re.compile(r"phj::k_ht_p2")),
     (re.compile(r"\.hist$"), re.compile(r"phj::k_hist")),
     (re.compile(r"\.scatter$"), re.compile(r"phj::k_(scatter|chunk_codes)")),
-    (re.compile(r"^build$"), re.compile(r"phj::k_(build_small|ht_fill|join_fused)")),
-    (re.compile(r"^probe$"), re.compile(r"phj::k_(probe|join_fused)")),
+    (re.compile(r"^build$"), re.compile(r"phj::k_(build_small|ht_fill|join_fused|cluster_probe)")),
+    (re.compile(r"^build\.big$"), re.compile(r"phj::k_cluster_big_fill")),
+    (re.compile(r"^probe$"), re.compile(r"phj::k_(probe|join_fused|cluster_probe)")),
     (re.compile(r"^np\.build$"), re.compile(r"phj::k_(np_build(?!_overflow)|ht_fill)")),
     (re.compile(r"^np\.probe$"), re.compile(r"phj::k_np_probe")),
 ]
@@ -77,7 +78,7 @@ def attribute(rows, timers):
     seq = [disp[k] for k in sorted(disp)]
     res = {}
     i = len(seq) - 1
-    shared = None   # the fused join: "build" and "probe" are one dispatch
+    shared = None   # the fused join, the LDS join: "build" and "probe" are one dispatch
     for t in reversed(timers):
         fam = family(t)
         if fam is None:
@@ -91,7 +92,7 @@ def attribute(rows, timers):
         if i < 0:
             break
         res[t] = dict(seq[i]["vals"])
-        shared = seq[i] if "k_join_fused" in seq[i]["name"] else None
+        shared = seq[i] if ("k_join_fused" in seq[i]["name"] or "k_cluster_probe" in seq[i]["name"]) else None
         i -= 1
     return res
 

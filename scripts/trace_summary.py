@@ -2,7 +2,9 @@
 """Summarise a rocprofv3 --kernel-trace CSV: per-kernel average duration and,
 for the last bench step, the device timeline (start offsets and gaps).
 
-  python scripts/trace_summary.py <dir with *_kernel_trace.csv> [--step-kernel k_probe]
+  python scripts/trace_summary.py <dir with *_kernel_trace.csv> [--step-kernel NAME]
+(the step ends at the last launch whose name contains NAME, default k_probe;
+k_cluster_probe is the LDS join's probe)
 """
 import csv
 import glob
@@ -29,11 +31,12 @@ def main():
     for n, v in sorted(stats.items(), key=lambda kv: -sum(kv[1])):
         print(f"{n:92s} {len(v):6d} {sum(v) / len(v):9.1f} {sum(v):10.1f}")
     # timeline of the last step: from the last k_hist launch preceding the last k_probe
-    probes = [i for i, r in enumerate(rows) if "k_probe" in r[2]]
+    key = sys.argv[sys.argv.index("--step-kernel") + 1] if "--step-kernel" in sys.argv else "k_probe"
+    probes = [i for i, r in enumerate(rows) if key in r[2]]
     if probes:
         last = probes[-1]
         first = last
-        while first > 0 and rows[first - 1][0] > rows[last][0] - 20_000_000 and "k_probe" not in rows[first - 1][2]:
+        while first > 0 and rows[first - 1][0] > rows[last][0] - 20_000_000 and key not in rows[first - 1][2]:
             first -= 1
         t0 = rows[first][0]
         print("\nlast step timeline (us): start  dur  gap-before  kernel")

@@ -33,6 +33,8 @@ SCHEDULES = [
     {"PHJ_BLOCK": "512", "PHJ_TILE": "8192"},
     {"PHJ_BLOCK": "1024", "PHJ_TILE": "8192"},
     {"PHJ_BLOCK": "333"},                      # not compiled: falls back to 512 x 4096
+    {"PHJ_BLOCK": "256", "PHJ_TILE": "2048", "PHJ_P1_MIN_TILES": "0"},    # chunked whole-tuple pass 1, non-PACK form
+    {"PHJ_BLOCK": "1024", "PHJ_TILE": "8192", "PHJ_P1_MIN_TILES": "0"},   # ... 16 waves (scan words 0-15, reservations 16+)
     {"PHJ_FUSED": "0", "PHJ_PTAB": "0"},
     {"PHJ_FUSED": "0"},
     {"PHJ_FUSED": "0", "PHJ_PTAB": "2"},
@@ -55,8 +57,9 @@ SCHEDULES = [
     {"PHJ_CL_CAP": "8192"},                                     # LDS join: 64 KB tables, two workgroups per CU
     {"PHJ_CL_BITS": "11"},                                      # LDS join: 2048 clusters (four digits per pass-1 thread)
     {"PHJ_CL_BITS": "10", "PHJ_P1_KO_TPS": "4"},                # ... 1024 clusters over 16 shards
-    {"PHJ_CL_PF": "1"},                                         # LDS join probe: one tile of codes in flight
-    {"PHJ_CL_PF": "3"},                                         # ... three tiles
+    {"PHJ_CL_PF": "1"},                                         # LDS join probe: one register buffer of codes (no prefetch)
+    {"PHJ_CL_PF": "2"},                                         # ... two
+    {"PHJ_CL_PRE": "0"},                                        # ... each cluster's R codes loaded when its build starts
     {"PHJ_P1_PIPE": "0"},                                       # keys-only pass 1 resolving its claims in the same tile
     {"PHJ_P1_PIPE": "0", "PHJ_CL_BITS": "11"},                  # ... with four digits per thread
 ]
