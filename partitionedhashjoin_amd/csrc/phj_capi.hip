@@ -58,6 +58,8 @@ struct Tuning {
     int p1_ko_tps = 1024;      // ... the keys-only form for the on-chip probe: tiles per shard (at every size)
     int p2probe = 1;      // radix join, 2 passes: the probe side's pass 2 on-chip (k_probe_ht)
     int p1_pipe = 1;      // keys-only pass 1: claims resolved a tile later over pre-allocated chunks (k_chunk_codes_pipe)
+    int cl_prof = 0;      // PHJ_CL_PROF: the LDS join's build sections to stderr (diagnostics)
+    int p1_block = 1024;  // ... its workgroup: 1024 x 4 codes (16 waves per CU; measured 1.20 -> 1.07 ms at C2) or 512 x 8, the same tile
     int cluster = 1;      // radix join: LDS cluster tables (phj_cluster.h) when the build side's clusters fit
     int cl_cap = static_cast<int>(kClCapMax);   // ... LDS table slots (8192: two workgroups per CU, 16384: one)
     int cl_bits = 0;      // ... clusters = 2^cl_bits (0: the fewest >= 256 whose average fits the table)
@@ -149,7 +151,7 @@ struct phj_ctx {
     DevBuf np_tab, np_pays;
     DevBuf np_ovf, np_ovfb, np_ovfn;   // region build: overflow tuples, their start buckets, count
     DevBuf np_uni;                     // code-table NoPartitioning: {uniform?, cap} (k_np_ct_plan)
-    DevBuf fitems, split;
+    DevBuf fitems, split, cl_prof;
     DevBuf mat_mark, mat_cnt, mat_rows;   // materialised join: per-probe match, block offsets, rows
     uint64_t mat_n = 0;   // fused join: item slots; wave clocks {build, probe} since the last timer reset
     std::vector<hipEvent_t> evpool;
@@ -569,14 +571,22 @@ int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const st
             const bool pipe = a.keys_only && c->tune.p1_pipe && BLOCK == 512 && ITEMS == 8;
             const size_t lds = pipe ? chunk_pipe_lds_bytes(T, a.nbins) : a.keys_only ? chunk_codes_lds_bytes(T, a.nbins) : sc_lds;
             const void* kfn = nullptr;
-            const int kblock = BLOCK;
+            int kblock = BLOCK;
             // keys only, written as hash codes (the on-chip probe): k_chunk_codes;
             // whole tuples: VAR 3, LDS-atomic ranking, 16-B LDS entries (phj_partition.h)
             // (more digits than threads: the cluster plans, 512 x 4096 only)
             if (a.keys_only && pipe) {
                 if constexpr (BLOCK == 512 && ITEMS == 8) {
                     const int dpt = a.nbins > 2 * BLOCK ? 4 : a.nbins > BLOCK ? 2 : 1;
-                    if (hk == kMurmur3)
+                    if (c->tune.p1_block == 1024) {   // 16 waves per CU, 4 codes per thread
+                        kblock = 1024;
+                        if (hk == kMurmur3)
+                            kfn = dpt == 4 ? reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kMurmur3, 2>)
+                                           : reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kMurmur3, 1>);
+                        else
+                            kfn = dpt == 4 ? reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kXXH3, 2>)
+                                           : reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kXXH3, 1>);
+                    } else if (hk == kMurmur3)
                         kfn = dpt == 4 ? reinterpret_cast<const void*>(&k_chunk_codes_pipe<BLOCK, ITEMS, kMurmur3, 4>)
                             : dpt == 2 ? reinterpret_cast<const void*>(&k_chunk_codes_pipe<BLOCK, ITEMS, kMurmur3, 2>)
                                        : reinterpret_cast<const void*>(&k_chunk_codes_pipe<BLOCK, ITEMS, kMurmur3, 1>);
@@ -781,7 +791,7 @@ int partition_state(phj_ctx* c, SideState& S, const char* tag, const Plan& pl, b
     }
     if (chunked) {
         PHJ_TRY(ensure(c, S.ccur, chunk_state_bytes(pl.nb1)));
-        if (ko) PHJ_TRY(ensure(c, S.csink, static_cast<size_t>(kSinkGroups) * tile_shape(c, pl.nb1).block * 8));
+        if (ko) PHJ_TRY(ensure(c, S.csink, static_cast<size_t>(kSinkGroups) * std::max(1024, tile_shape(c, pl.nb1).block) * 8));
         PHJ_TRY(ensure(c, S.tstart, static_cast<size_t>(nt2max) * 8));   // tile_start, tile_cnt
         // all zero between passes (kPublished): cleared when new, and when a
         // pass that published entries never reached k_tile_chunks (an error)
@@ -1415,7 +1425,13 @@ int probe_cluster(phj_ctx* c, const Plan& pl, SideState& PS, int nseg, const int
     }
     constexpr int B = kClBlock, I = kClItems;
     const size_t lds = static_cast<size_t>(a.cap) * 8;
-    const void* kfn = !c->tune.cl_pre      ? reinterpret_cast<const void*>(&k_cluster_probe<B, I, 2, false>)
+    if (c->tune.cl_prof) {
+        PHJ_TRY(ensure(c, c->cl_prof, kClProfWords * 8));
+        a.prof = static_cast<unsigned long long*>(c->cl_prof.p);
+        PHJ_HIP(c, hipMemsetAsync(a.prof, 0, kClProfWords * 8, c->ks));
+    }
+    const void* kfn = c->tune.cl_prof      ? reinterpret_cast<const void*>(&k_cluster_probe<B, I, 3, true, true>)
+                      : !c->tune.cl_pre      ? reinterpret_cast<const void*>(&k_cluster_probe<B, I, 2, false>)
                       : c->tune.cl_pf == 2 ? reinterpret_cast<const void*>(&k_cluster_probe<B, I, 2>)
                       : c->tune.cl_pf == 3 ? reinterpret_cast<const void*>(&k_cluster_probe<B, I, 3>)
                                            : reinterpret_cast<const void*>(&k_cluster_probe<B, I, 1>);
@@ -1428,6 +1444,13 @@ int probe_cluster(phj_ctx* c, const Plan& pl, SideState& PS, int nseg, const int
     void* kargs[] = {&a};
     PHJ_HIP(c, hipLaunchKernel(kfn, dim3(grid), dim3(B), kargs, lds, c->ks));
     PHJ_LAUNCHED(c, "k_cluster_probe");
+    if (c->tune.cl_prof) {   // diagnostics (PHJ_CL_PROF): synchronous, to stderr, in microseconds summed over workgroups
+        unsigned long long h[kClProfWords] = {};
+        PHJ_HIP(c, hipMemcpyAsync(h, a.prof, sizeof(h), hipMemcpyDeviceToHost, c->ks));
+        PHJ_HIP(c, hipStreamSynchronize(c->ks));
+        std::fprintf(stderr, "cl_prof grid %u: cold %.1f us, clear+runs %.1f us, inserts %.1f us, prefetch %.1f us; builds %llu, cold %llu\n",
+                     grid, h[0] / 100.0, h[1] / 100.0, h[2] / 100.0, h[3] / 100.0, h[4], h[5]);
+    }
     // the big clusters' tiles against their HBM tables (workgroups of the
     // other clusters return at once)
     a.split = nullptr;
@@ -1792,6 +1815,8 @@ int ctx_create_device(int device, phj_ctx** out) {
     c->tune.p2probe = env_int("PHJ_P2PROBE", 1);
     c->tune.p1_slots = env_int("PHJ_P1_SLOTS", 0);
     c->tune.p1_wpc2 = std::max(0, env_int("PHJ_P1_WPC2", 2));
+    c->tune.cl_prof = env_int("PHJ_CL_PROF", 0);
+    c->tune.p1_block = env_int("PHJ_P1_BLOCK", 1024) == 512 ? 512 : 1024;
     c->tune.p1_tps = std::max(1, env_int("PHJ_P1_TPS", static_cast<int>(kTilesPerShard)));
     c->tune.p1_min_tiles = std::max(0, env_int("PHJ_P1_MIN_TILES", 32768));
     c->tune.p1_ko_tps = std::max(1, env_int("PHJ_P1_KO_TPS", 1024));
@@ -1930,7 +1955,7 @@ void phj_ctx_destroy(phj_ctx* c) {
             free_buf(*b);
     }
     for (DevBuf* b : {&c->ht_tab, &c->ht_desc, &c->r_codes, &c->r_bounds, &c->scan_partials, &c->prep, &c->tkeys, &c->tpays, &c->toffs, &c->gcursor, &c->items, &c->biglist,
-                      &c->count, &c->np_tab, &c->np_pays, &c->np_ovf, &c->np_ovfb, &c->np_ovfn, &c->fitems, &c->split, &c->mat_mark, &c->mat_cnt, &c->mat_rows})
+                      &c->count, &c->np_tab, &c->np_pays, &c->np_ovf, &c->np_ovfb, &c->np_ovfn, &c->fitems, &c->split, &c->cl_prof, &c->mat_mark, &c->mat_cnt, &c->mat_rows})
         free_buf(*b);
     for (hipEvent_t e : c->evpool) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->stream);

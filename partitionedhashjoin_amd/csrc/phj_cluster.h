@@ -72,7 +72,12 @@ struct ClusterArgs {
     unsigned long long* count;    // {count, failed}
     const uint32_t* err;          // S's pass-1 error word (fold_pass1_error), or null
     unsigned long long* split;    // null, or {build, probe}: the workgroups' wall clocks spent building tables / probing
+    unsigned long long* prof;     // PROF kernels: the builds' sections (wall clock, summed over workgroups), kClProfWords
 };
+// PROF sections of a build: runs + codes of a cluster not prefetched; table
+// cleared + the next cluster's runs; inserts; the next cluster's codes requested;
+// then the number of builds and of builds not prefetched
+constexpr int kClProfWords = 6;
 
 // Cluster d's runs over the segments: sseg[g] = codes before segment g (sseg[nseg] = m),
 // sptr[g] = where element r of segment g's run sits, minus r; returns B_d (first code
@@ -189,7 +194,7 @@ __global__ __launch_bounds__(256) void k_cluster_probe_big(ClusterArgs a) {
 // already loaded into registers (its runs staged in the other LDS run buffer
 // during this cluster's build), so a build waits on no memory; only the
 // first build of a workgroup, or a cluster its range skips, loads in place.
-template <int BLOCK, int ITEMS, int PF = 1, bool PRE = true>
+template <int BLOCK, int ITEMS, int PF = 1, bool PRE = true, bool PROF = false>
 __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
     constexpr int CPL = kClCapMax * 3 / 4 / BLOCK;   // R codes per lane at the limit
     extern __shared__ __attribute__((aligned(16))) uint64_t tab[];   // [cap]
@@ -209,6 +214,7 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
     uint32_t hits = 0;
     const unsigned long long clk0 = wall_clock64();
     unsigned long long clk_b = 0;   // wall clock in table builds (workgroup-uniform sections)
+    unsigned long long prof[kClProfWords] = {};
     if (t_lo < t_hi) {   // workgroup-uniform
         // PF register buffers of tile codes, used in turn (no register moves:
         // a move of a register a load is still writing waits for that load).
@@ -301,6 +307,7 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
             __syncthreads();   // every probe of the previous table is done
             const unsigned long long cb = wall_clock64();
             uint64_t rc[CPL];
+            if (PROF) prof[5] += PRE && pre == d ? 0u : 1u;
             if (PRE && pre == d) {   // runs staged in the other buffer, codes in registers
                 pb ^= 1u;
 #pragma unroll
@@ -310,7 +317,10 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
                 __syncthreads();
                 const uint32_t m0 = sseg_[pb][a.nseg];
                 if (m0 <= a.lim) fetch(pb, m0, rc);
+                if (PROF) __builtin_amdgcn_s_waitcnt(0xF70);
             }
+            unsigned long long c1 = 0, c2 = 0, c3 = 0;
+            if (PROF) c1 = wall_clock64();
             const uint32_t m = sseg_[pb][a.nseg];
             e = d == 0 ? a.e1 : 0ull;
             big = m > a.lim;
@@ -325,6 +335,7 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
             const bool nxt = PRE && d < d_last;
             if (nxt) cl_runs(a, d + 1, sseg_[pb ^ 1u], sptr_[pb ^ 1u], &sB_[pb ^ 1u]);
             __syncthreads();   // cleared; the next runs staged
+            if (PROF) c2 = wall_clock64();
             if (!big) {
 #pragma unroll
                 for (int j = 0; j < CPL; j++) {
@@ -345,6 +356,10 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
             // the compiler, merging this path with the no-build one, makes the
             // next step wait for every load in flight on both
             __builtin_amdgcn_s_waitcnt(0xF70);
+            if (PROF) {
+                __syncthreads();
+                c3 = wall_clock64();
+            }
             pre = 0xffffffffu;
             if constexpr (PRE) {   // the next cluster's codes: in flight during this cluster's tiles
                 if (nxt) {
@@ -357,7 +372,15 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
             }
             __syncthreads();   // built
             cur = d;
-            clk_b += wall_clock64() - cb;
+            const unsigned long long c4 = wall_clock64();
+            clk_b += c4 - cb;
+            if (PROF) {
+                prof[0] += c1 - cb;
+                prof[1] += c2 - c1;
+                prof[2] += c3 - c2;
+                prof[3] += c4 - c3;
+                prof[4] += 1;
+            }
         };
         const ulonglong2* tb = reinterpret_cast<const ulonglong2*>(tab);
         uint32_t t = t_lo;
@@ -417,6 +440,8 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
             atomicAdd(&a.split[0], clk_b);
             atomicAdd(&a.split[1], all - clk_b);
         }
+        if (PROF && a.prof)
+            for (int w = 0; w < kClProfWords; w++) atomicAdd(&a.prof[w], prof[w]);
     }
     fold_pass1_error(a.err, a.count);
 }

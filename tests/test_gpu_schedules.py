@@ -55,13 +55,15 @@ SCHEDULES = [
     {"PHJ_P1_KO_TPS": "4"},                                     # keys-only pass 1: 16 shards on small relations
     {"PHJ_CLUSTER": "0"},                                       # radix count: code tables in HBM (k_probe_ht), not the LDS join
     {"PHJ_CL_CAP": "8192"},                                     # LDS join: 64 KB tables, two workgroups per CU
-    {"PHJ_CL_BITS": "11"},                                      # LDS join: 2048 clusters (four digits per pass-1 thread)
+    {"PHJ_CL_BITS": "11"},                                      # LDS join: 2048 clusters (two digits per pass-1 thread)
     {"PHJ_CL_BITS": "10", "PHJ_P1_KO_TPS": "4"},                # ... 1024 clusters over 16 shards
     {"PHJ_CL_PF": "1"},                                         # LDS join probe: one register buffer of codes (no prefetch)
     {"PHJ_CL_PF": "2"},                                         # ... two
     {"PHJ_CL_PRE": "0"},                                        # ... each cluster's R codes loaded when its build starts
     {"PHJ_P1_PIPE": "0"},                                       # keys-only pass 1 resolving its claims in the same tile
     {"PHJ_P1_PIPE": "0", "PHJ_CL_BITS": "11"},                  # ... with four digits per thread
+    {"PHJ_P1_BLOCK": "512"},                                    # pipelined pass 1 in 512 x 8 workgroups
+    {"PHJ_P1_BLOCK": "512", "PHJ_CL_BITS": "11"},               # ... four digits per thread
 ]
 
 CASES = [((8, 8), 0, phj.HASH_MURMUR3), ((11, 0), 0, phj.HASH_XXH3), ((1, 0), 1000, phj.HASH_XXH3),
