@@ -58,6 +58,11 @@ struct Tuning {
     int p1_ko_tps = 1024;      // ... the keys-only form for the on-chip probe: tiles per shard (at every size)
     int p2probe = 1;      // radix join, 2 passes: the probe side's pass 2 on-chip (k_probe_ht)
     int p1_pipe = 1;      // keys-only pass 1: claims resolved a tile later over pre-allocated chunks (k_chunk_codes_pipe)
+    int p1_wpe = 0;       // ... 1024 x 4: waves per SIMD its registers allow (5: <= 96 VGPRs, room for R's kernels)
+    int r_order = 0;      // LDS join: R's pass 1 beside S's (0), after it (1), before it (2)
+    int p1_kpf = 1;       // ... 1024 x 4: tiles of keys in flight ahead of the one hashed (1 or 2)
+    int p1_prof = 0;      // PHJ_P1_PROF: the pipelined pass 1's phases to stderr (diagnostics)
+    int cl_cnt = 1;       // ... tables built by bucket fill counters (k_cluster_probe CNT; measured build 0.082 -> 0.055 ms at C2)
     int cl_prof = 0;      // PHJ_CL_PROF: the LDS join's build sections to stderr (diagnostics)
     int p1_block = 1024;  // ... its workgroup: 1024 x 4 codes (16 waves per CU; measured 1.20 -> 1.07 ms at C2) or 512 x 8, the same tile
     int cluster = 1;      // radix join: LDS cluster tables (phj_cluster.h) when the build side's clusters fit
@@ -580,12 +585,28 @@ int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const st
                     const int dpt = a.nbins > 2 * BLOCK ? 4 : a.nbins > BLOCK ? 2 : 1;
                     if (c->tune.p1_block == 1024) {   // 16 waves per CU, 4 codes per thread
                         kblock = 1024;
-                        if (hk == kMurmur3)
-                            kfn = dpt == 4 ? reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kMurmur3, 2>)
-                                           : reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kMurmur3, 1>);
+                        const bool w5 = c->tune.p1_wpe == 5;
+                        if (c->tune.p1_kpf == 2)
+                            kfn = hk == kMurmur3 ? (dpt == 4 ? reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kMurmur3, 2, 0, false, 2>)
+                                                             : reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kMurmur3, 1, 0, false, 2>))
+                                                 : (dpt == 4 ? reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kXXH3, 2, 0, false, 2>)
+                                                             : reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kXXH3, 1, 0, false, 2>));
+                        else if (c->tune.p1_prof)
+                            kfn = hk == kMurmur3 ? (dpt == 4 ? reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kMurmur3, 2, 0, true>)
+                                                             : reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kMurmur3, 1, 0, true>))
+                                                 : (dpt == 4 ? reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kXXH3, 2, 0, true>)
+                                                             : reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kXXH3, 1, 0, true>));
                         else
-                            kfn = dpt == 4 ? reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kXXH3, 2>)
-                                           : reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kXXH3, 1>);
+                        if (hk == kMurmur3)
+                            kfn = dpt == 4 ? (w5 ? reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kMurmur3, 2, 5>)
+                                                 : reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kMurmur3, 2>))
+                                           : (w5 ? reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kMurmur3, 1, 5>)
+                                                 : reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kMurmur3, 1>));
+                        else
+                            kfn = dpt == 4 ? (w5 ? reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kXXH3, 2, 5>)
+                                                 : reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kXXH3, 2>))
+                                           : (w5 ? reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kXXH3, 1, 5>)
+                                                 : reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kXXH3, 1>));
                     } else if (hk == kMurmur3)
                         kfn = dpt == 4 ? reinterpret_cast<const void*>(&k_chunk_codes_pipe<BLOCK, ITEMS, kMurmur3, 4>)
                             : dpt == 2 ? reinterpret_cast<const void*>(&k_chunk_codes_pipe<BLOCK, ITEMS, kMurmur3, 2>)
@@ -634,9 +655,25 @@ int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const st
             if (c->tune.p1_slots > 0) slots = std::min<uint32_t>(per, c->tune.p1_slots);
             if (c->tune.p1_slots < 0) slots = per;   // one tile per workgroup
             PassArgs ak = a;
+            const bool prof = pipe && c->tune.p1_prof && kblock == 1024;
+            if (prof) {   // diagnostics (PHJ_P1_PROF): synchronous, to stderr
+                PHJ_TRY(ensure(c, c->cl_prof, 64 * 8));   // words 32.. (the LDS join's are 0..)
+                ak.prof = static_cast<unsigned long long*>(c->cl_prof.p) + 32;
+                PHJ_HIP(c, hipMemsetAsync(ak.prof, 0, kP1ProfWords * 8, c->ks));
+            }
             void* kargs[] = {&ak, const_cast<uint32_t*>(&ntiles), const_cast<uint32_t*>(&per)};
             PHJ_HIP(c, hipLaunchKernel(kfn, dim3(slots * a.nshards), dim3(kblock), kargs, lds, c->ks));
             PHJ_LAUNCHED(c, sname);
+            if (prof) {
+                unsigned long long h[kP1ProfWords] = {};
+                PHJ_HIP(c, hipMemcpyAsync(h, ak.prof, sizeof(h), hipMemcpyDeviceToHost, c->ks));
+                PHJ_HIP(c, hipStreamSynchronize(c->ks));
+                const double n = h[7] ? static_cast<double>(h[7]) : 1.0;
+                std::fprintf(stderr, "p1_prof %s grid %u: cycles per tile: hash+rank %.0f B1 %.0f scan %.0f claims+B2 %.0f scatter+protocol %.0f B3 %.0f write %.0f; tiles %llu; "
+                             "waves' max/mean B3->B1 %.0f/%.0f B1->B2 %.0f/%.0f B2->B3 %.0f/%.0f\n",
+                             sname.c_str(), slots * a.nshards, h[0] / n, h[1] / n, h[2] / n, h[3] / n, h[4] / n, h[5] / n, h[6] / n, h[7],
+                             h[8] / n, h[11] / n, h[9] / n, h[12] / n, h[10] / n, h[13] / n);
+            }
         } else {
             (void)grid;
             return set_err(c, PHJ_ERR_INVALID, "chunked pass 1 needs AoS input and output, <= 8 tuples per thread");
@@ -1424,17 +1461,23 @@ int probe_cluster(phj_ctx* c, const Plan& pl, SideState& PS, int nseg, const int
         c->split_words = a.split;
     }
     constexpr int B = kClBlock, I = kClItems;
-    const size_t lds = static_cast<size_t>(a.cap) * 8;
+    const size_t lds = static_cast<size_t>(a.cap) * (c->tune.cl_cnt ? 9 : 8);
     if (c->tune.cl_prof) {
-        PHJ_TRY(ensure(c, c->cl_prof, kClProfWords * 8));
+        PHJ_TRY(ensure(c, c->cl_prof, 64 * 8));
         a.prof = static_cast<unsigned long long*>(c->cl_prof.p);
         PHJ_HIP(c, hipMemsetAsync(a.prof, 0, kClProfWords * 8, c->ks));
     }
-    const void* kfn = c->tune.cl_prof      ? reinterpret_cast<const void*>(&k_cluster_probe<B, I, 3, true, true>)
-                      : !c->tune.cl_pre      ? reinterpret_cast<const void*>(&k_cluster_probe<B, I, 2, false>)
-                      : c->tune.cl_pf == 2 ? reinterpret_cast<const void*>(&k_cluster_probe<B, I, 2>)
-                      : c->tune.cl_pf == 3 ? reinterpret_cast<const void*>(&k_cluster_probe<B, I, 3>)
-                                           : reinterpret_cast<const void*>(&k_cluster_probe<B, I, 1>);
+    // (table builds by fill counters: every prefetch form; by compare-and-swap:
+    // the default form, for comparison)
+    const bool pre = c->tune.cl_pre, pr = c->tune.cl_prof != 0;
+    const int pf = c->tune.cl_pf;
+    const void* kfn = !c->tune.cl_cnt ? (pr ? reinterpret_cast<const void*>(&k_cluster_probe<B, I, 3, true, true, false>)
+                                            : reinterpret_cast<const void*>(&k_cluster_probe<B, I, 3, true, false, false>))
+                      : pr            ? reinterpret_cast<const void*>(&k_cluster_probe<B, I, 3, true, true, true>)
+                      : !pre          ? reinterpret_cast<const void*>(&k_cluster_probe<B, I, 2, false, false, true>)
+                      : pf == 2       ? reinterpret_cast<const void*>(&k_cluster_probe<B, I, 2, true, false, true>)
+                      : pf == 3       ? reinterpret_cast<const void*>(&k_cluster_probe<B, I, 3, true, false, true>)
+                                      : reinterpret_cast<const void*>(&k_cluster_probe<B, I, 1, true, false, true>);
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, B, lds) != hipSuccess || per_cu < 1) per_cu = 1;
     per_cu = std::max(1, std::min<int>(per_cu, static_cast<int>(160 * 1024 / (lds + 256))));
@@ -1816,6 +1859,11 @@ int ctx_create_device(int device, phj_ctx** out) {
     c->tune.p1_slots = env_int("PHJ_P1_SLOTS", 0);
     c->tune.p1_wpc2 = std::max(0, env_int("PHJ_P1_WPC2", 2));
     c->tune.cl_prof = env_int("PHJ_CL_PROF", 0);
+    c->tune.cl_cnt = env_int("PHJ_CL_CNT", 1);
+    c->tune.p1_prof = env_int("PHJ_P1_PROF", 0);
+    c->tune.p1_kpf = env_int("PHJ_P1_KPF", 1) == 2 ? 2 : 1;
+    c->tune.r_order = std::min(2, std::max(0, env_int("PHJ_R_ORDER", 0)));
+    c->tune.p1_wpe = env_int("PHJ_P1_WPE", 0);
     c->tune.p1_block = env_int("PHJ_P1_BLOCK", 1024) == 512 ? 512 : 1024;
     c->tune.p1_tps = std::max(1, env_int("PHJ_P1_TPS", static_cast<int>(kTilesPerShard)));
     c->tune.p1_min_tiles = std::max(0, env_int("PHJ_P1_MIN_TILES", 32768));
@@ -2228,27 +2276,43 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
         // LDS and probes S's codes against it
         PHJ_TRY(ensure(c, c->count, 32));
         PHJ_TRY(mark(c, &t0));
+        const int64_t* rcodes = nullptr;
+        const uint32_t* rbnd = nullptr;
+        // R's chain on the aux stream, after event `after`
+        auto r_chain = [&](hipEvent_t after) -> int {
+            PHJ_HIP(c, hipStreamWaitEvent(c->aux, after, 0));
+            c->ks = c->aux;
+            int rc = ensure(c, c->r_codes, std::max<uint64_t>(1, R.n) * 8);
+            if (rc == PHJ_OK) rc = ensure(c, c->r_bounds, (static_cast<size_t>(cpl.nb1) + 1) * 4);
+            rcodes = static_cast<const int64_t*>(c->r_codes.p);
+            rbnd = static_cast<const uint32_t*>(c->r_bounds.p);
+            if (rc == PHJ_OK) rc = partition_build(c, cpl, static_cast<int64_t*>(c->r_codes.p), static_cast<uint32_t*>(c->r_bounds.p));
+            if (rc == PHJ_OK) rc = mark(c, &b0);
+            // the HBM tables of clusters beyond the LDS limit (none at the
+            // balanced configurations; the LDS tables are built inside the probe)
+            if (rc == PHJ_OK) rc = timer_begin(c, "build.big", 0);
+            if (rc == PHJ_OK) rc = cluster_big_fill(c, cpl, 1, &rcodes, &rbnd, R.n);
+            if (rc == PHJ_OK) rc = timer_end(c);
+            if (rc == PHJ_OK) rc = mark(c, &tr);
+            c->ks = c->stream;
+            return rc;
+        };
+        // PHJ_R_ORDER: 0 = R's chain beside S's pass 1 (it waits for t0: the
+        // previous step's probe read R's codes), 1 = after S's pass 1, 2 = before it
+        const int order = c->tune.r_order;
+        if (order == 2) {
+            PHJ_TRY(r_chain(t0));
+            PHJ_HIP(c, hipStreamWaitEvent(c->stream, tr, 0));
+        }
         // the code pass's bookkeeping kernel clears the count pair (an empty
         // S takes no chunked pass: a memset)
         PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, cpl, true, static_cast<unsigned long long*>(c->count.p)));
         if (!S.hcoded) PHJ_HIP(c, hipMemsetAsync(c->count.p, 0, 32, c->stream));
-        // R's chain waits for t0 (the previous step's probe read R's codes)
-        PHJ_HIP(c, hipStreamWaitEvent(c->aux, t0, 0));
-        c->ks = c->aux;
-        int rc = ensure(c, c->r_codes, std::max<uint64_t>(1, R.n) * 8);
-        if (rc == PHJ_OK) rc = ensure(c, c->r_bounds, (static_cast<size_t>(cpl.nb1) + 1) * 4);
-        const int64_t* rcodes = static_cast<const int64_t*>(c->r_codes.p);
-        const uint32_t* rbnd = static_cast<const uint32_t*>(c->r_bounds.p);
-        if (rc == PHJ_OK) rc = partition_build(c, cpl, static_cast<int64_t*>(c->r_codes.p), static_cast<uint32_t*>(c->r_bounds.p));
-        if (rc == PHJ_OK) rc = mark(c, &b0);
-        // the HBM tables of clusters beyond the LDS limit (none at the
-        // balanced configurations; the LDS tables are built inside the probe)
-        if (rc == PHJ_OK) rc = timer_begin(c, "build.big", 0);
-        if (rc == PHJ_OK) rc = cluster_big_fill(c, cpl, 1, &rcodes, &rbnd, R.n);
-        if (rc == PHJ_OK) rc = timer_end(c);
-        if (rc == PHJ_OK) rc = mark(c, &tr);
-        c->ks = c->stream;
-        PHJ_TRY(rc);
+        if (order != 2) {
+            hipEvent_t after = t0;
+            if (order == 1) PHJ_TRY(mark(c, &after));
+            PHJ_TRY(r_chain(after));
+        }
         PHJ_HIP(c, hipStreamWaitEvent(c->stream, tr, 0));
         PHJ_TRY(mark(c, &t1));
         // one launch, reported as "build" (the workgroups' table builds in LDS:

@@ -194,10 +194,17 @@ __global__ __launch_bounds__(256) void k_cluster_probe_big(ClusterArgs a) {
 // already loaded into registers (its runs staged in the other LDS run buffer
 // during this cluster's build), so a build waits on no memory; only the
 // first build of a workgroup, or a cluster its range skips, loads in place.
-template <int BLOCK, int ITEMS, int PF = 1, bool PRE = true, bool PROF = false>
+// CNT: inserts by bucket fill counters (16 bits per bucket, after the table in
+// LDS: cap bytes): one 32-bit LDS atomic add per bucket tried and a plain
+// store, not 64-bit compare-and-swaps slot by slot. A duplicate R code then
+// takes a second slot (the count is a set test: a probe stops at the first
+// match either way); a bucket's attempts are at most the cluster's codes
+// (<= lim < 2^16), so a counter never carries into its neighbour.
+template <int BLOCK, int ITEMS, int PF = 1, bool PRE = true, bool PROF = false, bool CNT = false>
 __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
     constexpr int CPL = kClCapMax * 3 / 4 / BLOCK;   // R codes per lane at the limit
-    extern __shared__ __attribute__((aligned(16))) uint64_t tab[];   // [cap]
+    extern __shared__ __attribute__((aligned(16))) uint64_t tab[];   // [cap] (+ CNT: cap / 4 words of fill counters)
+    uint32_t* const fill = reinterpret_cast<uint32_t*>(tab + a.cap);
     __shared__ uint32_t sseg_[2][kHtSegs + 1];
     __shared__ const int64_t* sptr_[2][kHtSegs];
     __shared__ uint32_t sB_[2];
@@ -214,7 +221,8 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
     uint32_t hits = 0;
     const unsigned long long clk0 = wall_clock64();
     unsigned long long clk_b = 0;   // wall clock in table builds (workgroup-uniform sections)
-    unsigned long long prof[kClProfWords] = {};
+    __shared__ unsigned long long prof[PROF ? kClProfWords : 1];   // thread 0's sums (workgroup-uniform sections)
+    if (PROF && tid < kClProfWords) prof[tid] = 0;
     if (t_lo < t_hi) {   // workgroup-uniform
         // PF register buffers of tile codes, used in turn (no register moves:
         // a move of a register a load is still writing waits for that load).
@@ -307,7 +315,7 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
             __syncthreads();   // every probe of the previous table is done
             const unsigned long long cb = wall_clock64();
             uint64_t rc[CPL];
-            if (PROF) prof[5] += PRE && pre == d ? 0u : 1u;
+            if (PROF && tid == 0) prof[5] += PRE && pre == d ? 0u : 1u;
             if (PRE && pre == d) {   // runs staged in the other buffer, codes in registers
                 pb ^= 1u;
 #pragma unroll
@@ -328,6 +336,8 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
                 bmask = a.cap / 2 - 1;
                 ulonglong2* t2 = reinterpret_cast<ulonglong2*>(tab);
                 for (uint32_t b = tid; b <= bmask; b += BLOCK) t2[b] = make_ulonglong2(e, e);
+                if (CNT)
+                    for (uint32_t w = tid; w < a.cap / 4; w += BLOCK) fill[w] = 0;
             } else {
                 bmask = cl_big_cap(m) / 2 - 1;
             }
@@ -336,7 +346,24 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
             if (nxt) cl_runs(a, d + 1, sseg_[pb ^ 1u], sptr_[pb ^ 1u], &sB_[pb ^ 1u]);
             __syncthreads();   // cleared; the next runs staged
             if (PROF) c2 = wall_clock64();
-            if (!big) {
+            if (CNT && !big) {
+#pragma unroll
+                for (int j = 0; j < CPL; j++) {
+                    if (j * BLOCK + tid < m) {
+                        const uint64_t c = rc[j];
+                        uint32_t b = static_cast<uint32_t>(c >> kHtBucketShift) & bmask;
+                        for (;;) {
+                            const uint32_t sh = (b & 1u) * 16u;
+                            const uint32_t pos = (atomicAdd(&fill[b >> 1], 1u << sh) >> sh) & 0xffffu;
+                            if (pos < 2) {
+                                tab[2 * b + pos] = c;
+                                break;
+                            }
+                            b = (b + 1) & bmask;
+                        }
+                    }
+                }
+            } else if (!big) {
 #pragma unroll
                 for (int j = 0; j < CPL; j++) {
                     if (j * BLOCK + tid < m) {
@@ -374,7 +401,7 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
             cur = d;
             const unsigned long long c4 = wall_clock64();
             clk_b += c4 - cb;
-            if (PROF) {
+            if (PROF && tid == 0) {
                 prof[0] += c1 - cb;
                 prof[1] += c2 - c1;
                 prof[2] += c3 - c2;
@@ -441,7 +468,7 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
             atomicAdd(&a.split[1], all - clk_b);
         }
         if (PROF && a.prof)
-            for (int w = 0; w < kClProfWords; w++) atomicAdd(&a.prof[w], prof[w]);
+            for (int w = 0; w < kClProfWords; w++) atomicAdd(&a.prof[w], prof[PROF ? w : 0]);
     }
     fold_pass1_error(a.err, a.count);
 }

@@ -138,7 +138,9 @@ struct PassArgs {
     uint32_t keys_only;         // chunked pass 1 for the counting probe: only the key column is written / read
     unsigned long long* sink;   // k_chunk_codes: [kSinkGroups][BLOCK] words the stores past the tile target (never read)
     DigitFn f;
+    unsigned long long* prof;   // k_chunk_codes_pipe PROF: clocks of its phases, kP1ProfWords (diagnostics)
 };
+constexpr int kP1ProfWords = 16;
 
 // Workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md,
 // "Workgroup dispatch"); with xcd_remap each XCD instead walks a contiguous
@@ -1101,8 +1103,16 @@ __host__ __device__ constexpr size_t chunk_pipe_lds_bytes(int T, uint32_t nb) {
     return 2 * static_cast<size_t>(T) * 8 + (static_cast<size_t>(2 * nb + 3) / 4 * 4 + 2 * 4 * static_cast<size_t>(nb)) * 4 + 128;
 }
 
-template <int BLOCK, int ITEMS, int HK, int DPT = 1>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(BLOCK / 256)))   // one workgroup per CU (LDS): the registers of two
+// Registers: one workgroup per CU (LDS). WPE: waves per SIMD the registers
+// must allow (0: the workgroup's own, BLOCK / 256). 1024 threads at 5 (<= 96
+// VGPRs) leave room in each SIMD's register file for R's pass-1 kernels on
+// the other stream; at 104-128 the file is full and they wait for this pass.
+// PROF: thread 0's clock64 between the phases of each tile, summed per
+// workgroup into a.prof: hash + rank, B1, scan, claims + B2, scatter +
+// protocol, B3, write-out, then the tiles (diagnostics; the barriers' times
+// are wave 0's waits for the slowest wave).
+template <int BLOCK, int ITEMS, int HK, int DPT = 1, int WPE = 0, bool PROF = false, int KPF = 1>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE ? WPE : BLOCK / 256)))
 void k_chunk_codes_pipe(PassArgs a, uint32_t ntiles, uint32_t per) {
     constexpr int NW = BLOCK / 64;
     constexpr int T = BLOCK * ITEMS;
@@ -1131,21 +1141,60 @@ void k_chunk_codes_pipe(PassArgs a, uint32_t ntiles, uint32_t per) {
         else return static_cast<uint32_t>(q_from_hash(h, a.f) >> a.f.shift) & a.f.dmask;
     };
     int64_t* const ssink = reinterpret_cast<int64_t*>(a.sink + static_cast<size_t>(blockIdx.x % kSinkGroups) * BLOCK + tid);
+    __shared__ unsigned long long prof[PROF ? kP1ProfWords : 1];
+    if (PROF && tid < kP1ProfWords) prof[tid] = 0;
+    long long pc0 = 0;
+    auto ptick = [&](int w) {
+        if constexpr (PROF) {
+            const long long now = clock64();
+            if (tid == 0) prof[w] += static_cast<unsigned long long>(now - pc0);
+            pc0 = now;
+        }
+    };
+    // per wave: its clock from a barrier's exit to the next barrier's arrival,
+    // max and mean over the waves (regions: B3 -> B1, B1 -> B2, B2 -> B3)
+    __shared__ uint32_t parr[PROF ? 3 : 1][PROF ? NW : 1];
+    long long px = 0;
+    auto parrive = [&](int r) {
+        if constexpr (PROF)
+            if (lane == 0) parr[r][wave] = static_cast<uint32_t>(clock64() - px);
+    };
+    auto pexit = [&](int r) {
+        if constexpr (PROF) {
+            px = clock64();
+            if (tid == 0) {
+                uint32_t mx = 0;
+                unsigned long long sm = 0;
+                for (int w = 0; w < NW; w++) {
+                    mx = max(mx, parr[r][w]);
+                    sm += parr[r][w];
+                }
+                prof[8 + r] += mx;
+                prof[11 + r] += sm / NW;
+            }
+        }
+    };
 
-    int64_t key[ITEMS];
+    // KPF register buffers of keys used in turn (the loop unrolled KPF times,
+    // so no register moves): tile t's keys were requested KPF tiles earlier
+    int64_t key[KPF][ITEMS];
     const longlong2* rel = reinterpret_cast<const longlong2*>(a.in_keys);
-    auto load = [&](uint32_t t) {
+    auto load = [&](int64_t* k, uint32_t t) {
         const uint32_t lo = t * T;
 #pragma unroll
         for (int i = 0; i < ITEMS; i++) {
             const uint32_t ix = min(lo + wbase + i * 64 + lane, a.n - 1);
-            if (a.nt_load) key[i] = __builtin_nontemporal_load(&rel[ix].x);
-            else key[i] = rel[ix].x;
+            if (a.nt_load) k[i] = __builtin_nontemporal_load(&rel[ix].x);
+            else k[i] = rel[ix].x;
         }
     };
 
     for (uint32_t i = tid; i < 2 * nb; i += BLOCK) wcnt[i] = 0;
-    load(tile);
+#pragma unroll
+    for (int f = 0; f < KPF; f++) {
+        const uint32_t t = tile + f * slots;
+        load(key[f], t < t_end ? t : tile);
+    }
     {
 #pragma unroll
         for (int i = 0; i < ITEMS; i++) {
@@ -1167,7 +1216,9 @@ void k_chunk_codes_pipe(PassArgs a, uint32_t ntiles, uint32_t per) {
     bool have_prev = false;
     uint32_t pcnt = 0, par = 0;
     const uint32_t d0 = tid * DPT;
-    for (;;) {
+    if (PROF) pc0 = px = clock64();
+    auto iter = [&](auto kbc) -> bool {
+        constexpr int kb = decltype(kbc)::value;
         const bool live = tile < t_end;   // workgroup-uniform; false: the drain of the last tile
         uint32_t* const crow = wcnt + par * nb;
         const uint32_t cnt = live ? min(static_cast<uint32_t>(T), a.n - tile * T) : 0u;
@@ -1178,18 +1229,23 @@ void k_chunk_codes_pipe(PassArgs a, uint32_t ntiles, uint32_t per) {
             auto hash_all = [&](auto pow2) {
 #pragma unroll
                 for (int i = 0; i < ITEMS; i++) {
-                    const uint64_t h = hash64<HK>(static_cast<uint64_t>(key[i]), a.f.seed);
+                    const uint64_t h = hash64<HK>(static_cast<uint64_t>(key[kb][i]), a.f.seed);
                     code[i] = static_cast<int64_t>(h);
                     dig[i] = wbase + i * 64 + lane < cnt ? code_digit(h, pow2) : 0u;
                 }
             };
             if (pow2q) hash_all(std::true_type{});
             else hash_all(std::false_type{});
-            load(next < t_end ? next : tile);
+            const uint32_t ahead = tile + KPF * slots;
+            load(key[kb], ahead < t_end ? ahead : tile);
 #pragma unroll
             for (int i = 0; i < ITEMS; i++) rank[i] = atomicAdd(&crow[dig[i]], wbase + i * 64 + lane < cnt ? 1u : 0u);
         }
+        ptick(0);
+        parrive(0);
         __syncthreads();   // B1: ranks counted
+        ptick(1);
+        pexit(0);
         uint32_t c[DPT], ds[DPT], v0[DPT];
         unsigned long long hint[DPT];
         {
@@ -1209,6 +1265,7 @@ void k_chunk_codes_pipe(PassArgs a, uint32_t ntiles, uint32_t per) {
                 v0[j] = 0;
                 hint[j] = 0;
             }
+            ptick(2);
             if (live) {   // claims of every digit (0 adds too): resolved next iteration
 #pragma unroll
                 for (int j = 0; j < DPT; j++) {
@@ -1225,7 +1282,10 @@ void k_chunk_codes_pipe(PassArgs a, uint32_t ntiles, uint32_t per) {
                 tmp[20] = 0;
             }
         }
+        parrive(1);
         __syncthreads();   // B2: tile-local starts, reservations
+        ptick(3);
+        pexit(1);
         if (live) {
             uint32_t base[ITEMS];
 #pragma unroll
@@ -1309,7 +1369,11 @@ void k_chunk_codes_pipe(PassArgs a, uint32_t ntiles, uint32_t per) {
                 atomicOr(errw, bad);
             }
         }
+        ptick(4);
+        parrive(2);
         __syncthreads();   // B3: the previous tile's slots, this tile sorted
+        ptick(5);
+        pexit(2);
         if (have_prev) {
             const uint32_t lim = tmp[20] ? 0u : pcnt;
             auto write_out = [&](auto pow2) {
@@ -1329,7 +1393,13 @@ void k_chunk_codes_pipe(PassArgs a, uint32_t ntiles, uint32_t per) {
             if (pow2q) write_out(std::true_type{});
             else write_out(std::false_type{});
         }
-        if (!live) return;
+        ptick(6);
+        if (PROF && tid == 0) prof[PROF ? 7 : 0] += 1;
+        if (!live) {
+            if (PROF && tid == 0 && a.prof)
+                for (int w = 0; w < kP1ProfWords; w++) atomicAdd(&a.prof[w], prof[PROF ? w : 0]);
+            return false;
+        }
 #pragma unroll
         for (int j = 0; j < DPT; j++) {
             pv0[j] = v0[j];
@@ -1341,6 +1411,15 @@ void k_chunk_codes_pipe(PassArgs a, uint32_t ntiles, uint32_t per) {
         have_prev = true;
         tile = next;
         par ^= 1u;
+        return true;
+    };
+    if constexpr (KPF == 1) {
+        while (iter(std::integral_constant<int, 0>{})) {
+        }
+    } else {
+        static_assert(KPF == 2, "one or two tiles of keys in flight");
+        while (iter(std::integral_constant<int, 0>{}) && iter(std::integral_constant<int, 1>{})) {
+        }
     }
 }
 

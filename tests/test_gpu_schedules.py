@@ -60,10 +60,18 @@ SCHEDULES = [
     {"PHJ_CL_PF": "1"},                                         # LDS join probe: one register buffer of codes (no prefetch)
     {"PHJ_CL_PF": "2"},                                         # ... two
     {"PHJ_CL_PRE": "0"},                                        # ... each cluster's R codes loaded when its build starts
+    {"PHJ_CL_CNT": "0"},                                        # ... tables built by 64-bit compare-and-swap, not fill counters
+    {"PHJ_CL_CNT": "0", "PHJ_CL_CAP": "8192"},                  # ... in 64 KB tables
     {"PHJ_P1_PIPE": "0"},                                       # keys-only pass 1 resolving its claims in the same tile
     {"PHJ_P1_PIPE": "0", "PHJ_CL_BITS": "11"},                  # ... with four digits per thread
     {"PHJ_P1_BLOCK": "512"},                                    # pipelined pass 1 in 512 x 8 workgroups
     {"PHJ_P1_BLOCK": "512", "PHJ_CL_BITS": "11"},               # ... four digits per thread
+    {"PHJ_P1_KPF": "2"},                                        # ... two tiles of keys in flight
+    {"PHJ_P1_KPF": "2", "PHJ_CL_BITS": "11"},                   # ... with two digits per thread
+    {"PHJ_R_ORDER": "1"},                                       # LDS join: R's pass 1 after S's
+    {"PHJ_R_ORDER": "2"},                                       # ... before it
+    {"PHJ_P1_WPE": "5"},                                        # ... 1024 x 4 held to 96 VGPRs (spills)
+    {"PHJ_P1_PROF": "1", "PHJ_CL_PROF": "1"},                   # the phase clocks of pass 1 and of the LDS join's builds
 ]
 
 CASES = [((8, 8), 0, phj.HASH_MURMUR3), ((11, 0), 0, phj.HASH_XXH3), ((1, 0), 1000, phj.HASH_XXH3),
