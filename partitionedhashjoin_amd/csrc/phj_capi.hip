@@ -58,9 +58,8 @@ struct Tuning {
     int p1_ko_tps = 1024;      // ... the keys-only form for the on-chip probe: tiles per shard (at every size)
     int p2probe = 1;      // radix join, 2 passes: the probe side's pass 2 on-chip (k_probe_ht)
     int p1_pipe = 1;      // keys-only pass 1: claims resolved a tile later over pre-allocated chunks (k_chunk_codes_pipe)
-    int p1_wpe = 0;       // ... 1024 x 4: waves per SIMD its registers allow (5: <= 96 VGPRs, room for R's kernels)
-    int r_order = 0;      // LDS join: R's pass 1 beside S's (0), after it (1), before it (2)
-    int p1_kpf = 1;       // ... 1024 x 4: tiles of keys in flight ahead of the one hashed (1 or 2)
+    int r_order = 1;      // LDS join: R's pass 1 beside S's (0), after it (1: measured C2 1.69 vs 1.72 ms, S.p1 1.05 vs 1.19), before it (2)
+    int p1_kpf = 2;       // ... 1024 x 4: tiles of keys in flight ahead of the one hashed (1 or 2; 2 measured 1.08 -> 1.05 ms)
     int p1_prof = 0;      // PHJ_P1_PROF: the pipelined pass 1's phases to stderr (diagnostics)
     int cl_cnt = 1;       // ... tables built by bucket fill counters (k_cluster_probe CNT; measured build 0.082 -> 0.055 ms at C2)
     int cl_prof = 0;      // PHJ_CL_PROF: the LDS join's build sections to stderr (diagnostics)
@@ -554,6 +553,15 @@ int scan_u32(phj_ctx* c, uint32_t* data, uint32_t len, uint32_t narrays, uint32_
 }
 
 
+// The pipelined code pass in 1024 x 4 workgroups: KPF tiles of keys in
+// flight (1 or 2); the phase-clock form (PHJ_P1_PROF) at KPF 2.
+template <int HK, int DPT>
+const void* pipe1024(int kpf, bool prof) {
+    if (prof) return reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, HK, DPT, 0, true, 2>);
+    return kpf == 1 ? reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, HK, DPT, 0, false, 1>)
+                    : reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, HK, DPT, 0, false, 2>);
+}
+
 template <int BLOCK, int ITEMS, bool IN_AOS, bool OUT_AOS>
 int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const std::string& prefix,
                   uint64_t n, uint32_t hist_len) {
@@ -585,28 +593,10 @@ int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const st
                     const int dpt = a.nbins > 2 * BLOCK ? 4 : a.nbins > BLOCK ? 2 : 1;
                     if (c->tune.p1_block == 1024) {   // 16 waves per CU, 4 codes per thread
                         kblock = 1024;
-                        const bool w5 = c->tune.p1_wpe == 5;
-                        if (c->tune.p1_kpf == 2)
-                            kfn = hk == kMurmur3 ? (dpt == 4 ? reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kMurmur3, 2, 0, false, 2>)
-                                                             : reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kMurmur3, 1, 0, false, 2>))
-                                                 : (dpt == 4 ? reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kXXH3, 2, 0, false, 2>)
-                                                             : reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kXXH3, 1, 0, false, 2>));
-                        else if (c->tune.p1_prof)
-                            kfn = hk == kMurmur3 ? (dpt == 4 ? reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kMurmur3, 2, 0, true>)
-                                                             : reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kMurmur3, 1, 0, true>))
-                                                 : (dpt == 4 ? reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kXXH3, 2, 0, true>)
-                                                             : reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kXXH3, 1, 0, true>));
-                        else
-                        if (hk == kMurmur3)
-                            kfn = dpt == 4 ? (w5 ? reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kMurmur3, 2, 5>)
-                                                 : reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kMurmur3, 2>))
-                                           : (w5 ? reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kMurmur3, 1, 5>)
-                                                 : reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kMurmur3, 1>));
-                        else
-                            kfn = dpt == 4 ? (w5 ? reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kXXH3, 2, 5>)
-                                                 : reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kXXH3, 2>))
-                                           : (w5 ? reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kXXH3, 1, 5>)
-                                                 : reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, kXXH3, 1>));
+                        const int kpf = c->tune.p1_kpf;
+                        const bool pr = c->tune.p1_prof != 0;
+                        kfn = hk == kMurmur3 ? (dpt == 4 ? pipe1024<kMurmur3, 2>(kpf, pr) : pipe1024<kMurmur3, 1>(kpf, pr))
+                                             : (dpt == 4 ? pipe1024<kXXH3, 2>(kpf, pr) : pipe1024<kXXH3, 1>(kpf, pr));
                     } else if (hk == kMurmur3)
                         kfn = dpt == 4 ? reinterpret_cast<const void*>(&k_chunk_codes_pipe<BLOCK, ITEMS, kMurmur3, 4>)
                             : dpt == 2 ? reinterpret_cast<const void*>(&k_chunk_codes_pipe<BLOCK, ITEMS, kMurmur3, 2>)
@@ -1861,9 +1851,8 @@ int ctx_create_device(int device, phj_ctx** out) {
     c->tune.cl_prof = env_int("PHJ_CL_PROF", 0);
     c->tune.cl_cnt = env_int("PHJ_CL_CNT", 1);
     c->tune.p1_prof = env_int("PHJ_P1_PROF", 0);
-    c->tune.p1_kpf = env_int("PHJ_P1_KPF", 1) == 2 ? 2 : 1;
-    c->tune.r_order = std::min(2, std::max(0, env_int("PHJ_R_ORDER", 0)));
-    c->tune.p1_wpe = env_int("PHJ_P1_WPE", 0);
+    c->tune.p1_kpf = env_int("PHJ_P1_KPF", 2) == 1 ? 1 : 2;
+    c->tune.r_order = std::min(2, std::max(0, env_int("PHJ_R_ORDER", 1)));
     c->tune.p1_block = env_int("PHJ_P1_BLOCK", 1024) == 512 ? 512 : 1024;
     c->tune.p1_tps = std::max(1, env_int("PHJ_P1_TPS", static_cast<int>(kTilesPerShard)));
     c->tune.p1_min_tiles = std::max(0, env_int("PHJ_P1_MIN_TILES", 32768));

@@ -315,7 +315,7 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
             __syncthreads();   // every probe of the previous table is done
             const unsigned long long cb = wall_clock64();
             uint64_t rc[CPL];
-            if (PROF && tid == 0) prof[5] += PRE && pre == d ? 0u : 1u;
+            if (PROF && tid == 0) prof[PROF ? 5 : 0] += PRE && pre == d ? 0u : 1u;
             if (PRE && pre == d) {   // runs staged in the other buffer, codes in registers
                 pb ^= 1u;
 #pragma unroll
@@ -403,10 +403,10 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
             clk_b += c4 - cb;
             if (PROF && tid == 0) {
                 prof[0] += c1 - cb;
-                prof[1] += c2 - c1;
-                prof[2] += c3 - c2;
-                prof[3] += c4 - c3;
-                prof[4] += 1;
+                prof[PROF ? 1 : 0] += c2 - c1;
+                prof[PROF ? 2 : 0] += c3 - c2;
+                prof[PROF ? 3 : 0] += c4 - c3;
+                prof[PROF ? 4 : 0] += 1;
             }
         };
         const ulonglong2* tb = reinterpret_cast<const ulonglong2*>(tab);

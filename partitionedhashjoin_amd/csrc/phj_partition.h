@@ -1104,13 +1104,13 @@ __host__ __device__ constexpr size_t chunk_pipe_lds_bytes(int T, uint32_t nb) {
 }
 
 // Registers: one workgroup per CU (LDS). WPE: waves per SIMD the registers
-// must allow (0: the workgroup's own, BLOCK / 256). 1024 threads at 5 (<= 96
-// VGPRs) leave room in each SIMD's register file for R's pass-1 kernels on
-// the other stream; at 104-128 the file is full and they wait for this pass.
+// must allow (0: the workgroup's own, BLOCK / 256; 1024 x 4 held to 5, <= 96
+// VGPRs, spilled and ran 1.12 -> 1.54 ms at C2, so none is instantiated).
 // PROF: thread 0's clock64 between the phases of each tile, summed per
-// workgroup into a.prof: hash + rank, B1, scan, claims + B2, scatter +
-// protocol, B3, write-out, then the tiles (diagnostics; the barriers' times
-// are wave 0's waits for the slowest wave).
+// workgroup into a.prof: hash + rank, B1, scan,
+// claims + B2, scatter + protocol, B3, write-out, then the tiles, and each
+// wave's time from a barrier to the next (max / mean over the waves)
+// (diagnostics; a barrier's time is wave 0's wait for the slowest wave).
 template <int BLOCK, int ITEMS, int HK, int DPT = 1, int WPE = 0, bool PROF = false, int KPF = 1>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE ? WPE : BLOCK / 256)))
 void k_chunk_codes_pipe(PassArgs a, uint32_t ntiles, uint32_t per) {
@@ -1136,10 +1136,21 @@ void k_chunk_codes_pipe(PassArgs a, uint32_t ntiles, uint32_t per) {
     unsigned long long* hints = reinterpret_cast<unsigned long long*>(a.chunk_cursor + chunk_hint_word(nb)) + static_cast<size_t>(x) * nb;
     const uint32_t id_lo = x * a.pool_stride, id_hi = id_lo + a.pool_stride;
     const bool pow2q = a.f.mode == 0 && a.f.sub_bits == 0;
-    auto code_digit = [&](uint64_t h, auto pow2) -> uint32_t {
-        if constexpr (decltype(pow2)::value) return static_cast<uint32_t>((h & (a.f.P - 1)) >> a.f.shift) & a.f.dmask;
+    // digit forms (workgroup-uniform): 2 = one bit-field extract (q = h mod a
+    // power of two <= 2^32 and the digit's bits inside q), 1 = power of two, 0 = any plan
+    const uint32_t dwidth = __popc(a.f.dmask);
+    const int dform = pow2q && a.f.P <= (1ull << 32) && ((a.f.dmask + 1ull) & a.f.dmask) == 0 &&
+                              ((static_cast<uint64_t>(a.f.dmask) << a.f.shift) & ~(a.f.P - 1)) == 0
+                          ? 2
+                          : pow2q ? 1 : 0;
+    auto code_digit = [&](uint64_t h, auto form) -> uint32_t {
+        if constexpr (decltype(form)::value == 2) return __builtin_amdgcn_ubfe(static_cast<uint32_t>(h), a.f.shift, dwidth);
+        else if constexpr (decltype(form)::value == 1) return static_cast<uint32_t>((h & (a.f.P - 1)) >> a.f.shift) & a.f.dmask;
         else return static_cast<uint32_t>(q_from_hash(h, a.f) >> a.f.shift) & a.f.dmask;
     };
+    using F0 = std::integral_constant<int, 0>;
+    using F1 = std::integral_constant<int, 1>;
+    using F2 = std::integral_constant<int, 2>;
     int64_t* const ssink = reinterpret_cast<int64_t*>(a.sink + static_cast<size_t>(blockIdx.x % kSinkGroups) * BLOCK + tid);
     __shared__ unsigned long long prof[PROF ? kP1ProfWords : 1];
     if (PROF && tid < kP1ProfWords) prof[tid] = 0;
@@ -1204,21 +1215,30 @@ void k_chunk_codes_pipe(PassArgs a, uint32_t ntiles, uint32_t per) {
     }
     __syncthreads();
     // the previous tile's claims, resolved in this iteration
-    uint32_t pv0[DPT], pc[DPT], pds[DPT];
-    unsigned long long phint[DPT];
+    // the claims' returns (cursor, hint) in two register sets, one per
+    // iteration parity (the loop unrolled twice): a tile's claims land in set
+    // cb and are read one iteration later as the previous tile's, with no
+    // register move at the back edge (a move waits for its load, and vmcnt
+    // retires in order: it would wait for the write-out's stores as well)
+    uint32_t pc[DPT], pds[DPT], cv0[2][DPT];
+    unsigned long long chint[2][DPT];
 #pragma unroll
     for (int j = 0; j < DPT; j++) {
-        pv0[j] = 0;
         pc[j] = 0;
         pds[j] = 0;
-        phint[j] = 0;
+        cv0[0][j] = cv0[1][j] = 0;
+        chint[0][j] = chint[1][j] = 0;
     }
     bool have_prev = false;
     uint32_t pcnt = 0, par = 0;
     const uint32_t d0 = tid * DPT;
     if (PROF) pc0 = px = clock64();
-    auto iter = [&](auto kbc) -> bool {
-        constexpr int kb = decltype(kbc)::value;
+    auto iter = [&](auto kbc, auto cbc) -> bool {
+        constexpr int kb = decltype(kbc)::value, cb = decltype(cbc)::value;
+        uint32_t(&v0)[DPT] = cv0[cb];
+        unsigned long long(&hint)[DPT] = chint[cb];
+        const uint32_t(&pv0)[DPT] = cv0[cb ^ 1];
+        const unsigned long long(&phint)[DPT] = chint[cb ^ 1];
         const bool live = tile < t_end;   // workgroup-uniform; false: the drain of the last tile
         uint32_t* const crow = wcnt + par * nb;
         const uint32_t cnt = live ? min(static_cast<uint32_t>(T), a.n - tile * T) : 0u;
@@ -1226,16 +1246,22 @@ void k_chunk_codes_pipe(PassArgs a, uint32_t ntiles, uint32_t per) {
         int64_t code[ITEMS];
         uint32_t dig[ITEMS], rank[ITEMS];
         if (live) {
-            auto hash_all = [&](auto pow2) {
+            // full: a whole tile (every lane valid; the checks compiled out).
+            // The loads stay outside the forms: one instance, straight into
+            // the key buffer (a copy per form would be merged by register
+            // moves, and a move waits for its load)
+            auto hash_all = [&](auto form, auto full) {
 #pragma unroll
                 for (int i = 0; i < ITEMS; i++) {
                     const uint64_t h = hash64<HK>(static_cast<uint64_t>(key[kb][i]), a.f.seed);
                     code[i] = static_cast<int64_t>(h);
-                    dig[i] = wbase + i * 64 + lane < cnt ? code_digit(h, pow2) : 0u;
+                    dig[i] = decltype(full)::value || wbase + i * 64 + lane < cnt ? code_digit(h, form) : 0u;
                 }
             };
-            if (pow2q) hash_all(std::true_type{});
-            else hash_all(std::false_type{});
+            if (dform == 2 && cnt == static_cast<uint32_t>(T)) hash_all(F2{}, std::true_type{});
+            else if (dform == 2) hash_all(F2{}, std::false_type{});
+            else if (dform == 1) hash_all(F1{}, std::false_type{});
+            else hash_all(F0{}, std::false_type{});
             const uint32_t ahead = tile + KPF * slots;
             load(key[kb], ahead < t_end ? ahead : tile);
 #pragma unroll
@@ -1246,8 +1272,7 @@ void k_chunk_codes_pipe(PassArgs a, uint32_t ntiles, uint32_t per) {
         __syncthreads();   // B1: ranks counted
         ptick(1);
         pexit(0);
-        uint32_t c[DPT], ds[DPT], v0[DPT];
-        unsigned long long hint[DPT];
+        uint32_t c[DPT], ds[DPT];
         {
             uint32_t local = 0;
 #pragma unroll
@@ -1262,8 +1287,6 @@ void k_chunk_codes_pipe(PassArgs a, uint32_t ntiles, uint32_t per) {
                 ds[j] = run;
                 if (live && d0 + j < nb) crow[d0 + j] = run;
                 run += c[j];
-                v0[j] = 0;
-                hint[j] = 0;
             }
             ptick(2);
             if (live) {   // claims of every digit (0 adds too): resolved next iteration
@@ -1376,7 +1399,7 @@ void k_chunk_codes_pipe(PassArgs a, uint32_t ntiles, uint32_t per) {
         pexit(2);
         if (have_prev) {
             const uint32_t lim = tmp[20] ? 0u : pcnt;
-            auto write_out = [&](auto pow2) {
+            auto write_out = [&](auto form, auto full) {
                 int64_t v[ITEMS];
                 uint32_t o[ITEMS];
 #pragma unroll
@@ -1384,14 +1407,19 @@ void k_chunk_codes_pipe(PassArgs a, uint32_t ntiles, uint32_t per) {
 #pragma unroll
                 for (int i = 0; i < ITEMS; i++) {
                     const uint32_t k = i * BLOCK + tid;
-                    const uint4 w = wdesc[pp * nb + code_digit(static_cast<uint64_t>(v[i]), pow2)];
+                    const uint4 w = wdesc[pp * nb + code_digit(static_cast<uint64_t>(v[i]), form)];
                     o[i] = (k < w.z ? w.x : w.y) + k;
                 }
 #pragma unroll
-                for (int i = 0; i < ITEMS; i++) *(i * BLOCK + tid < lim ? a.out_keys + o[i] : ssink) = v[i];
+                for (int i = 0; i < ITEMS; i++) {
+                    if constexpr (decltype(full)::value) a.out_keys[o[i]] = v[i];
+                    else *(i * BLOCK + tid < lim ? a.out_keys + o[i] : ssink) = v[i];
+                }
             };
-            if (pow2q) write_out(std::true_type{});
-            else write_out(std::false_type{});
+            if (dform == 2 && lim == static_cast<uint32_t>(T)) write_out(F2{}, std::true_type{});
+            else if (dform == 2) write_out(F2{}, std::false_type{});
+            else if (dform == 1) write_out(F1{}, std::false_type{});
+            else write_out(F0{}, std::false_type{});
         }
         ptick(6);
         if (PROF && tid == 0) prof[PROF ? 7 : 0] += 1;
@@ -1402,10 +1430,8 @@ void k_chunk_codes_pipe(PassArgs a, uint32_t ntiles, uint32_t per) {
         }
 #pragma unroll
         for (int j = 0; j < DPT; j++) {
-            pv0[j] = v0[j];
             pc[j] = c[j];
             pds[j] = ds[j];
-            phint[j] = hint[j];
         }
         pcnt = cnt;
         have_prev = true;
@@ -1413,12 +1439,14 @@ void k_chunk_codes_pipe(PassArgs a, uint32_t ntiles, uint32_t per) {
         par ^= 1u;
         return true;
     };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    static_assert(KPF == 1 || KPF == 2, "one or two tiles of keys in flight");
     if constexpr (KPF == 1) {
-        while (iter(std::integral_constant<int, 0>{})) {
+        while (iter(I0{}, I0{}) && iter(I0{}, I1{})) {
         }
     } else {
-        static_assert(KPF == 2, "one or two tiles of keys in flight");
-        while (iter(std::integral_constant<int, 0>{}) && iter(std::integral_constant<int, 1>{})) {
+        while (iter(I0{}, I0{}) && iter(I1{}, I1{})) {
         }
     }
 }

@@ -66,11 +66,10 @@ SCHEDULES = [
     {"PHJ_P1_PIPE": "0", "PHJ_CL_BITS": "11"},                  # ... with four digits per thread
     {"PHJ_P1_BLOCK": "512"},                                    # pipelined pass 1 in 512 x 8 workgroups
     {"PHJ_P1_BLOCK": "512", "PHJ_CL_BITS": "11"},               # ... four digits per thread
-    {"PHJ_P1_KPF": "2"},                                        # ... two tiles of keys in flight
-    {"PHJ_P1_KPF": "2", "PHJ_CL_BITS": "11"},                   # ... with two digits per thread
-    {"PHJ_R_ORDER": "1"},                                       # LDS join: R's pass 1 after S's
+    {"PHJ_P1_KPF": "1"},                                        # ... one tile of keys in flight
+    {"PHJ_P1_KPF": "1", "PHJ_CL_BITS": "11"},                   # ... with two digits per thread
+    {"PHJ_R_ORDER": "0"},                                       # LDS join: R's pass 1 beside S's
     {"PHJ_R_ORDER": "2"},                                       # ... before it
-    {"PHJ_P1_WPE": "5"},                                        # ... 1024 x 4 held to 96 VGPRs (spills)
     {"PHJ_P1_PROF": "1", "PHJ_CL_PROF": "1"},                   # the phase clocks of pass 1 and of the LDS join's builds
 ]
 
