@@ -58,6 +58,7 @@ struct Tuning {
     int p1_ko_tps = 1024;      // ... the keys-only form for the on-chip probe: tiles per shard (at every size)
     int p2probe = 1;      // radix join, 2 passes: the probe side's pass 2 on-chip (k_probe_ht)
     int p1_pipe = 1;      // keys-only pass 1: claims resolved a tile later over pre-allocated chunks (k_chunk_codes_pipe)
+    int r_chunk = 1;      // LDS join on one device: R through the chunked code pass, read by tiles ("tile mode")
     int r_order = 1;      // LDS join: R's pass 1 beside S's (0), after it (1: measured C2 1.69 vs 1.72 ms, S.p1 1.05 vs 1.19), before it (2)
     int p1_kpf = 2;       // ... 1024 x 4: tiles of keys in flight ahead of the one hashed (1 or 2; 2 measured 1.08 -> 1.05 ms)
     int p1_prof = 0;      // PHJ_P1_PROF: the pipelined pass 1's phases to stderr (diagnostics)
@@ -752,7 +753,7 @@ int launch_pass(phj_ctx* c, int hk, bool in_aos, bool out_aos, PassArgs a, uint3
 }
 
 int partition_state(phj_ctx* c, SideState& S, const char* tag, const Plan& pl, bool p1_only,
-                    unsigned long long* zero = nullptr) {
+                    unsigned long long* zero = nullptr, uint32_t max_shards = kShards) {
     c->scan_scratch = &S.partials;
     if (!S.rel && S.n > 0) return set_err(c, PHJ_ERR_STATE, "relation not bound");
     const uint64_t n64 = S.n;
@@ -786,9 +787,12 @@ int partition_state(phj_ctx* c, SideState& S, const char* tag, const Plan& pl, b
                           ((kPipeRes + 1) * (static_cast<uint64_t>(n) / tile + kShards) + kShards * (3ull * pl.nb1 + 1)) * tile < (1ull << 32));
     S.hcoded = chunked && ko;   // k_chunk_codes
     // chains per digit: ~kTilesPerShard tiles each, a power of two <= kShards
+    // (max_shards < kShards: R in tile mode takes exactly that many, so a
+    // cluster below the LDS limit has at most max_shards + lim / tile runs)
     uint32_t nshards = 1;
-    const uint32_t tps = static_cast<uint32_t>(ko ? c->tune.p1_ko_tps : c->tune.p1_tps);
-    while (nshards < kShards && static_cast<uint64_t>(nshards) * tps < nt1) nshards <<= 1;
+    const uint32_t tps = max_shards < kShards ? std::max<uint32_t>(1, (nt1 + max_shards - 1) / max_shards)
+                                              : static_cast<uint32_t>(ko ? c->tune.p1_ko_tps : c->tune.p1_tps);
+    while (nshards < max_shards && static_cast<uint64_t>(nshards) * tps < nt1) nshards <<= 1;
     // pool of pass-1 chunks, one region per shard: a shard takes at most
     // `per` tiles, each with two chunks reserved up front (k_scatter_chunked, k_chunk_codes;
     // unused ones are never touched), then at most per + nb1 chunks for its
@@ -1328,6 +1332,27 @@ bool use_cluster(const phj_ctx* c, const Plan& pl, uint64_t nS, uint64_t nR, Pla
     return cluster_empty0(out) != 0 && 4 * nR + 2ull * out.nb1 < (1ull << 32);
 }
 
+// A multi-GPU member's R shard as codes contiguous per cluster, straight into
+// its exchange block {codes | bounds}: the chunked code pass (8 shards) and
+// k_cluster_gather (PHJ_R_CHUNK, default: one pass over R and a copy of its
+// codes, where the stable pass is a histogram, two scan launches and a
+// scatter), else partition_build. Its error word is folded by the probe.
+int cluster_r_codes(phj_ctx* c, const Plan& pl, int64_t* out, uint32_t* bounds) {
+    SideState& R = c->side[PHJ_SIDE_BUILD];
+    if (c->tune.r_chunk && R.n > 0) {
+        PHJ_TRY(partition_state(c, R, "R", pl, true, nullptr, 8));
+        if (R.hcoded) {
+            if (c->dry) return PHJ_OK;
+            PHJ_TRY(timer_begin(c, "R.gather", R.n * 16));
+            hipLaunchKernelGGL(k_cluster_gather, dim3(pl.nb1), dim3(256), 0, c->ks, R.p2.tile_base, R.p2.tile_start,
+                               R.p2.tile_cnt, R.p2.in_keys, static_cast<const uint32_t*>(R.bounds1.p), pl.nb1, out, bounds);
+            PHJ_LAUNCHED(c, "k_cluster_gather");
+            return timer_end(c);
+        }
+    }
+    return partition_build(c, pl, out, bounds);
+}
+
 // Probe a probe-side pass-1 output (partition_state p1_only) against the
 // tables of build_ht; the count lands in (clear) or is added to c->count.
 int probe_ht(phj_ctx* c, const Plan& pl, SideState& PS, bool clear = true) {
@@ -1399,12 +1424,24 @@ int check_chunk_errors(phj_ctx* c) {
 // then (probe_cluster, on the main stream) k_cluster_probe over the probe
 // side's pass-1 tiles. `nseg` build segments of codes contiguous per cluster
 // and nb1 + 1 bounds each; nR = their codes. The count pair is added to.
+// RT (tile mode, one device): R's chunked code pass; its tiles are the runs,
+// its cluster offsets (bounds1) give each cluster's size and first code.
 ClusterArgs cluster_args(phj_ctx* c, const Plan& pl, int nseg, const int64_t* const* codes,
-                         const uint32_t* const* bounds) {
+                         const uint32_t* const* bounds, SideState* RT = nullptr) {
     ClusterArgs a{};
-    for (int g = 0; g < nseg; g++) {
-        a.r_codes[g] = codes[g];
-        a.r_bounds[g] = bounds[g];
+    if (RT) {
+        nseg = 1;
+        a.r_codes[0] = RT->p2.in_keys;
+        a.r_bounds[0] = static_cast<const uint32_t*>(RT->bounds1.p);
+        a.rt_base = RT->p2.tile_base;
+        a.rt_start = RT->p2.tile_start;
+        a.rt_cnt = RT->p2.tile_cnt;
+        a.r_pool = RT->p2.in_keys;
+    } else {
+        for (int g = 0; g < nseg; g++) {
+            a.r_codes[g] = codes[g];
+            a.r_bounds[g] = bounds[g];
+        }
     }
     a.nseg = static_cast<uint32_t>(nseg);
     a.nb1 = pl.nb1;
@@ -1417,24 +1454,29 @@ ClusterArgs cluster_args(phj_ctx* c, const Plan& pl, int nseg, const int64_t* co
 }
 
 int cluster_big_fill(phj_ctx* c, const Plan& pl, int nseg, const int64_t* const* codes, const uint32_t* const* bounds,
-                     uint64_t nR) {
+                     uint64_t nR, SideState* RT = nullptr) {
     if (nseg < 1 || nseg > kHtSegs) return set_err(c, PHJ_ERR_INVALID, "build segments must be in [1,16]");
     const uint64_t slots = 4 * nR + 2ull * pl.nb1;
     if (slots >= (1ull << 32)) return set_err(c, PHJ_ERR_RANGE, "build side too large for 32-bit table slots");
     PHJ_TRY(ensure(c, c->ht_tab, slots * 8));
     PHJ_TRY(ensure(c, c->count, 32));
     if (c->dry) return PHJ_OK;
-    ClusterArgs a = cluster_args(c, pl, nseg, codes, bounds);
+    ClusterArgs a = cluster_args(c, pl, nseg, codes, bounds, RT);
     hipLaunchKernelGGL(k_cluster_big_fill, dim3(pl.nb1), dim3(256), 0, c->ks, a);
     PHJ_LAUNCHED(c, "k_cluster_big_fill");
     return PHJ_OK;
 }
 
 int probe_cluster(phj_ctx* c, const Plan& pl, SideState& PS, int nseg, const int64_t* const* codes,
-                  const uint32_t* const* bounds) {
+                  const uint32_t* const* bounds, SideState* RT = nullptr) {
     if (c->dry || PS.nt2 == 0) return PHJ_OK;
     if (!PS.hcoded) return set_err(c, PHJ_ERR_STATE, "the LDS join needs the keys-only pass 1 (codes)");
-    ClusterArgs a = cluster_args(c, pl, nseg, codes, bounds);
+    ClusterArgs a = cluster_args(c, pl, nseg, codes, bounds, RT);
+    SideState& RS = c->side[PHJ_SIDE_BUILD];
+    if (RS.chunk_check) {   // R's chunked pass-1 error word, folded into the count pair as S's
+        a.err_r = static_cast<const uint32_t*>(RS.ccur.p) + chunk_err_word(RS.plan.nb1);
+        RS.chunk_check = false;
+    }
     a.s_codes = PS.p2.in_keys;
     a.tile_base = PS.p2.tile_base;
     a.tile_seg = PS.p2.tile_seg;
@@ -1488,6 +1530,7 @@ int probe_cluster(phj_ctx* c, const Plan& pl, SideState& PS, int nseg, const int
     // other clusters return at once)
     a.split = nullptr;
     a.err = nullptr;
+    a.err_r = nullptr;
     hipLaunchKernelGGL(k_cluster_probe_big, dim3(pl.nb1), dim3(256), 0, c->ks, a);
     PHJ_LAUNCHED(c, "k_cluster_probe_big");
     return PHJ_OK;
@@ -1853,6 +1896,7 @@ int ctx_create_device(int device, phj_ctx** out) {
     c->tune.p1_prof = env_int("PHJ_P1_PROF", 0);
     c->tune.p1_kpf = env_int("PHJ_P1_KPF", 2) == 1 ? 1 : 2;
     c->tune.r_order = std::min(2, std::max(0, env_int("PHJ_R_ORDER", 1)));
+    c->tune.r_chunk = env_int("PHJ_R_CHUNK", 1) != 0;
     c->tune.p1_block = env_int("PHJ_P1_BLOCK", 1024) == 512 ? 512 : 1024;
     c->tune.p1_tps = std::max(1, env_int("PHJ_P1_TPS", static_cast<int>(kTilesPerShard)));
     c->tune.p1_min_tiles = std::max(0, env_int("PHJ_P1_MIN_TILES", 32768));
@@ -2268,19 +2312,31 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
         const int64_t* rcodes = nullptr;
         const uint32_t* rbnd = nullptr;
         // R's chain on the aux stream, after event `after`
+        // R in tile mode (PHJ_R_CHUNK, default): R through the chunked code
+        // pass as S (one launch; 8 shards, so a cluster below the LDS limit
+        // has at most 8 + 3 runs), its tiles read by the builds; else the
+        // stable pass (k_hist + scan + k_scatter_codes: codes contiguous per cluster)
+        SideState* RT = nullptr;
         auto r_chain = [&](hipEvent_t after) -> int {
             PHJ_HIP(c, hipStreamWaitEvent(c->aux, after, 0));
             c->ks = c->aux;
-            int rc = ensure(c, c->r_codes, std::max<uint64_t>(1, R.n) * 8);
-            if (rc == PHJ_OK) rc = ensure(c, c->r_bounds, (static_cast<size_t>(cpl.nb1) + 1) * 4);
-            rcodes = static_cast<const int64_t*>(c->r_codes.p);
-            rbnd = static_cast<const uint32_t*>(c->r_bounds.p);
-            if (rc == PHJ_OK) rc = partition_build(c, cpl, static_cast<int64_t*>(c->r_codes.p), static_cast<uint32_t*>(c->r_bounds.p));
+            int rc = PHJ_OK;
+            if (c->tune.r_chunk && R.n > 0) {
+                rc = partition_state(c, R, "R", cpl, true, nullptr, 8);
+                if (rc == PHJ_OK && R.hcoded) RT = &R;
+            }
+            if (!RT) {
+                if (rc == PHJ_OK) rc = ensure(c, c->r_codes, std::max<uint64_t>(1, R.n) * 8);
+                if (rc == PHJ_OK) rc = ensure(c, c->r_bounds, (static_cast<size_t>(cpl.nb1) + 1) * 4);
+                rcodes = static_cast<const int64_t*>(c->r_codes.p);
+                rbnd = static_cast<const uint32_t*>(c->r_bounds.p);
+                if (rc == PHJ_OK) rc = partition_build(c, cpl, static_cast<int64_t*>(c->r_codes.p), static_cast<uint32_t*>(c->r_bounds.p));
+            }
             if (rc == PHJ_OK) rc = mark(c, &b0);
             // the HBM tables of clusters beyond the LDS limit (none at the
             // balanced configurations; the LDS tables are built inside the probe)
             if (rc == PHJ_OK) rc = timer_begin(c, "build.big", 0);
-            if (rc == PHJ_OK) rc = cluster_big_fill(c, cpl, 1, &rcodes, &rbnd, R.n);
+            if (rc == PHJ_OK) rc = cluster_big_fill(c, cpl, 1, &rcodes, &rbnd, R.n, RT);
             if (rc == PHJ_OK) rc = timer_end(c);
             if (rc == PHJ_OK) rc = mark(c, &tr);
             c->ks = c->stream;
@@ -2307,7 +2363,7 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
         // one launch, reported as "build" (the workgroups' table builds in LDS:
         // R's codes read) and "probe" (S's codes read), split by the kernel's own clocks
         PHJ_TRY(timer_begin_split(c, R.n * 8, S.n * 8));
-        PHJ_TRY(probe_cluster(c, cpl, S, 1, &rcodes, &rbnd));
+        PHJ_TRY(probe_cluster(c, cpl, S, 1, &rcodes, &rbnd, RT));
         PHJ_TRY(timer_end_split(c));
         PHJ_TRY(mark(c, &p1));
         uint64_t m = 0;

@@ -10,8 +10,10 @@
 //   pass 1 (both sides): hash codes c = h(k) partitioned into K clusters, the
 //     top log2 K bits of the plan's partition number q (so every cluster is a
 //     union of whole final partitions of the requested radix / h % P plan);
-//     S by the chunked keys-only pass (k_chunk_codes), R by k_hist + scan +
-//     k_scatter_codes (codes contiguous per cluster).
+//     S by the chunked keys-only pass (k_chunk_codes_pipe); R by the same
+//     pass on one device (its codes read through its pass-1 tile list: "tile
+//     mode", below), or by k_hist + scan + k_scatter_codes (codes contiguous
+//     per cluster: a multi-GPU member's exchange block, or PHJ_R_CHUNK=0).
 //   probe (k_cluster_probe): persistent; workgroup w walks a contiguous range
 //     of S's pass-1 tiles (cluster-major). When the cluster changes it builds
 //     that cluster's R codes into an open-addressed table in LDS (the R run of
@@ -35,6 +37,14 @@
 // 4 * B_d + 2 * d, B_d = its first code over all segments: tables never
 // overlap), and the probe reads it there: correct for any input, fast for
 // the balanced ones.
+//
+// R's codes of cluster d are "runs": in segment mode one contiguous run per
+// build segment g (r_codes[g] + r_bounds[g][d] .. r_bounds[g][d + 1]); in tile
+// mode (rt_base set) the cluster's pass-1 tiles [rt_base[d], rt_base[d + 1])
+// of R's chunk pool, each a run of rt_cnt codes at rt_start, with
+// r_bounds[0] the cluster offsets of R's pass 1 (m and B_d). A cluster whose
+// runs exceed kHtSegs (only possible above the LDS limit when R's pass 1 has
+// <= 8 shards: <= 8 + lim / 4096 runs below it) takes the HBM table.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -73,7 +83,18 @@ struct ClusterArgs {
     const uint32_t* err;          // S's pass-1 error word (fold_pass1_error), or null
     unsigned long long* split;    // null, or {build, probe}: the workgroups' wall clocks spent building tables / probing
     unsigned long long* prof;     // PROF kernels: the builds' sections (wall clock, summed over workgroups), kClProfWords
+    // tile mode (R through the chunked code pass on one device): null = segment mode
+    const uint32_t* rt_base;      // [nb1 + 1]: R's pass-1 tiles of each cluster
+    const uint32_t* rt_start;     // tile -> first pool slot
+    const uint32_t* rt_cnt;       // tile -> codes
+    const int64_t* r_pool;        // R's chunk pool (codes)
+    const uint32_t* err_r;        // R's pass-1 error word (fold_pass1_error), or null
 };
+
+// A cluster's table is in HBM (k_cluster_big_fill / k_cluster_probe_big):
+// more codes than the LDS table holds, or (tile mode) more runs than a build
+// reads at once. The three kernels decide it the same way.
+__device__ __forceinline__ bool cl_big(uint32_t m, uint32_t runs, uint32_t lim) { return m > lim || runs > kHtSegs; }
 // PROF sections of a build: runs + codes of a cluster not prefetched; table
 // cleared + the next cluster's runs; inserts; the next cluster's codes requested;
 // then the number of builds and of builds not prefetched
@@ -83,8 +104,36 @@ constexpr int kClProfWords = 6;
 // sptr[g] = where element r of segment g's run sits, minus r; returns B_d (first code
 // over all segments). Wave 0 computes, every thread sees it after the caller's barrier.
 __device__ __forceinline__ void cl_runs(const ClusterArgs& a, uint32_t d, uint32_t* sseg, const int64_t** sptr,
-                                        uint32_t* sB) {
+                                        uint32_t* sB, uint32_t* sM, uint32_t* sN) {
     const uint32_t tid = threadIdx.x;
+    if (a.rt_base) {   // tile mode: the cluster's R tiles are its runs
+        if (tid < 64) {
+            const uint32_t t0 = a.rt_base[d], nt = a.rt_base[d + 1] - t0;
+            uint32_t lo = 0, len = 0;
+            if (tid < nt && nt <= static_cast<uint32_t>(kHtSegs)) {
+                lo = a.rt_start[t0 + tid];
+                len = a.rt_cnt[t0 + tid];
+            }
+            uint32_t x = len;
+#pragma unroll
+            for (int o = 1; o < kHtSegs; o <<= 1) {
+                const uint32_t y = __shfl_up(x, o, 64);
+                if (tid >= static_cast<uint32_t>(o)) x += y;
+            }
+            if (tid < nt && nt <= static_cast<uint32_t>(kHtSegs)) {
+                sseg[tid + 1] = x;
+                sptr[tid] = a.r_pool + lo - (x - len);
+            }
+            if (tid == 0) {
+                sseg[0] = 0;
+                const uint32_t b0 = a.r_bounds[0][d];
+                *sB = b0;
+                *sM = a.r_bounds[0][d + 1] - b0;
+                *sN = nt;
+            }
+        }
+        return;
+    }
     if (tid < 64) {
         uint32_t lo = 0, len = 0;
         if (tid < a.nseg) {
@@ -108,6 +157,8 @@ __device__ __forceinline__ void cl_runs(const ClusterArgs& a, uint32_t d, uint32
             sseg[0] = 0;
             *sB = b;
         }
+        if (tid == a.nseg - 1) *sM = x;
+        if (tid == 0) *sN = a.nseg;
     }
 }
 
@@ -120,6 +171,30 @@ __device__ __forceinline__ uint32_t cl_seg_of(const uint32_t* sseg, uint32_t nse
     return g;
 }
 
+// R's chunked code pass gathered into a multi-GPU member's exchange block:
+// codes contiguous per cluster (out_codes + bounds1[d] ..) and the cluster
+// bounds beside them, from the pass-1 tile list (one workgroup per cluster).
+// Replaces the stable pass (k_hist + scan + k_scatter_codes) on the member's
+// R chain: one pass over R, then this copy of its codes.
+__global__ __launch_bounds__(256) void k_cluster_gather(const uint32_t* rt_base, const uint32_t* rt_start,
+                                                         const uint32_t* rt_cnt, const int64_t* pool,
+                                                         const uint32_t* bounds1, uint32_t nb1, int64_t* out_codes,
+                                                         uint32_t* out_bounds) {
+    const uint32_t d = blockIdx.x, tid = threadIdx.x;
+    const uint32_t b0 = bounds1[d];
+    if (tid == 0) {
+        out_bounds[d] = b0;
+        if (d + 1 == nb1) out_bounds[nb1] = bounds1[nb1];
+    }
+    int64_t* dst = out_codes + b0;
+    for (uint32_t t = rt_base[d]; t < rt_base[d + 1]; t++) {
+        const int64_t* src = pool + rt_start[t];
+        const uint32_t c = rt_cnt[t];
+        for (uint32_t r = tid; r < c; r += 256) dst[r] = src[r];
+        dst += c;
+    }
+}
+
 // HBM tables of the clusters beyond the LDS limit: one workgroup per cluster,
 // the others return at once (none at the balanced configurations). Their S
 // tiles are probed by k_cluster_probe_big after k_cluster_probe (which skips
@@ -127,18 +202,26 @@ __device__ __forceinline__ uint32_t cl_seg_of(const uint32_t* sseg, uint32_t nse
 __global__ __launch_bounds__(256) void k_cluster_big_fill(ClusterArgs a) {
     __shared__ uint32_t sseg[kHtSegs + 1];
     __shared__ const int64_t* sptr[kHtSegs];
-    __shared__ uint32_t sB;
+    __shared__ uint32_t sB, sM, sN;
     const uint32_t d = blockIdx.x, tid = threadIdx.x;
-    cl_runs(a, d, sseg, sptr, &sB);
+    cl_runs(a, d, sseg, sptr, &sB, &sM, &sN);
     __syncthreads();
-    const uint32_t m = sseg[a.nseg];
-    if (m <= a.lim) return;   // workgroup-uniform
+    const uint32_t m = sM;
+    if (!cl_big(m, sN, a.lim)) return;   // workgroup-uniform
     const uint64_t e = d == 0 ? a.e1 : 0ull;
     const uint32_t cap = cl_big_cap(m);
     uint64_t* t = a.gtab + 4ull * sB + 2ull * d;
     for (uint32_t sl = tid; sl < cap; sl += 256) t[sl] = e;
     __threadfence();
     __syncthreads();
+    if (a.rt_base) {   // tile mode: tile by tile
+        for (uint32_t ti = a.rt_base[d]; ti < a.rt_base[d + 1]; ti++) {
+            const int64_t* src = a.r_pool + a.rt_start[ti];
+            const uint32_t c = a.rt_cnt[ti];
+            for (uint32_t r = tid; r < c; r += 256) ht_insert(t, cap / 2 - 1, e, static_cast<uint64_t>(src[r]));
+        }
+        return;
+    }
     for (uint32_t r = tid; r < m; r += 256) {
         const uint32_t g = cl_seg_of(sseg, a.nseg, r);
         ht_insert(t, cap / 2 - 1, e, static_cast<uint64_t>(sptr[g][r]));
@@ -150,13 +233,13 @@ __global__ __launch_bounds__(256) void k_cluster_big_fill(ClusterArgs a) {
 __global__ __launch_bounds__(256) void k_cluster_probe_big(ClusterArgs a) {
     __shared__ uint32_t sseg[kHtSegs + 1];
     __shared__ const int64_t* sptr[kHtSegs];
-    __shared__ uint32_t sB;
+    __shared__ uint32_t sB, sM, sN;
     __shared__ uint32_t red[4];
     const uint32_t d = blockIdx.x, tid = threadIdx.x;
-    cl_runs(a, d, sseg, sptr, &sB);
+    cl_runs(a, d, sseg, sptr, &sB, &sM, &sN);
     __syncthreads();
-    const uint32_t m = sseg[a.nseg];
-    if (m <= a.lim) return;   // workgroup-uniform
+    const uint32_t m = sM;
+    if (!cl_big(m, sN, a.lim)) return;   // workgroup-uniform
     const uint64_t e = d == 0 ? a.e1 : 0ull;
     const uint32_t bmask = cl_big_cap(m) / 2 - 1;
     const ulonglong2* g2 = reinterpret_cast<const ulonglong2*>(a.gtab + 4ull * sB + 2ull * d);
@@ -207,7 +290,7 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
     uint32_t* const fill = reinterpret_cast<uint32_t*>(tab + a.cap);
     __shared__ uint32_t sseg_[2][kHtSegs + 1];
     __shared__ const int64_t* sptr_[2][kHtSegs];
-    __shared__ uint32_t sB_[2];
+    __shared__ uint32_t sB_[2], sM_[2], sN_[2];   // first code, codes, runs of the cluster in each run buffer
     __shared__ uint32_t red[BLOCK / 64];
     constexpr uint32_t MR = 512;                 // tiles of metadata staged in LDS at a time
     __shared__ uint32_t smeta[3][MR];            // {cluster, first slot, codes} of tiles mbase .. mbase + MR - 1
@@ -289,7 +372,8 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
         auto fetch = [&](uint32_t buf, uint32_t m, uint64_t* rc) {
             const uint32_t* sseg = sseg_[buf];
             const int64_t* const* sptr = sptr_[buf];
-            if (a.nseg == 1) {   // one build segment: element r at sptr[0] + r
+            const uint32_t nrun = sN_[buf];   // <= kHtSegs (else the cluster is big)
+            if (nrun == 1) {   // one run: element r at sptr[0] + r
                 const int64_t* src = sptr[0];
 #pragma unroll
                 for (int j = 0; j < CPL; j++) {
@@ -299,14 +383,14 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
             } else {   // the segments' run ends in registers (broadcast reads), searched per element
                 uint32_t se[kHtSegs];
 #pragma unroll
-                for (int g = 0; g < kHtSegs; g++) se[g] = g < static_cast<int>(a.nseg) ? sseg[g + 1] : 0xffffffffu;
+                for (int g = 0; g < kHtSegs; g++) se[g] = g < static_cast<int>(nrun) ? sseg[g + 1] : 0xffffffffu;
 #pragma unroll
                 for (int j = 0; j < CPL; j++) {
                     const uint32_t r = j * BLOCK + tid;
                     uint32_t g = 0;
 #pragma unroll
                     for (int q = 0; q < kHtSegs; q++) g += r >= se[q] ? 1u : 0u;   // segments ending at or before r
-                    rc[j] = r < m ? static_cast<uint64_t>(sptr[min(g, a.nseg - 1)][r]) : 0ull;
+                    rc[j] = r < m ? static_cast<uint64_t>(sptr[min(g, nrun - 1)][r]) : 0ull;
                 }
             }
         };
@@ -321,17 +405,17 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
 #pragma unroll
                 for (int j = 0; j < CPL; j++) rc[j] = rn[PRE ? j : 0];
             } else {
-                cl_runs(a, d, sseg_[pb], sptr_[pb], &sB_[pb]);
+                cl_runs(a, d, sseg_[pb], sptr_[pb], &sB_[pb], &sM_[pb], &sN_[pb]);
                 __syncthreads();
-                const uint32_t m0 = sseg_[pb][a.nseg];
-                if (m0 <= a.lim) fetch(pb, m0, rc);
+                const uint32_t m0 = sM_[pb];
+                if (!cl_big(m0, sN_[pb], a.lim)) fetch(pb, m0, rc);
                 if (PROF) __builtin_amdgcn_s_waitcnt(0xF70);
             }
             unsigned long long c1 = 0, c2 = 0, c3 = 0;
             if (PROF) c1 = wall_clock64();
-            const uint32_t m = sseg_[pb][a.nseg];
+            const uint32_t m = sM_[pb];
             e = d == 0 ? a.e1 : 0ull;
-            big = m > a.lim;
+            big = cl_big(m, sN_[pb], a.lim);
             if (!big) {
                 bmask = a.cap / 2 - 1;
                 ulonglong2* t2 = reinterpret_cast<ulonglong2*>(tab);
@@ -343,7 +427,7 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
             }
             // the next cluster's runs into the other buffer (read after the barrier)
             const bool nxt = PRE && d < d_last;
-            if (nxt) cl_runs(a, d + 1, sseg_[pb ^ 1u], sptr_[pb ^ 1u], &sB_[pb ^ 1u]);
+            if (nxt) cl_runs(a, d + 1, sseg_[pb ^ 1u], sptr_[pb ^ 1u], &sB_[pb ^ 1u], &sM_[pb ^ 1u], &sN_[pb ^ 1u]);
             __syncthreads();   // cleared; the next runs staged
             if (PROF) c2 = wall_clock64();
             if (CNT && !big) {
@@ -390,8 +474,8 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
             pre = 0xffffffffu;
             if constexpr (PRE) {   // the next cluster's codes: in flight during this cluster's tiles
                 if (nxt) {
-                    const uint32_t mn = sseg_[pb ^ 1u][a.nseg];
-                    if (mn <= a.lim) {
+                    const uint32_t mn = sM_[pb ^ 1u];
+                    if (!cl_big(mn, sN_[pb ^ 1u], a.lim)) {
                         fetch(pb ^ 1u, mn, rn);
                         pre = d + 1;
                     }
@@ -471,6 +555,7 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
             for (int w = 0; w < kClProfWords; w++) atomicAdd(&a.prof[w], prof[PROF ? w : 0]);
     }
     fold_pass1_error(a.err, a.count);
+    fold_pass1_error(a.err_r, a.count);
 }
 
 }  // namespace phj

@@ -69,9 +69,9 @@ for step in "$@"; do
       done ;;
     traces)
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$GRAFT_REPO_ROOT/${O}_w8trace" -o run -- python3 "$GRAFT_REPO_ROOT/scripts/rehearse_world.py" --worlds 8 --steps 5 > "$GRAFT_REPO_ROOT/${O}_w8trace.log" 2>&1) || { echo "rocprof w8 failed"; tail -5 ${O}_w8trace.log; exit 8; }
-      python3 scripts/trace_summary.py ${O}_w8trace --step-kernel k_cluster_probe > ${O}_w8trace.txt 2>&1
+      python3 scripts/trace_summary.py ${O}_w8trace --step-kernel "k_cluster_probe<" > ${O}_w8trace.txt 2>&1
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$GRAFT_REPO_ROOT/${O}_c2trace" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-traffic > "$GRAFT_REPO_ROOT/${O}_c2trace.log" 2>&1) || { echo "rocprof c2 failed"; tail -5 ${O}_c2trace.log; exit 8; }
-      python3 scripts/trace_summary.py ${O}_c2trace --step-kernel k_cluster_probe > ${O}_c2trace.txt 2>&1
+      python3 scripts/trace_summary.py ${O}_c2trace --step-kernel "k_cluster_probe<" > ${O}_c2trace.txt 2>&1
       tail -30 ${O}_c2trace.txt ;;
     sweep)
       timeout -k 10 900 python scripts/sweep.py --skew 1.05 1.25 --out ${O}_sweep_cli > ${O}_sweep.log 2>&1 || { echo "sweep failed"; tail -5 ${O}_sweep.log; exit 9; }

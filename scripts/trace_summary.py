@@ -3,8 +3,8 @@
 for the last bench step, the device timeline (start offsets and gaps).
 
   python scripts/trace_summary.py <dir with *_kernel_trace.csv> [--step-kernel NAME]
-(the step ends at the last launch whose name contains NAME, default k_probe;
-k_cluster_probe is the LDS join's probe)
+(the step ends at the last launch whose name contains NAME, default k_probe,
+and the launches right behind it; "k_cluster_probe<" is the LDS join's probe)
 """
 import csv
 import glob
@@ -41,6 +41,9 @@ def main():
         t0 = rows[first][0]
         print("\nlast step timeline (us): start  dur  gap-before  kernel")
         prev_end = None
+        # (kernels after the last match in the same step, e.g. k_cluster_probe_big, belong to it)
+        while last + 1 < len(rows) and rows[last + 1][0] < rows[last][1] + 200_000 and key not in rows[last + 1][2]:
+            last += 1
         for s, e, n in rows[first:last + 1]:
             gap = (s - prev_end) / 1e3 if prev_end is not None else 0.0
             print(f"{(s - t0) / 1e3:9.1f} {(e - s) / 1e3:8.1f} {gap:8.1f}  {n.split('(')[0][:70]}")

@@ -470,6 +470,31 @@ def test_cluster_tables_lds_and_hbm(monkeypatch, env, name, params):
         c.close()
 
 
+@pytest.mark.parametrize("env", [{}, {"PHJ_R_CHUNK": "0"}], ids=["tiles", "stable"])
+def test_cluster_tile_mode_runs(monkeypatch, env):
+    """R through the chunked code pass (tile mode, the one-device default):
+    a cluster's R codes are read through its pass-1 tiles. Here one key
+    repeated 150K times makes its cluster span more tiles than a build reads
+    at once (8 shards x ~5 chunks: the HBM table, read tile by tile), a second
+    cluster sits just under the LDS limit in several runs, and R is small
+    enough elsewhere for one-tile clusters. Counted against the oracle."""
+    c = _cluster_ctx(monkeypatch, **env)
+    try:
+        params = phj.radix_params((8, 8), hash=phj.HASH_MURMUR3, seed=SEED)
+        rng = np.random.default_rng(77)
+        R = np.concatenate([np.full(150_000, 4242, dtype=np.int64), np.full(11_000, -99, dtype=np.int64),
+                            rng.integers(-3_000_000, 3_000_000, 900_000, dtype=np.int64)])
+        S = np.concatenate([np.full(40_000, 4242, dtype=np.int64), np.full(7_000, -99, dtype=np.int64),
+                            rng.integers(-6_000_000, 6_000_000, 1_500_000, dtype=np.int64)])
+        rng.shuffle(R)
+        rng.shuffle(S)
+        expect = O.semijoin_count_keys(R, S)
+        assert _gpu_count(c, R, S, params) == expect
+        assert c.join(params).matches == expect
+    finally:
+        c.close()
+
+
 def test_cluster_path_is_default_for_c2_shape(ctx):
     """10M-scale build side at 8+8 radix bits: the join's pass 1 is the LDS
     join's 1024 clusters (the probe-side pass-1 hook reports its digits)."""

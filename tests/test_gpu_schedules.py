@@ -68,6 +68,8 @@ SCHEDULES = [
     {"PHJ_P1_BLOCK": "512", "PHJ_CL_BITS": "11"},               # ... four digits per thread
     {"PHJ_P1_KPF": "1"},                                        # ... one tile of keys in flight
     {"PHJ_P1_KPF": "1", "PHJ_CL_BITS": "11"},                   # ... with two digits per thread
+    {"PHJ_R_CHUNK": "0"},                                       # LDS join: R by the stable pass (codes contiguous per cluster)
+    {"PHJ_R_CHUNK": "0", "PHJ_CL_BITS": "11"},                  # ... 2048 clusters
     {"PHJ_R_ORDER": "0"},                                       # LDS join: R's pass 1 beside S's
     {"PHJ_R_ORDER": "2"},                                       # ... before it
     {"PHJ_P1_PROF": "1", "PHJ_CL_PROF": "1"},                   # the phase clocks of pass 1 and of the LDS join's builds
