@@ -1332,27 +1332,6 @@ bool use_cluster(const phj_ctx* c, const Plan& pl, uint64_t nS, uint64_t nR, Pla
     return cluster_empty0(out) != 0 && 4 * nR + 2ull * out.nb1 < (1ull << 32);
 }
 
-// A multi-GPU member's R shard as codes contiguous per cluster, straight into
-// its exchange block {codes | bounds}: the chunked code pass (8 shards) and
-// k_cluster_gather (PHJ_R_CHUNK, default: one pass over R and a copy of its
-// codes, where the stable pass is a histogram, two scan launches and a
-// scatter), else partition_build. Its error word is folded by the probe.
-int cluster_r_codes(phj_ctx* c, const Plan& pl, int64_t* out, uint32_t* bounds) {
-    SideState& R = c->side[PHJ_SIDE_BUILD];
-    if (c->tune.r_chunk && R.n > 0) {
-        PHJ_TRY(partition_state(c, R, "R", pl, true, nullptr, 8));
-        if (R.hcoded) {
-            if (c->dry) return PHJ_OK;
-            PHJ_TRY(timer_begin(c, "R.gather", R.n * 16));
-            hipLaunchKernelGGL(k_cluster_gather, dim3(pl.nb1), dim3(256), 0, c->ks, R.p2.tile_base, R.p2.tile_start,
-                               R.p2.tile_cnt, R.p2.in_keys, static_cast<const uint32_t*>(R.bounds1.p), pl.nb1, out, bounds);
-            PHJ_LAUNCHED(c, "k_cluster_gather");
-            return timer_end(c);
-        }
-    }
-    return partition_build(c, pl, out, bounds);
-}
-
 // Probe a probe-side pass-1 output (partition_state p1_only) against the
 // tables of build_ht; the count lands in (clear) or is added to c->count.
 int probe_ht(phj_ctx* c, const Plan& pl, SideState& PS, bool clear = true) {

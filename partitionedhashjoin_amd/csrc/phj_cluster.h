@@ -171,30 +171,6 @@ __device__ __forceinline__ uint32_t cl_seg_of(const uint32_t* sseg, uint32_t nse
     return g;
 }
 
-// R's chunked code pass gathered into a multi-GPU member's exchange block:
-// codes contiguous per cluster (out_codes + bounds1[d] ..) and the cluster
-// bounds beside them, from the pass-1 tile list (one workgroup per cluster).
-// Replaces the stable pass (k_hist + scan + k_scatter_codes) on the member's
-// R chain: one pass over R, then this copy of its codes.
-__global__ __launch_bounds__(256) void k_cluster_gather(const uint32_t* rt_base, const uint32_t* rt_start,
-                                                         const uint32_t* rt_cnt, const int64_t* pool,
-                                                         const uint32_t* bounds1, uint32_t nb1, int64_t* out_codes,
-                                                         uint32_t* out_bounds) {
-    const uint32_t d = blockIdx.x, tid = threadIdx.x;
-    const uint32_t b0 = bounds1[d];
-    if (tid == 0) {
-        out_bounds[d] = b0;
-        if (d + 1 == nb1) out_bounds[nb1] = bounds1[nb1];
-    }
-    int64_t* dst = out_codes + b0;
-    for (uint32_t t = rt_base[d]; t < rt_base[d + 1]; t++) {
-        const int64_t* src = pool + rt_start[t];
-        const uint32_t c = rt_cnt[t];
-        for (uint32_t r = tid; r < c; r += 256) dst[r] = src[r];
-        dst += c;
-    }
-}
-
 // HBM tables of the clusters beyond the LDS limit: one workgroup per cluster,
 // the others return at once (none at the balanced configurations). Their S
 // tiles are probed by k_cluster_probe_big after k_cluster_probe (which skips

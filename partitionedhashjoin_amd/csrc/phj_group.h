@@ -469,7 +469,7 @@ int member_prepare_radix(Group& G, int i, const Plan& pl) {
     PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, pl, p2));
     const PackLayout L = member_layout(G, pl, p2);
     if (pl.cluster) {
-        PHJ_TRY(cluster_r_codes(c, pl, nullptr, nullptr));
+        PHJ_TRY(partition_build(c, pl, nullptr, nullptr));
         PHJ_TRY(cluster_big_fill(c, pl, G.world, nullptr, nullptr, total(G.n[PHJ_SIDE_BUILD])));
     } else if (p2) {
         PHJ_TRY(partition_build(c, pl, nullptr, nullptr));
@@ -544,7 +544,7 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
     if (rc == PHJ_OK && hipStreamWaitEvent(c->aux, t0, 0) != hipSuccess) rc = set_err(c, PHJ_ERR_HIP, "wait t0");
     if (p2) {   // the R shard as codes in partition order, straight into the exchange block
         if (rc == PHJ_OK)
-            rc = (pl.cluster ? cluster_r_codes : partition_build)(c, pl, static_cast<int64_t*>(B.send.p),
+            rc = partition_build(c, pl, static_cast<int64_t*>(B.send.p),
                                  reinterpret_cast<uint32_t*>(static_cast<int64_t*>(B.send.p) + L.maxn));
     } else {
         if (rc == PHJ_OK) rc = partition_side(c, PHJ_SIDE_BUILD, pl);
