@@ -1482,7 +1482,13 @@ int probe_cluster(phj_ctx* c, const Plan& pl, SideState& PS, int nseg, const int
     // the default form, for comparison)
     const bool pre = c->tune.cl_pre, pr = c->tune.cl_prof != 0;
     const int pf = c->tune.cl_pf;
-    const void* kfn = !c->tune.cl_cnt ? (pr ? reinterpret_cast<const void*>(&k_cluster_probe<B, I, 3, true, true, false>)
+    // (tile mode, R read by its pass-1 tiles: the default form and the
+    // compare-and-swap and clock forms; segment mode: every form)
+    const void* kfn = RT ? (!c->tune.cl_cnt ? reinterpret_cast<const void*>(&k_cluster_probe<B, I, 3, true, false, false, true>)
+                            : pr           ? reinterpret_cast<const void*>(&k_cluster_probe<B, I, 3, true, true, true, true>)
+                            : pf == 3      ? reinterpret_cast<const void*>(&k_cluster_probe<B, I, 3, true, false, true, true>)
+                                           : reinterpret_cast<const void*>(&k_cluster_probe<B, I, 2, true, false, true, true>))
+                      : !c->tune.cl_cnt ? (pr ? reinterpret_cast<const void*>(&k_cluster_probe<B, I, 3, true, true, false>)
                                             : reinterpret_cast<const void*>(&k_cluster_probe<B, I, 3, true, false, false>))
                       : pr            ? reinterpret_cast<const void*>(&k_cluster_probe<B, I, 3, true, true, true>)
                       : !pre          ? reinterpret_cast<const void*>(&k_cluster_probe<B, I, 2, false, false, true>)

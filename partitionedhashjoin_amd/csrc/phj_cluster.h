@@ -103,10 +103,13 @@ constexpr int kClProfWords = 6;
 // Cluster d's runs over the segments: sseg[g] = codes before segment g (sseg[nseg] = m),
 // sptr[g] = where element r of segment g's run sits, minus r; returns B_d (first code
 // over all segments). Wave 0 computes, every thread sees it after the caller's barrier.
+// TM: 1 = tile mode, 0 = segment mode, -1 = decided by a.rt_base (the big
+// kernels); the probe is instantiated per mode (one path's registers each).
+template <int TM = -1>
 __device__ __forceinline__ void cl_runs(const ClusterArgs& a, uint32_t d, uint32_t* sseg, const int64_t** sptr,
                                         uint32_t* sB, uint32_t* sM, uint32_t* sN) {
     const uint32_t tid = threadIdx.x;
-    if (a.rt_base) {   // tile mode: the cluster's R tiles are its runs
+    if (TM == 1 || (TM == -1 && a.rt_base)) {   // tile mode: the cluster's R tiles are its runs
         if (tid < 64) {
             const uint32_t t0 = a.rt_base[d], nt = a.rt_base[d + 1] - t0;
             uint32_t lo = 0, len = 0;
@@ -259,7 +262,7 @@ __global__ __launch_bounds__(256) void k_cluster_probe_big(ClusterArgs a) {
 // takes a second slot (the count is a set test: a probe stops at the first
 // match either way); a bucket's attempts are at most the cluster's codes
 // (<= lim < 2^16), so a counter never carries into its neighbour.
-template <int BLOCK, int ITEMS, int PF = 1, bool PRE = true, bool PROF = false, bool CNT = false>
+template <int BLOCK, int ITEMS, int PF = 1, bool PRE = true, bool PROF = false, bool CNT = false, bool TM = false>
 __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
     constexpr int CPL = kClCapMax * 3 / 4 / BLOCK;   // R codes per lane at the limit
     extern __shared__ __attribute__((aligned(16))) uint64_t tab[];   // [cap] (+ CNT: cap / 4 words of fill counters)
@@ -348,7 +351,7 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
         auto fetch = [&](uint32_t buf, uint32_t m, uint64_t* rc) {
             const uint32_t* sseg = sseg_[buf];
             const int64_t* const* sptr = sptr_[buf];
-            const uint32_t nrun = sN_[buf];   // <= kHtSegs (else the cluster is big)
+            const uint32_t nrun = TM ? sN_[buf] : a.nseg;   // <= kHtSegs (else the cluster is big)
             if (nrun == 1) {   // one run: element r at sptr[0] + r
                 const int64_t* src = sptr[0];
 #pragma unroll
@@ -359,7 +362,8 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
             } else {   // the segments' run ends in registers (broadcast reads), searched per element
                 uint32_t se[kHtSegs];
 #pragma unroll
-                for (int g = 0; g < kHtSegs; g++) se[g] = g < static_cast<int>(nrun) ? sseg[g + 1] : 0xffffffffu;
+                for (int g = 0; g < kHtSegs; g++)   // workgroup-uniform: scalar registers
+                    se[g] = __builtin_amdgcn_readfirstlane(g < static_cast<int>(nrun) ? sseg[g + 1] : 0xffffffffu);
 #pragma unroll
                 for (int j = 0; j < CPL; j++) {
                     const uint32_t r = j * BLOCK + tid;
@@ -381,7 +385,7 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
 #pragma unroll
                 for (int j = 0; j < CPL; j++) rc[j] = rn[PRE ? j : 0];
             } else {
-                cl_runs(a, d, sseg_[pb], sptr_[pb], &sB_[pb], &sM_[pb], &sN_[pb]);
+                cl_runs<TM ? 1 : 0>(a, d, sseg_[pb], sptr_[pb], &sB_[pb], &sM_[pb], &sN_[pb]);
                 __syncthreads();
                 const uint32_t m0 = sM_[pb];
                 if (!cl_big(m0, sN_[pb], a.lim)) fetch(pb, m0, rc);
@@ -403,7 +407,7 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
             }
             // the next cluster's runs into the other buffer (read after the barrier)
             const bool nxt = PRE && d < d_last;
-            if (nxt) cl_runs(a, d + 1, sseg_[pb ^ 1u], sptr_[pb ^ 1u], &sB_[pb ^ 1u], &sM_[pb ^ 1u], &sN_[pb ^ 1u]);
+            if (nxt) cl_runs<TM ? 1 : 0>(a, d + 1, sseg_[pb ^ 1u], sptr_[pb ^ 1u], &sB_[pb ^ 1u], &sM_[pb ^ 1u], &sN_[pb ^ 1u]);
             __syncthreads();   // cleared; the next runs staged
             if (PROF) c2 = wall_clock64();
             if (CNT && !big) {
