@@ -594,7 +594,10 @@ int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const st
                     const int dpt = a.nbins > 2 * BLOCK ? 4 : a.nbins > BLOCK ? 2 : 1;
                     if (c->tune.p1_block == 1024) {   // 16 waves per CU, 4 codes per thread
                         kblock = 1024;
-                        const int kpf = c->tune.p1_kpf;
+                        // R's pass (LDS join, tile mode: ~10 tiles per workgroup at C2)
+                        // keeps one tile in flight, which also gives it a kernel name of
+                        // its own in rocprof summaries (S's is the roofline kernel)
+                        const int kpf = prefix.rfind("R.", 0) == 0 ? 1 : c->tune.p1_kpf;
                         const bool pr = c->tune.p1_prof != 0;
                         kfn = hk == kMurmur3 ? (dpt == 4 ? pipe1024<kMurmur3, 2>(kpf, pr) : pipe1024<kMurmur3, 1>(kpf, pr))
                                              : (dpt == 4 ? pipe1024<kXXH3, 2>(kpf, pr) : pipe1024<kXXH3, 1>(kpf, pr));
