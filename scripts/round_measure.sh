@@ -56,16 +56,18 @@ for step in "$@"; do
       cut -c1-160 ${O}_rehearse.jsonl ;;
     pmc)
       # per kernel (pmc_kernel.py keeps the last matching dispatch): S's pass 1, the probe
-      for kr in "c2:k_chunk_codes" "c2:k_cluster_probe" "c5:k_cluster_probe" "c4:k_np_probe_ct"; do
-        cfg=${kr%%:*}; k=${kr#*:}
+      # (S's pass 1 is the KPF=2 form; R's the KPF=1 form of the same kernel; the LDS join's
+      # main kernel, not its big-cluster companion)
+      for kr in "c2:k_chunk_codes_pipe<.*, 2>\(" "c2:k_cluster_probe<" "c5:k_cluster_probe<" "c4:k_np_probe_ct"; do
+        cfg=${kr%%:*}; k=${kr#*:}; kf=$(echo "$k" | tr -c 'a-z0-9_' '_')
         timeout -k 10 400 python scripts/pmc_kernel.py --config $cfg --kernel "$k" \
           --group FETCH_SIZE --group WRITE_SIZE \
           --group TCC_HIT_sum,TCC_MISS_sum,TCC_EA0_RDREQ_sum \
           --group TCC_EA0_RDREQ_32B_sum,TCC_REQ_sum \
           --group SQ_WAVES,SQ_WAVE_CYCLES,SQ_WAIT_ANY,SQ_BUSY_CYCLES,SQ_INSTS_VALU,SQ_INSTS_LDS,SQ_WAIT_INST_ANY,SQ_INSTS_SALU \
           --group SQ_ACTIVE_INST_VALU,SQ_ACTIVE_INST_LDS,SQ_ACTIVE_INST_VMEM,SQ_LDS_BANK_CONFLICT,SQ_INSTS_VMEM_RD,SQ_INSTS_VMEM_WR,SQ_WAIT_INST_LDS,SQ_ACTIVE_INST_ANY \
-          > ${O}_pmc_${cfg}_$k.jsonl 2> ${O}_pmc_${cfg}_$k.err || { echo "pmc $cfg $k failed"; tail -20 ${O}_pmc_${cfg}_$k.err; exit 7; }
-        cut -c1-1500 ${O}_pmc_${cfg}_$k.jsonl
+          > ${O}_pmc_${cfg}_$kf.jsonl 2> ${O}_pmc_${cfg}_$kf.err || { echo "pmc $cfg $k failed"; tail -20 ${O}_pmc_${cfg}_$kf.err; exit 7; }
+        cut -c1-1500 ${O}_pmc_${cfg}_$kf.jsonl
       done ;;
     traces)
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$GRAFT_REPO_ROOT/${O}_w8trace" -o run -- python3 "$GRAFT_REPO_ROOT/scripts/rehearse_world.py" --worlds 8 --steps 5 > "$GRAFT_REPO_ROOT/${O}_w8trace.log" 2>&1) || { echo "rocprof w8 failed"; tail -5 ${O}_w8trace.log; exit 8; }
