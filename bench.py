@@ -48,6 +48,9 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: the core share - 1 (cpu_threads)")
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes")
+    ap.add_argument("--timers-per-step", dest="timers_deferred", action="store_false",
+                    help="read each step's timers inside it (default: one device defers the readout past the timed "
+                         "loop, PHJ_DEFER_TIMERS)")
     ap.add_argument("--exchange", action="store_true",
                     help="at one GPU, run the N>1 step (RCCL all-gather + all-reduce) on a world of one")
     return ap.parse_args()
@@ -287,7 +290,16 @@ def main():
             a[0] += ms
             a[1] += nbytes
 
-    results = [step() for _ in range(args.steps)]
+    # one device: PHJ_DEFER_TIMERS keeps the timer readout (event queries, the
+    # LDS join's clock split) out of the timed steps; the events are recorded
+    # inside them and summed by timers_report after the loop
+    defer = world == 1 and not args.exchange and args.timers_deferred
+    timed_params = params
+    if defer:
+        timed_params = type(params).from_buffer_copy(params)
+        timed_params.flags = params.flags | phj.DEFER_TIMERS
+        ctx.timers_report()   # a clean slate
+    results = [ctx.join(timed_params) for _ in range(args.steps)]
     barrier()
     elapsed = time.perf_counter() - t0
     # each step's timers are its own HIP events, recorded in the timed region;
@@ -295,7 +307,10 @@ def main():
     for res in results:
         matches = res.matches
         exch += res.exchange_ms
-        accumulate(res.timers())
+        if not defer:
+            accumulate(res.timers())
+    if defer:
+        accumulate(ctx.timers_report().timers())
 
     def allsum(x):
         if world == 1:

@@ -96,6 +96,14 @@ typedef struct phj_join_params {
  * semantics (phj_table.h). Counts are identical either way; the host driver's
  * SeparateChainingFactory sets it. Ignored by NoPartitioning. */
 #define PHJ_TABLE_CHAINED 0x2
+/* flags: PHJ_DEFER_TIMERS (one device) leaves this join's timers in the
+ * context instead of reading them into the result: no event queries and no
+ * extra synchronisation after the count is read back. Timers accumulate over
+ * such joins; phj_timers_report returns their sums (the LDS join's build /
+ * probe split then uses the last join's clocks) and resets them. Result
+ * fields partition_ms .. total_ms and the timer list stay zero. A benchmark
+ * loop sets it to keep the readout off its timed steps (bench.py). */
+#define PHJ_DEFER_TIMERS 0x4
 #define PHJ_MAX_TIMERS 32
 #define PHJ_TIMER_NAME 24
 

@@ -171,6 +171,7 @@ struct phj_ctx {
     uint32_t since_ev = 0;             // ... and the kernels launched since
     unsigned long long* count_host = nullptr;   // pinned: the count read back
     unsigned long long* split_words = nullptr;  // the LDS probe's {build, probe} clocks (count buffer words 2-3), this join
+    bool defer_timers = false;  // the running join has PHJ_DEFER_TIMERS: its timers stay for phj_timers_report
 };
 
 namespace {
@@ -316,6 +317,7 @@ double fused_build_fraction(phj_ctx* c) {
 // one join, or many when a caller reports once after several joins).
 int fill_timers(phj_ctx* c, phj_join_result* r) {
     r->num_timers = 0;
+    if (c->defer_timers) return PHJ_OK;   // PHJ_DEFER_TIMERS: read later by phj_timers_report
     double fb = -1.0;
     for (const TimerRec& t : c->timers) {
         float ms = 0;
@@ -340,9 +342,9 @@ int fill_timers(phj_ctx* c, phj_join_result* r) {
 }
 
 double elapsed(phj_ctx* c, hipEvent_t a, hipEvent_t b) {
+    if (c->defer_timers) return 0.0;   // PHJ_DEFER_TIMERS: no event queries in the join
     float ms = 0;
     if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return -1.0;
-    (void)c;
     return ms;
 }
 
@@ -2211,6 +2213,7 @@ int phj_partition(phj_ctx* c, int side, const phj_join_params* p, phj_partitione
     PHJ_HIP(c, hipSetDevice(c->device));
     // timers accumulate until phj_join / phj_join_partitioned / phj_timers_report
     // reports them; a caller that never reports loses the oldest records
+    c->defer_timers = false;
     if (c->timers.size() > kMaxTimerRecs) reset_timers(c);
     PHJ_TRY(partition_side(c, side, pl));
     if (out) *out = c->side[side].view;
@@ -2246,6 +2249,7 @@ int phj_join_partitioned(phj_ctx* c, const phj_join_params* p, int nbuild, const
     uint64_t nR = 0;
     for (int g = 0; g < nbuild; g++) nR += build[g].n;
     r->algorithmic_bytes = nR * 32 + c->side[PHJ_SIDE_PROBE].view.n * 8 + nR * 8;
+    c->defer_timers = false;
     const int rc = fill_timers(c, r);  // includes the phj_partition launches since the last report
     reset_timers(c);
     return rc;
@@ -2280,7 +2284,8 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
     }
     PHJ_HIP(c, hipSetDevice(c->device));
     std::memset(r, 0, sizeof(*r));
-    reset_timers(c);
+    c->defer_timers = (p->flags & PHJ_DEFER_TIMERS) != 0;
+    if (!c->defer_timers || c->timers.size() > kMaxTimerRecs) reset_timers(c);
     if (p->algo == PHJ_ALGO_NO_PARTITIONING) return join_nopart(c, p, r);
     if (p->algo != PHJ_ALGO_RADIX) return set_err(c, PHJ_ERR_INVALID, "Unrecognized join algorithm");
     Plan pl;
@@ -2305,9 +2310,16 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
         // has at most 8 + 3 runs), its tiles read by the builds; else the
         // stable pass (k_hist + scan + k_scatter_codes: codes contiguous per cluster)
         SideState* RT = nullptr;
+        // after S's pass (PHJ_R_ORDER=1, default) R's chain runs on the main
+        // stream itself: nothing runs beside it, and a cross-stream event wait
+        // before the probe costs ~15 us (measured gap, r05z timeline)
+        const int order = c->tune.r_order;
+        const bool r_main = order == 1;
         auto r_chain = [&](hipEvent_t after) -> int {
-            PHJ_HIP(c, hipStreamWaitEvent(c->aux, after, 0));
-            c->ks = c->aux;
+            if (!r_main) {
+                PHJ_HIP(c, hipStreamWaitEvent(c->aux, after, 0));
+                c->ks = c->aux;
+            }
             int rc = PHJ_OK;
             if (c->tune.r_chunk && R.n > 0) {
                 rc = partition_state(c, R, "R", cpl, true, nullptr, 8);
@@ -2332,7 +2344,6 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
         };
         // PHJ_R_ORDER: 0 = R's chain beside S's pass 1 (it waits for t0: the
         // previous step's probe read R's codes), 1 = after S's pass 1, 2 = before it
-        const int order = c->tune.r_order;
         if (order == 2) {
             PHJ_TRY(r_chain(t0));
             PHJ_HIP(c, hipStreamWaitEvent(c->stream, tr, 0));
@@ -2341,12 +2352,8 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
         // S takes no chunked pass: a memset)
         PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, cpl, true, static_cast<unsigned long long*>(c->count.p)));
         if (!S.hcoded) PHJ_HIP(c, hipMemsetAsync(c->count.p, 0, 32, c->stream));
-        if (order != 2) {
-            hipEvent_t after = t0;
-            if (order == 1) PHJ_TRY(mark(c, &after));
-            PHJ_TRY(r_chain(after));
-        }
-        PHJ_HIP(c, hipStreamWaitEvent(c->stream, tr, 0));
+        if (order != 2) PHJ_TRY(r_chain(t0));
+        if (!r_main) PHJ_HIP(c, hipStreamWaitEvent(c->stream, tr, 0));
         PHJ_TRY(mark(c, &t1));
         // one launch, reported as "build" (the workgroups' table builds in LDS:
         // R's codes read) and "probe" (S's codes read), split by the kernel's own clocks
@@ -2359,7 +2366,7 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
         r->matches = m;
         r->partition_ms = elapsed(c, t0, t1);
         {   // the probe launch split by its clocks (build = the LDS table builds + the big clusters' HBM tables)
-            const double t = elapsed(c, t1, p1), fb = c->tune.timers ? fused_build_fraction(c) : 0.0;
+            const double t = elapsed(c, t1, p1), fb = c->tune.timers && !c->defer_timers ? fused_build_fraction(c) : 0.0;
             r->build_ms = elapsed(c, b0, tr) + t * fb;
             r->probe_ms = t * (1.0 - fb);
         }
@@ -2506,6 +2513,7 @@ int phj_timers_report(phj_ctx* c, phj_join_result* r) {
     PHJ_HIP(c, hipSetDevice(c->device));
     PHJ_HIP(c, hipStreamSynchronize(c->ks));
     std::memset(r, 0, sizeof(*r));
+    c->defer_timers = false;
     const int rc = fill_timers(c, r);
     reset_timers(c);
     return rc;
@@ -2549,6 +2557,7 @@ int phj_join_materialize(phj_ctx* c, const phj_join_params* p, phj_join_result* 
     if (!p) return set_err(c, PHJ_ERR_INVALID, "null params");
     PHJ_HIP(c, hipSetDevice(c->device));
     std::memset(r, 0, sizeof(*r));
+    c->defer_timers = false;
     reset_timers(c);
     c->mat_n = 0;
     if (p->algo == PHJ_ALGO_NO_PARTITIONING) {
@@ -2612,6 +2621,7 @@ int phj_probe_pass1(phj_ctx* c, const phj_join_params* p, int64_t* keys, uint64_
         if (!use_p2probe(c, pl, S.n, c->side[PHJ_SIDE_BUILD].n))
             return set_err(c, PHJ_ERR_STATE, "these params do not take the on-chip probe");
     }
+    c->defer_timers = false;
     reset_timers(c);
     c->ks = c->stream;
     PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, pl, true));

@@ -324,14 +324,18 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
             const uint32_t c = t < t_hi ? smeta[2][j] : 0u;
             m = 0;
             // 16-B loads, two codes per lane each: a tile is one pass-1 chunk of
-            // BLOCK * ITEMS allocated slots, read whole (the slots past its codes
-            // are masked off); element (i, h) = code 2 * (i / 2 * BLOCK + tid) + h
+            // BLOCK * ITEMS allocated slots; element (i, h) = code 2 * (i / 2 *
+            // BLOCK + tid) + h. Every lane loads (the same loads on every path),
+            // lanes past the tile's codes at its last pair, which they share
+            // with a valid lane (masked off: a chain's last, partial chunk is
+            // not read whole; ~15 % of the bytes at C2)
             typedef long long v2i __attribute__((ext_vector_type(2)));
             const v2i* src = reinterpret_cast<const v2i*>(a.s_codes + lo);
+            const uint32_t last = c ? (c - 1) / 2 : 0u;
 #pragma unroll
             for (int i = 0; i < ITEMS; i += 2) {
                 const uint32_t e = 2 * ((i / 2) * BLOCK + tid);
-                const v2i v = __builtin_nontemporal_load(src + (i / 2) * BLOCK + tid);
+                const v2i v = __builtin_nontemporal_load(src + min((i / 2) * BLOCK + tid, last));
                 k[i] = v.x;
                 k[i + 1] = v.y;
                 m |= (e < c ? (1u << i) : 0u) | (e + 1 < c ? (2u << i) : 0u);

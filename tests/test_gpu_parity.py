@@ -495,6 +495,30 @@ def test_cluster_tile_mode_runs(monkeypatch, env):
         c.close()
 
 
+def test_deferred_timers(ctx):
+    """PHJ_DEFER_TIMERS: the join's result carries its count but no timers;
+    the context keeps them, and timers_report returns their sums over the
+    deferred joins (then a normal join reports its own again)."""
+    ctx.generate_sequential(phj.SIDE_BUILD, 1_000_000, 1)
+    ctx.generate_zipf(phj.SIDE_PROBE, 3_000_000, 1.05, 1, 1_000_000, 9)
+    p = phj.radix_params((8, 8), hash=phj.HASH_MURMUR3, seed=SEED)
+    one = ctx.join(p)
+    single = {name: ms for name, ms, _ in one.timers()}
+    assert one.matches == 3_000_000 and single
+    q = type(p).from_buffer_copy(p)
+    q.flags = p.flags | phj.DEFER_TIMERS
+    ctx.timers_report()
+    for _ in range(3):
+        r = ctx.join(q)
+        assert r.matches == 3_000_000
+        assert list(r.timers()) == [] and r.total_ms == 0
+    summed = {name: ms for name, ms, _ in ctx.timers_report().timers()}
+    assert set(summed) == set(single)
+    for name in ("S.p1.scatter", "probe"):
+        assert summed[name] > 1.5 * single[name]   # three joins' worth
+    assert ctx.join(p).timers()
+
+
 def test_cluster_path_is_default_for_c2_shape(ctx):
     """10M-scale build side at 8+8 radix bits: the join's pass 1 is the LDS
     join's 1024 clusters (the probe-side pass-1 hook reports its digits)."""
