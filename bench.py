@@ -293,7 +293,8 @@ def main():
     # one device: PHJ_DEFER_TIMERS keeps the timer readout (event queries, the
     # LDS join's clock split) out of the timed steps; the events are recorded
     # inside them and summed by timers_report after the loop
-    defer = world == 1 and not args.exchange and args.timers_deferred
+    # (at N>1 each rank's context has one member: the same, per rank)
+    defer = args.timers_deferred and params.algo == phj.ALGO_RADIX
     timed_params = params
     if defer:
         timed_params = type(params).from_buffer_copy(params)
@@ -310,7 +311,9 @@ def main():
         if not defer:
             accumulate(res.timers())
     if defer:
-        accumulate(ctx.timers_report().timers())
+        rep = ctx.timers_report().timers()
+        accumulate(rep)
+        exch = sum(ms for name, ms, _ in rep if name == "exchange")
 
     def allsum(x):
         if world == 1:

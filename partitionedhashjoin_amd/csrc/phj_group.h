@@ -501,7 +501,7 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
     // return): the local exchange's barrier must see every member
     int rc = hipSetDevice(c->device) == hipSuccess ? PHJ_OK : set_err(c, PHJ_ERR_HIP, "hipSetDevice");
     if (rc == PHJ_OK) {
-        reset_timers(c);
+        if (!c->defer_timers || c->timers.size() > kMaxTimerRecs) reset_timers(c);
         rc = member_alloc_radix(G, i, pl, p2);
     }
     if (rc == PHJ_OK && G.fail_member == i) rc = set_err(c, PHJ_ERR_STATE, "injected failure (phj_debug_fail_member)");
@@ -636,12 +636,12 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
     r->partition_ms = elapsed(c, t0, t1);
     r->build_ms = elapsed(c, b0, b1);
     r->probe_ms = p2 ? elapsed(c, t1, p1) : elapsed(c, b1, p1);
-    if (pl.cluster && c->tune.timers) {   // the LDS probe launch split by its clocks
+    if (pl.cluster && c->tune.timers && !c->defer_timers) {   // the LDS probe launch split by its clocks
         const double t = elapsed(c, t1, p1), fb = fused_build_fraction(c);
         r->build_ms += t * fb;
         r->probe_ms = t * (1.0 - fb);
     }
-    if (!p2 && c->last_fused) {
+    if (!p2 && c->last_fused && !c->defer_timers) {
         const double t = elapsed(c, b0, p1), fb = fused_build_fraction(c);
         r->build_ms = t * fb;
         r->probe_ms = t * (1.0 - fb);
@@ -795,6 +795,10 @@ void merge_results(Group& G, phj_join_result* r) {
 int group_join(phj_ctx* shell, const phj_join_params* p, phj_join_result* r, bool dry) {
     Group& G = *shell->group;
     G.res.assign(G.nlocal(), phj_join_result{});
+    // PHJ_DEFER_TIMERS (radix joins): each member keeps its timers for
+    // phj_timers_report (a rank context: one member); they accumulate over such joins
+    for (int i = 0; i < G.nlocal(); i++)
+        G.mem[i]->defer_timers = !dry && p->algo == PHJ_ALGO_RADIX && (p->flags & PHJ_DEFER_TIMERS) != 0;
     G.failed.store(0);
     struct FailOnce {   // an injected failure applies to one join
         Group& G;

@@ -106,6 +106,18 @@ def test_rccl_rank_context_world_of_one():
         assert 0 < expect < nS
         for name, p in PARAMS:
             assert ctx.join(p).matches == expect, name
+        # PHJ_DEFER_TIMERS on a rank context: the member keeps its timers,
+        # timers_report sums them (bench.py's timed loop at N > 1)
+        p = phj.radix_params((8, 8), hash=phj.HASH_MURMUR3)
+        single = {n for n, _, _ in ctx.join(p).timers()}
+        q = type(p).from_buffer_copy(p)
+        q.flags = p.flags | phj.DEFER_TIMERS
+        ctx.timers_report()
+        for _ in range(2):
+            r = ctx.join(q)
+            assert r.matches == expect and list(r.timers()) == []
+        summed = {n: ms for n, ms, _ in ctx.timers_report().timers()}
+        assert "exchange" in summed and set(summed) == single and all(ms >= 0 for ms in summed.values())
         # a one-device rank context also takes the building blocks
         v = ctx.partition(phj.SIDE_PROBE, phj.radix_params((8, 8)))
         assert v.n == nS
