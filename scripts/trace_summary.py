@@ -5,6 +5,9 @@ for the last bench step, the device timeline (start offsets and gaps).
   python scripts/trace_summary.py <dir with *_kernel_trace.csv> [--step-kernel NAME]
 (the step ends at the last launch whose name contains NAME, default k_probe,
 and the launches right behind it; "k_cluster_probe<" is the LDS join's probe)
+  --steps: also every step between consecutive matches, one line each: the
+  launches as name:gap-before+duration (us), and the span from one step's
+  last launch to the next step's (the timed loop's steps, host gaps included)
 """
 import csv
 import glob
@@ -49,6 +52,22 @@ def main():
             print(f"{(s - t0) / 1e3:9.1f} {(e - s) / 1e3:8.1f} {gap:8.1f}  {n.split('(')[0][:70]}")
             prev_end = e if prev_end is None else max(prev_end, e)
         print(f"step span: {(rows[last][1] - t0) / 1e3:.1f} us")
+    if "--steps" in sys.argv and probes:
+        ends = []   # each step's last launch: the match and the launches right behind it
+        for i in probes:
+            j = i
+            while j + 1 < len(rows) and rows[j + 1][0] < rows[j][1] + 200_000 and key not in rows[j + 1][2] \
+                    and rows[j + 1][0] - rows[j][1] < 2_000:
+                j += 1
+            ends.append(j)
+        print("\nsteps (us): span from the previous step's last launch; name:gap+duration")
+        for a, b in zip(ends[:-1], ends[1:]):
+            seq, prev = [], rows[a][1]
+            for s_, e_, n in rows[a + 1:b + 1]:
+                short = n.split("(")[0].replace("void ", "").replace("phj::", "").replace("__amd_rocclr_", "")[:28]
+                seq.append(f"{short}:{(s_ - prev) / 1e3:.1f}+{(e_ - s_) / 1e3:.1f}")
+                prev = e_
+            print(f"{(rows[b][1] - rows[a][1]) / 1e3:9.1f}  " + " | ".join(seq))
 
 
 if __name__ == "__main__":
