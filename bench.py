@@ -48,6 +48,9 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: the core share - 1 (cpu_threads)")
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes")
+    ap.add_argument("--all-timers", action="store_true",
+                    help="time every phase in the timed loop (default: PHJ_LEAN_TIMERS, only S's pass 1 and the "
+                         "LDS join; each event between two kernels delays the second by ~4 us)")
     ap.add_argument("--timers-per-step", dest="timers_deferred", action="store_false",
                     help="read each step's timers inside it (default: one device defers the readout past the timed "
                          "loop, PHJ_DEFER_TIMERS)")
@@ -293,12 +296,13 @@ def main():
     # one device: PHJ_DEFER_TIMERS keeps the timer readout (event queries, the
     # LDS join's clock split) out of the timed steps; the events are recorded
     # inside them and summed by timers_report after the loop
-    # (at N>1 each rank's context has one member: the same, per rank)
+    # (at N>1 each rank's context has one member: the same, per rank); one
+    # device: PHJ_LEAN_TIMERS also leaves R's pass-1 timer out (--all-timers)
     defer = args.timers_deferred and params.algo == phj.ALGO_RADIX
     timed_params = params
     if defer:
         timed_params = type(params).from_buffer_copy(params)
-        timed_params.flags = params.flags | phj.DEFER_TIMERS
+        timed_params.flags = params.flags | phj.DEFER_TIMERS | (0 if args.all_timers else phj.LEAN_TIMERS)
         ctx.timers_report()   # a clean slate
     results = [ctx.join(timed_params) for _ in range(args.steps)]
     barrier()

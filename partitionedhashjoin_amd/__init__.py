@@ -25,6 +25,7 @@ DEFAULT_SEED = 0x9E3779B97F4A7C15
 PART_STABLE = 0x1   # include/phj.h PHJ_PART_STABLE
 TABLE_CHAINED = 0x2   # include/phj.h PHJ_TABLE_CHAINED
 DEFER_TIMERS = 0x4   # include/phj.h PHJ_DEFER_TIMERS: timers read later by Context.timers_report()
+LEAN_TIMERS = 0x8    # include/phj.h PHJ_LEAN_TIMERS: only the critical path's large kernels timed
 
 
 def radix_params(bits=(8, 8), num_partitions=0, hash=HASH_MURMUR3, seed=DEFAULT_SEED,

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -59,6 +60,7 @@ struct Tuning {
     int p2probe = 1;      // radix join, 2 passes: the probe side's pass 2 on-chip (k_probe_ht)
     int p1_pipe = 1;      // keys-only pass 1: claims resolved a tile later over pre-allocated chunks (k_chunk_codes_pipe)
     int r_chunk = 1;      // LDS join on one device: R through the chunked code pass, read by tiles ("tile mode")
+    int count_pin = 1;    // LDS join: the last workgroup writes the count to pinned host memory (0: a copy back)
     int r_order = 1;      // LDS join: R's pass 1 beside S's (0), after it (1: measured C2 1.69 vs 1.72 ms, S.p1 1.05 vs 1.19), before it (2)
     int p1_kpf = 2;       // ... 1024 x 4: tiles of keys in flight ahead of the one hashed (1 or 2; 2 measured 1.08 -> 1.05 ms)
     int p1_prof = 0;      // PHJ_P1_PROF: the pipelined pass 1's phases to stderr (diagnostics)
@@ -170,8 +172,23 @@ struct phj_ctx {
     hipStream_t last_ev_stream = nullptr;  // ... on this stream ...
     uint32_t since_ev = 0;             // ... and the kernels launched since
     unsigned long long* count_host = nullptr;   // pinned: the count read back
+    // fine-grained pinned {count, failed} written by the LDS join's last
+    // workgroup (k_cluster_probe_big), its device address, and the launch's
+    // finished-workgroup counter; count_pinned: this join's count is there
+    unsigned long long* count_pin = nullptr;
+    unsigned long long* count_pin_dev = nullptr;
+    DevBuf cl_done;
+    bool count_pin_failed = false, count_pinned = false;
     unsigned long long* split_words = nullptr;  // the LDS probe's {build, probe} clocks (count buffer words 2-3), this join
     bool defer_timers = false;  // the running join has PHJ_DEFER_TIMERS: its timers stay for phj_timers_report
+    bool lean_timers = false;   // ... and PHJ_LEAN_TIMERS: the build side's timers are not recorded
+    bool timer_skipped = false; // the open timer was not recorded (timer_end records nothing)
+    // the next chunked pass-1 bookkeeping kernel also clears this chunk state
+    // (the LDS join: R's, cleared by S's k_pass1_finish_sizes on the same
+    // stream), and the pass whose state p1_cleared names skips its memset
+    void* p1_clear = nullptr;
+    size_t p1_clear_bytes = 0;
+    void* p1_cleared = nullptr;
 };
 
 namespace {
@@ -263,8 +280,20 @@ int mark(phj_ctx* c, hipEvent_t* out) {
     return PHJ_OK;
 }
 
+// mark, or the last event when it was recorded on this stream with nothing
+// launched after it (the same point of the stream: one marker packet fewer)
+int mark_shared(phj_ctx* c, hipEvent_t* out) {
+    if (c->last_ev && c->last_ev_stream == c->ks && c->since_ev == 0) {
+        *out = c->last_ev;
+        return PHJ_OK;
+    }
+    return mark(c, out);
+}
+
 int timer_begin(phj_ctx* c, const char* name, uint64_t bytes) {
     if (!c->tune.timers) return PHJ_OK;
+    c->timer_skipped = c->lean_timers && (std::strncmp(name, "R.", 2) == 0 || std::strcmp(name, "build.big") == 0);
+    if (c->timer_skipped) return PHJ_OK;   // PHJ_LEAN_TIMERS
     TimerRec t{name, bytes, nullptr, nullptr};
     // back-to-back timers on one stream share the boundary event (the previous
     // timer's end is this one's start when nothing was launched in between)
@@ -274,7 +303,13 @@ int timer_begin(phj_ctx* c, const char* name, uint64_t bytes) {
     return PHJ_OK;
 }
 
-int timer_end(phj_ctx* c) { return c->tune.timers ? mark(c, &c->timers.back().b) : PHJ_OK; }
+int timer_end(phj_ctx* c) {
+    if (c->timer_skipped) {
+        c->timer_skipped = false;
+        return PHJ_OK;
+    }
+    return c->tune.timers ? mark(c, &c->timers.back().b) : PHJ_OK;
+}
 
 // One launch reported as two timers (build, probe) split by the kernel's own clocks.
 int timer_begin_split(phj_ctx* c, uint64_t build_bytes, uint64_t probe_bytes) {
@@ -576,7 +611,8 @@ int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const st
     if (a.chunk_cursor) {
         // chunked pass 1: no histogram / scan; the digit cursors and the pool
         // counter start at zero
-        PHJ_HIP(c, hipMemsetAsync(a.chunk_cursor, 0, chunk_state_bytes(a.nbins), c->ks));
+        if (a.chunk_cursor == c->p1_cleared) c->p1_cleared = nullptr;   // cleared by the kernel before it
+        else PHJ_HIP(c, hipMemsetAsync(a.chunk_cursor, 0, chunk_state_bytes(a.nbins), c->ks));
         c->since_ev++;
         PHJ_TRY(timer_begin(c, sname.c_str(), n * (a.keys_only ? 24 : 32) + (a.out_dig ? n * (a.dig_wide ? 2 : 1) : 0)));
         if constexpr (IN_AOS && OUT_AOS && ITEMS <= 8) {
@@ -879,8 +915,14 @@ int partition_state(phj_ctx* c, SideState& S, const char* tag, const Plan& pl, b
     uint32_t* tb2 = pl.npass == 2 ? static_cast<uint32_t*>(S.tbase2.p) : nullptr;
     PHJ_TRY(launch_pass(c, pl.hk, true, p1_aos, a, nt1, std::string(tag) + ".p1", n, nt1 * pl.nb1));
     if (chunked) {
+        uint4* clr = nullptr;   // another pass's chunk state, cleared here (c->p1_clear)
+        if (c->p1_clear) {
+            clr = static_cast<uint4*>(c->p1_clear);
+            c->p1_cleared = c->p1_clear;
+            c->p1_clear = nullptr;
+        }
         hipLaunchKernelGGL(k_pass1_finish_sizes, dim3(1), dim3(kFinSizesBlock), 0, c->ks, a.chunk_cursor, pl.nb1, nshards, n, tile2,
-                           static_cast<uint32_t*>(S.bounds1.p), tb2, zero);
+                           static_cast<uint32_t*>(S.bounds1.p), tb2, zero, clr, static_cast<uint32_t>(c->p1_clear_bytes / 16));
         PHJ_LAUNCHED(c, "k_pass1_finish_sizes");
     } else {
         hipLaunchKernelGGL(k_pass1_finish, dim3(1), dim3(kFinBlock), 0, c->ks, a.hist, nt1, pl.nb1, n,
@@ -1451,8 +1493,30 @@ int cluster_big_fill(phj_ctx* c, const Plan& pl, int nseg, const int64_t* const*
     return PHJ_OK;
 }
 
+// The pinned count word pair (count_pin) and its device side; false: the
+// count comes back by a copy (get_count).
+bool count_pin_ready(phj_ctx* c) {
+    if (c->count_pin) return true;
+    if (c->count_pin_failed) return false;
+    void* h = nullptr;
+    void* d = nullptr;
+    if (hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer(&d, h, 0) != hipSuccess || ensure(c, c->cl_done, 4) != PHJ_OK ||
+        hipMemset(c->cl_done.p, 0, 4) != hipSuccess) {
+        (void)hipGetLastError();
+        if (h) (void)hipHostFree(h);
+        c->count_pin_failed = true;
+        return false;
+    }
+    c->count_pin = static_cast<unsigned long long*>(h);
+    c->count_pin_dev = static_cast<unsigned long long*>(d);
+    return true;
+}
+
+// pin: the last kernel also writes the count pair to count_pin (get_count
+// then only synchronises; one device-to-host copy fewer per join)
 int probe_cluster(phj_ctx* c, const Plan& pl, SideState& PS, int nseg, const int64_t* const* codes,
-                  const uint32_t* const* bounds, SideState* RT = nullptr) {
+                  const uint32_t* const* bounds, SideState* RT = nullptr, bool pin = false) {
     if (c->dry || PS.nt2 == 0) return PHJ_OK;
     if (!PS.hcoded) return set_err(c, PHJ_ERR_STATE, "the LDS join needs the keys-only pass 1 (codes)");
     ClusterArgs a = cluster_args(c, pl, nseg, codes, bounds, RT);
@@ -1521,7 +1585,15 @@ int probe_cluster(phj_ctx* c, const Plan& pl, SideState& PS, int nseg, const int
     a.split = nullptr;
     a.err = nullptr;
     a.err_r = nullptr;
-    hipLaunchKernelGGL(k_cluster_probe_big, dim3(pl.nb1), dim3(256), 0, c->ks, a);
+    if (pin && c->tune.count_pin && count_pin_ready(c)) {
+        // a value no launch writes (failed holds error bits): get_count falls
+        // back to the copy if the kernel left it
+        reinterpret_cast<volatile unsigned long long*>(c->count_pin)[1] = ~0ull;
+        a.host_out = c->count_pin_dev;
+        a.done = static_cast<uint32_t*>(c->cl_done.p);
+        c->count_pinned = true;
+    }
+    hipLaunchKernelGGL(k_cluster_probe_big, dim3(std::max<uint32_t>(kProbeBigGrid, (pl.nb1 + 255) / 256)), dim3(256), 0, c->ks, a);
     PHJ_LAUNCHED(c, "k_cluster_probe_big");
     return PHJ_OK;
 }
@@ -1531,6 +1603,36 @@ int probe_cluster(phj_ctx* c, const Plan& pl, SideState& PS, int nseg, const int
 // the on-chip probes' {count, failed}, failed set when S's pass 1 met a stale
 // chunk table (fold_pass1_error).
 int get_count(phj_ctx* c, uint64_t* out, bool pair = false) {
+    if (c->count_pinned) {   // written by the join's last workgroup (probe_cluster)
+        c->count_pinned = false;
+        const volatile unsigned long long* v = c->count_pin;
+        if (c->defer_timers) {
+            // no event is read in this join: poll the pinned word (the
+            // driver's stream synchronisation wakes later), asking every
+            // 4096 polls whether the stream has finished without it
+            for (uint32_t i = 1; v[1] == ~0ull; i++) {
+                if ((i & 4095u) == 0) {
+                    const hipError_t q = hipStreamQuery(c->ks);
+                    if (q == hipSuccess) break;
+                    if (q != hipErrorNotReady) PHJ_HIP(c, q);
+                }
+                __builtin_ia32_pause();
+            }
+            std::atomic_thread_fence(std::memory_order_acquire);
+        } else {
+            PHJ_HIP(c, hipStreamSynchronize(c->ks));
+        }
+        const unsigned long long failed = v[1];
+        if (failed != ~0ull) {
+            *out = v[0];
+            if (pair && failed) {
+                c->side[PHJ_SIDE_PROBE].chunk_check = true;   // read its word for the message
+                const int rc = check_chunk_errors(c);
+                return rc != PHJ_OK ? rc : chunk_table_error(c, 0);
+            }
+            return check_chunk_errors(c);
+        }
+    }
     if (!c->count_host && hipHostMalloc(reinterpret_cast<void**>(&c->count_host), 16, hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();
         c->count_host = nullptr;
@@ -1886,6 +1988,7 @@ int ctx_create_device(int device, phj_ctx** out) {
     c->tune.p1_prof = env_int("PHJ_P1_PROF", 0);
     c->tune.p1_kpf = env_int("PHJ_P1_KPF", 2) == 1 ? 1 : 2;
     c->tune.r_order = std::min(2, std::max(0, env_int("PHJ_R_ORDER", 1)));
+    c->tune.count_pin = env_int("PHJ_COUNT_PIN", 1);
     c->tune.r_chunk = env_int("PHJ_R_CHUNK", 1) != 0;
     c->tune.p1_block = env_int("PHJ_P1_BLOCK", 1024) == 512 ? 512 : 1024;
     c->tune.p1_tps = std::max(1, env_int("PHJ_P1_TPS", static_cast<int>(kTilesPerShard)));
@@ -2020,13 +2123,14 @@ void phj_ctx_destroy(phj_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     (void)hipStreamSynchronize(c->aux);
     if (c->count_host) (void)hipHostFree(c->count_host);
+    if (c->count_pin) (void)hipHostFree(c->count_pin);
     for (SideState& S : c->side) {
         for (DevBuf* b : {&S.owned, &S.kA, &S.pA, &S.kB, &S.pB, &S.hist1, &S.hist2, &S.bounds1, &S.tbase2,
                           &S.bounds, &S.partials, &S.tseg2, &S.dig, &S.ccur, &S.ctab, &S.tstart, &S.csink})
             free_buf(*b);
     }
     for (DevBuf* b : {&c->ht_tab, &c->ht_desc, &c->r_codes, &c->r_bounds, &c->scan_partials, &c->prep, &c->tkeys, &c->tpays, &c->toffs, &c->gcursor, &c->items, &c->biglist,
-                      &c->count, &c->np_tab, &c->np_pays, &c->np_ovf, &c->np_ovfb, &c->np_ovfn, &c->fitems, &c->split, &c->cl_prof, &c->mat_mark, &c->mat_cnt, &c->mat_rows})
+                      &c->count, &c->np_tab, &c->np_pays, &c->np_ovf, &c->np_ovfb, &c->np_ovfn, &c->fitems, &c->split, &c->cl_prof, &c->mat_mark, &c->mat_cnt, &c->mat_rows, &c->cl_done})
         free_buf(*b);
     for (hipEvent_t e : c->evpool) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->stream);
@@ -2214,6 +2318,7 @@ int phj_partition(phj_ctx* c, int side, const phj_join_params* p, phj_partitione
     // timers accumulate until phj_join / phj_join_partitioned / phj_timers_report
     // reports them; a caller that never reports loses the oldest records
     c->defer_timers = false;
+    c->lean_timers = false;
     if (c->timers.size() > kMaxTimerRecs) reset_timers(c);
     PHJ_TRY(partition_side(c, side, pl));
     if (out) *out = c->side[side].view;
@@ -2250,6 +2355,7 @@ int phj_join_partitioned(phj_ctx* c, const phj_join_params* p, int nbuild, const
     for (int g = 0; g < nbuild; g++) nR += build[g].n;
     r->algorithmic_bytes = nR * 32 + c->side[PHJ_SIDE_PROBE].view.n * 8 + nR * 8;
     c->defer_timers = false;
+    c->lean_timers = false;
     const int rc = fill_timers(c, r);  // includes the phj_partition launches since the last report
     reset_timers(c);
     return rc;
@@ -2285,6 +2391,9 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
     PHJ_HIP(c, hipSetDevice(c->device));
     std::memset(r, 0, sizeof(*r));
     c->defer_timers = (p->flags & PHJ_DEFER_TIMERS) != 0;
+    c->lean_timers = c->defer_timers && (p->flags & PHJ_LEAN_TIMERS) != 0;
+    c->timer_skipped = false;
+    c->count_pinned = false;
     if (!c->defer_timers || c->timers.size() > kMaxTimerRecs) reset_timers(c);
     if (p->algo == PHJ_ALGO_NO_PARTITIONING) return join_nopart(c, p, r);
     if (p->algo != PHJ_ALGO_RADIX) return set_err(c, PHJ_ERR_INVALID, "Unrecognized join algorithm");
@@ -2301,7 +2410,16 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
         // aux stream beside it; then the probe builds each cluster's table in
         // LDS and probes S's codes against it
         PHJ_TRY(ensure(c, c->count, 32));
-        PHJ_TRY(mark(c, &t0));
+        // the result's phase marks: with deferred timers nothing reads them
+        // (the result's phase times stay zero) and, R's chain on the main
+        // stream, no stream waits on them: not recorded (each event between
+        // two kernels delays the second by ~4 us)
+        const int order = c->tune.r_order;
+        const bool r_main = order == 1;
+        const bool no_marks = c->defer_timers && r_main;
+        t0 = tr = b0 = t1 = p1 = nullptr;
+        auto phase_mark = [&](hipEvent_t* e) -> int { return no_marks ? PHJ_OK : mark_shared(c, e); };
+        if (!no_marks) PHJ_TRY(mark(c, &t0));
         const int64_t* rcodes = nullptr;
         const uint32_t* rbnd = nullptr;
         // R's chain on the aux stream, after event `after`
@@ -2313,8 +2431,6 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
         // after S's pass (PHJ_R_ORDER=1, default) R's chain runs on the main
         // stream itself: nothing runs beside it, and a cross-stream event wait
         // before the probe costs ~15 us (measured gap, r05z timeline)
-        const int order = c->tune.r_order;
-        const bool r_main = order == 1;
         auto r_chain = [&](hipEvent_t after) -> int {
             if (!r_main) {
                 PHJ_HIP(c, hipStreamWaitEvent(c->aux, after, 0));
@@ -2332,13 +2448,13 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
                 rbnd = static_cast<const uint32_t*>(c->r_bounds.p);
                 if (rc == PHJ_OK) rc = partition_build(c, cpl, static_cast<int64_t*>(c->r_codes.p), static_cast<uint32_t*>(c->r_bounds.p));
             }
-            if (rc == PHJ_OK) rc = mark(c, &b0);
+            if (rc == PHJ_OK) rc = phase_mark(&b0);
             // the HBM tables of clusters beyond the LDS limit (none at the
             // balanced configurations; the LDS tables are built inside the probe)
             if (rc == PHJ_OK) rc = timer_begin(c, "build.big", 0);
             if (rc == PHJ_OK) rc = cluster_big_fill(c, cpl, 1, &rcodes, &rbnd, R.n, RT);
             if (rc == PHJ_OK) rc = timer_end(c);
-            if (rc == PHJ_OK) rc = mark(c, &tr);
+            if (rc == PHJ_OK) rc = phase_mark(&tr);
             c->ks = c->stream;
             return rc;
         };
@@ -2349,18 +2465,40 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
             PHJ_HIP(c, hipStreamWaitEvent(c->stream, tr, 0));
         }
         // the code pass's bookkeeping kernel clears the count pair (an empty
-        // S takes no chunked pass: a memset)
-        PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, cpl, true, static_cast<unsigned long long*>(c->count.p)));
+        // S takes no chunked pass: a memset). R's chain after S's pass on the
+        // same stream: S's bookkeeping kernel also clears R's chunk state (one
+        // memset launch and its gap fewer before R's pass)
+        const bool pre_clear = r_main && c->tune.r_chunk && R.n > 0 && !c->dry;
+        if (pre_clear) {
+            PHJ_TRY(ensure(c, R.ccur, chunk_state_bytes(cpl.nb1)));
+            c->p1_clear = R.ccur.p;
+            c->p1_clear_bytes = chunk_state_bytes(cpl.nb1);
+        }
+        const int prc = partition_side(c, PHJ_SIDE_PROBE, cpl, true, static_cast<unsigned long long*>(c->count.p));
+        c->p1_clear = nullptr;
+        if (prc != PHJ_OK) {
+            c->p1_cleared = nullptr;
+            return prc;
+        }
         if (!S.hcoded) PHJ_HIP(c, hipMemsetAsync(c->count.p, 0, 32, c->stream));
-        if (order != 2) PHJ_TRY(r_chain(t0));
+        if (order != 2) {
+            const int rc = r_chain(t0);
+            c->p1_cleared = nullptr;   // (R's pass may not have taken the chunked form)
+            PHJ_TRY(rc);
+        }
         if (!r_main) PHJ_HIP(c, hipStreamWaitEvent(c->stream, tr, 0));
-        PHJ_TRY(mark(c, &t1));
+        PHJ_TRY(phase_mark(&t1));
         // one launch, reported as "build" (the workgroups' table builds in LDS:
         // R's codes read) and "probe" (S's codes read), split by the kernel's own clocks
         PHJ_TRY(timer_begin_split(c, R.n * 8, S.n * 8));
-        PHJ_TRY(probe_cluster(c, cpl, S, 1, &rcodes, &rbnd, RT));
+        if (c->lean_timers && c->tune.timers) {   // build.big not timed: a zero-length record keeps the phase listed
+            const hipEvent_t e = c->timers.back().a;
+            c->timers.insert(c->timers.end() - 2, TimerRec{"build.big", 0, e, e});
+        }
+        c->count_pinned = false;
+        PHJ_TRY(probe_cluster(c, cpl, S, 1, &rcodes, &rbnd, RT, true));
         PHJ_TRY(timer_end_split(c));
-        PHJ_TRY(mark(c, &p1));
+        PHJ_TRY(phase_mark(&p1));
         uint64_t m = 0;
         PHJ_TRY(get_count(c, &m, true));
         r->matches = m;
@@ -2514,6 +2652,7 @@ int phj_timers_report(phj_ctx* c, phj_join_result* r) {
     PHJ_HIP(c, hipStreamSynchronize(c->ks));
     std::memset(r, 0, sizeof(*r));
     c->defer_timers = false;
+    c->lean_timers = false;
     const int rc = fill_timers(c, r);
     reset_timers(c);
     return rc;
@@ -2558,6 +2697,7 @@ int phj_join_materialize(phj_ctx* c, const phj_join_params* p, phj_join_result* 
     PHJ_HIP(c, hipSetDevice(c->device));
     std::memset(r, 0, sizeof(*r));
     c->defer_timers = false;
+    c->lean_timers = false;
     reset_timers(c);
     c->mat_n = 0;
     if (p->algo == PHJ_ALGO_NO_PARTITIONING) {
@@ -2622,6 +2762,7 @@ int phj_probe_pass1(phj_ctx* c, const phj_join_params* p, int64_t* keys, uint64_
             return set_err(c, PHJ_ERR_STATE, "these params do not take the on-chip probe");
     }
     c->defer_timers = false;
+    c->lean_timers = false;
     reset_timers(c);
     c->ks = c->stream;
     PHJ_TRY(partition_side(c, PHJ_SIDE_PROBE, pl, true));

@@ -89,6 +89,11 @@ struct ClusterArgs {
     const uint32_t* rt_cnt;       // tile -> codes
     const int64_t* r_pool;        // R's chunk pool (codes)
     const uint32_t* err_r;        // R's pass-1 error word (fold_pass1_error), or null
+    // k_cluster_probe_big: null, or the host's pinned {count, failed} that the
+    // launch's last workgroup writes (no read-back copy after the join); done
+    // counts its finished workgroups (zero between launches)
+    unsigned long long* host_out;
+    uint32_t* done;
 };
 
 // A cluster's table is in HBM (k_cluster_big_fill / k_cluster_probe_big):
@@ -207,38 +212,61 @@ __global__ __launch_bounds__(256) void k_cluster_big_fill(ClusterArgs a) {
     }
 }
 
-// The S tiles of the big clusters against their HBM tables: one workgroup per
-// cluster (the others return at once), its tiles from the pass-1 tile list.
+// Whether cluster d takes the HBM table (cl_big), from its sizes alone (one
+// thread; the same decision as cl_runs + cl_big).
+__device__ __forceinline__ bool cl_is_big(const ClusterArgs& a, uint32_t d) {
+    if (a.rt_base) return cl_big(a.r_bounds[0][d + 1] - a.r_bounds[0][d], a.rt_base[d + 1] - a.rt_base[d], a.lim);
+    uint32_t m = 0;
+    for (uint32_t g = 0; g < a.nseg; g++) m += a.r_bounds[g][d + 1] - a.r_bounds[g][d];
+    return cl_big(m, a.nseg, a.lim);
+}
+
+// The S tiles of the big clusters against their HBM tables, their tiles from
+// the pass-1 tile list. kProbeBigGrid workgroups: each finds the big clusters
+// among its share (clusters blockIdx.x + k * grid, one load round) and probes
+// them one by one (none at the balanced configurations). host_out: the last
+// workgroup to finish copies the count pair to the host.
+constexpr uint32_t kProbeBigGrid = 64;
 __global__ __launch_bounds__(256) void k_cluster_probe_big(ClusterArgs a) {
     __shared__ uint32_t sseg[kHtSegs + 1];
     __shared__ const int64_t* sptr[kHtSegs];
     __shared__ uint32_t sB, sM, sN;
     __shared__ uint32_t red[4];
-    const uint32_t d = blockIdx.x, tid = threadIdx.x;
-    cl_runs(a, d, sseg, sptr, &sB, &sM, &sN);
+    __shared__ uint32_t list[256], nlist;
+    const uint32_t tid = threadIdx.x, G = gridDim.x;
+    if (tid == 0) nlist = 0;
     __syncthreads();
-    const uint32_t m = sM;
-    if (!cl_big(m, sN, a.lim)) return;   // workgroup-uniform
-    const uint64_t e = d == 0 ? a.e1 : 0ull;
-    const uint32_t bmask = cl_big_cap(m) / 2 - 1;
-    const ulonglong2* g2 = reinterpret_cast<const ulonglong2*>(a.gtab + 4ull * sB + 2ull * d);
+    for (uint32_t d = blockIdx.x + tid * G; d < a.nb1; d += 256 * G)
+        if (cl_is_big(a, d)) list[atomicAdd(&nlist, 1u)] = d;   // (<= 256: nb1 <= 256 * grid)
+    __syncthreads();
+    const uint32_t nbig = nlist;
     uint32_t hits = 0;
-    for (uint32_t t = a.tile_base[d]; t < a.tile_base[d + 1]; t++) {
-        const uint32_t lo = a.tile_start[t], c = a.tile_cnt[t];
-        for (uint32_t i = tid; i < c; i += 256) {
-            const uint64_t cc = static_cast<uint64_t>(a.s_codes[lo + i]);
-            uint32_t b = static_cast<uint32_t>(cc >> kHtBucketShift) & bmask;
-            for (;;) {
-                const ulonglong2 w = g2[b];
-                if (w.x == cc || w.y == cc) {
-                    hits++;
-                    break;
+    for (uint32_t k = 0; k < nbig; k++) {
+        const uint32_t d = list[k];
+        cl_runs(a, d, sseg, sptr, &sB, &sM, &sN);
+        __syncthreads();
+        const uint64_t e = d == 0 ? a.e1 : 0ull;
+        const uint32_t bmask = cl_big_cap(sM) / 2 - 1;
+        const ulonglong2* g2 = reinterpret_cast<const ulonglong2*>(a.gtab + 4ull * sB + 2ull * d);
+        __syncthreads();   // (sB / sM read before the next cluster's cl_runs)
+        for (uint32_t t = a.tile_base[d]; t < a.tile_base[d + 1]; t++) {
+            const uint32_t lo = a.tile_start[t], c = a.tile_cnt[t];
+            for (uint32_t i = tid; i < c; i += 256) {
+                const uint64_t cc = static_cast<uint64_t>(a.s_codes[lo + i]);
+                uint32_t b = static_cast<uint32_t>(cc >> kHtBucketShift) & bmask;
+                for (;;) {
+                    const ulonglong2 w = g2[b];
+                    if (w.x == cc || w.y == cc) {
+                        hits++;
+                        break;
+                    }
+                    if (w.y == e) break;
+                    b = (b + 1) & bmask;
                 }
-                if (w.y == e) break;
-                b = (b + 1) & bmask;
             }
         }
     }
+    if (nbig == 0 && !a.host_out) return;   // workgroup-uniform
     uint32_t x = hits;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) x += __shfl_down(x, o, 64);
@@ -247,6 +275,18 @@ __global__ __launch_bounds__(256) void k_cluster_probe_big(ClusterArgs a) {
     if (tid == 0) {
         const unsigned long long s = static_cast<unsigned long long>(red[0]) + red[1] + red[2] + red[3];
         if (s) atomicAdd(a.count, s);
+        if (a.host_out) {
+            __threadfence();
+            if (atomicAdd(a.done, 1u) == G - 1) {   // every other workgroup's count is in
+                __threadfence();
+                const unsigned long long c0 = atomicAdd(a.count, 0ull), c1 = atomicAdd(a.count + 1, 0ull);
+                a.host_out[0] = c0;   // vector stores to fine-grained host memory; the
+                __threadfence_system();   // host polls word 1, so word 0 lands first
+                a.host_out[1] = c1;
+                __threadfence_system();
+                atomicExch(a.done, 0u);
+            }
+        }
     }
 }
 

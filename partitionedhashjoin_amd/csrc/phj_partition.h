@@ -1660,15 +1660,19 @@ __global__ __launch_bounds__(kBlock) void k_tile_chunks(const uint32_t* tile_bas
 // After a chunked pass 1: bounds1 = exclusive scan of the digit sizes (summed
 // over the shards: the segments' offsets in the pass-2 output) and
 // tile_base2 = exclusive scan of their chunk counts; `zero` (may be null: four
-// words) is cleared. One workgroup.
+// words) and `clr` (may be null: clr16 16-B words, another pass's chunk state)
+// are cleared. One workgroup.
 constexpr uint32_t kFinSizesBlock = 1024;   // one digit per thread at 1024 clusters: one round of shard loads
 __global__ __launch_bounds__(kFinSizesBlock) void k_pass1_finish_sizes(const uint32_t* sizes, uint32_t nb, uint32_t nshards,
                                                                        uint32_t n, uint32_t T, uint32_t* bounds1,
-                                                                       uint32_t* tile_base2, unsigned long long* zero) {
+                                                                       uint32_t* tile_base2, unsigned long long* zero,
+                                                                       uint4* clr, uint32_t clr16) {
     constexpr uint32_t B = kFinSizesBlock;
     __shared__ uint32_t wsum[2][B / 64];
     const uint32_t tid = threadIdx.x;
     if (zero && tid < 4) zero[tid] = 0;   // the on-chip probe's {count, failed} and its clock split (one launch fewer before it)
+    if (clr)
+        for (uint32_t i = tid; i < clr16; i += B) clr[i] = make_uint4(0, 0, 0, 0);
     uint32_t cx = 0, cy = 0;
     for (uint32_t base = 0; base < nb; base += B) {
         const uint32_t d = base + tid;

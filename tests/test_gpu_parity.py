@@ -495,6 +495,29 @@ def test_cluster_tile_mode_runs(monkeypatch, env):
         c.close()
 
 
+@pytest.mark.parametrize("env", [{}, {"PHJ_R_CHUNK": "0"}, {"PHJ_COUNT_PIN": "0"}], ids=["tiles", "stable", "copy"])
+def test_cluster_many_big(monkeypatch, env):
+    """Hundreds of clusters above the LDS limit (300 hot keys, 13K copies
+    each, beside 1M distinct keys): each of k_cluster_probe_big's workgroups
+    finds several big clusters in its share and probes them in turn; its last
+    workgroup writes the count to the host (PHJ_COUNT_PIN=0: the count is
+    copied back). Counted against the oracle."""
+    c = _cluster_ctx(monkeypatch, **env)
+    try:
+        params = phj.radix_params((8, 8), hash=phj.HASH_MURMUR3, seed=SEED)
+        rng = np.random.default_rng(91)
+        hot = rng.choice(np.arange(-10_000_000, 10_000_000, dtype=np.int64), 300, replace=False)
+        R = np.concatenate([np.repeat(hot, 13_000), rng.integers(-20_000_000, 20_000_000, 1_000_000, dtype=np.int64)])
+        S = np.concatenate([hot[::2], rng.integers(-40_000_000, 40_000_000, 2_000_000, dtype=np.int64)])
+        rng.shuffle(R)
+        rng.shuffle(S)
+        expect = O.semijoin_count_keys(R, S)
+        assert _gpu_count(c, R, S, params) == expect
+        assert c.join(params).matches == expect
+    finally:
+        c.close()
+
+
 def test_deferred_timers(ctx):
     """PHJ_DEFER_TIMERS: the join's result carries its count but no timers;
     the context keeps them, and timers_report returns their sums over the

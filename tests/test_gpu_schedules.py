@@ -72,6 +72,7 @@ SCHEDULES = [
     {"PHJ_R_CHUNK": "0", "PHJ_CL_BITS": "11"},                  # ... 2048 clusters
     {"PHJ_R_ORDER": "0"},                                       # LDS join: R's pass 1 beside S's
     {"PHJ_R_ORDER": "2"},                                       # ... before it
+    {"PHJ_COUNT_PIN": "0"},                                     # LDS join: the count read back by a copy
     {"PHJ_P1_PROF": "1", "PHJ_CL_PROF": "1"},                   # the phase clocks of pass 1 and of the LDS join's builds
 ]
 
