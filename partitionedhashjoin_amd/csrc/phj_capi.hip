@@ -189,6 +189,13 @@ struct phj_ctx {
     void* p1_clear = nullptr;
     size_t p1_clear_bytes = 0;
     void* p1_cleared = nullptr;
+    // the probe side's chunk state left all zero by the last join's final
+    // workgroup (k_cluster_probe_big, s_clear) and its size; pending: asked
+    // of the running join, confirmed when its count shows no failure
+    void* s_zeroed = nullptr;
+    size_t s_zeroed_bytes = 0;
+    void* s_zero_pending = nullptr;
+    size_t s_zero_pending_bytes = 0;
 };
 
 namespace {
@@ -611,8 +618,10 @@ int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const st
     if (a.chunk_cursor) {
         // chunked pass 1: no histogram / scan; the digit cursors and the pool
         // counter start at zero
+        const bool zeroed = a.chunk_cursor == c->s_zeroed && chunk_state_bytes(a.nbins) <= c->s_zeroed_bytes;
+        if (a.chunk_cursor == c->s_zeroed) c->s_zeroed = nullptr;   // (this pass writes it)
         if (a.chunk_cursor == c->p1_cleared) c->p1_cleared = nullptr;   // cleared by the kernel before it
-        else PHJ_HIP(c, hipMemsetAsync(a.chunk_cursor, 0, chunk_state_bytes(a.nbins), c->ks));
+        else if (!zeroed) PHJ_HIP(c, hipMemsetAsync(a.chunk_cursor, 0, chunk_state_bytes(a.nbins), c->ks));
         c->since_ev++;
         PHJ_TRY(timer_begin(c, sname.c_str(), n * (a.keys_only ? 24 : 32) + (a.out_dig ? n * (a.dig_wide ? 2 : 1) : 0)));
         if constexpr (IN_AOS && OUT_AOS && ITEMS <= 8) {
@@ -1592,6 +1601,11 @@ int probe_cluster(phj_ctx* c, const Plan& pl, SideState& PS, int nseg, const int
         a.host_out = c->count_pin_dev;
         a.done = static_cast<uint32_t*>(c->cl_done.p);
         c->count_pinned = true;
+        // S's chunk state is read no more after this launch: cleared for the next join
+        a.s_clear = static_cast<uint4*>(PS.ccur.p);
+        a.s_clear16 = static_cast<uint32_t>(chunk_state_bytes(PS.plan.nb1) / 16);
+        c->s_zero_pending = PS.ccur.p;
+        c->s_zero_pending_bytes = chunk_state_bytes(PS.plan.nb1);
     }
     hipLaunchKernelGGL(k_cluster_probe_big, dim3(std::max<uint32_t>(kProbeBigGrid, (pl.nb1 + 255) / 256)), dim3(256), 0, c->ks, a);
     PHJ_LAUNCHED(c, "k_cluster_probe_big");
@@ -1623,6 +1637,11 @@ int get_count(phj_ctx* c, uint64_t* out, bool pair = false) {
             PHJ_HIP(c, hipStreamSynchronize(c->ks));
         }
         const unsigned long long failed = v[1];
+        if (failed == 0) {   // the last workgroup cleared S's chunk state
+            c->s_zeroed = c->s_zero_pending;
+            c->s_zeroed_bytes = c->s_zero_pending_bytes;
+        }
+        c->s_zero_pending = nullptr;
         if (failed != ~0ull) {
             *out = v[0];
             if (pair && failed) {

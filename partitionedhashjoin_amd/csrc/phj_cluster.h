@@ -94,6 +94,11 @@ struct ClusterArgs {
     // counts its finished workgroups (zero between launches)
     unsigned long long* host_out;
     uint32_t* done;
+    // with host_out: the probe side's chunk state (s_clear16 16-B words),
+    // cleared by the last workgroup when the join did not fail (the next
+    // join's pass 1 then skips its memset)
+    uint4* s_clear;
+    uint32_t s_clear16;
 };
 
 // A cluster's table is in HBM (k_cluster_big_fill / k_cluster_probe_big):
@@ -267,12 +272,14 @@ __global__ __launch_bounds__(256) void k_cluster_probe_big(ClusterArgs a) {
         }
     }
     if (nbig == 0 && !a.host_out) return;   // workgroup-uniform
+    __shared__ uint32_t clear_state;
     uint32_t x = hits;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) x += __shfl_down(x, o, 64);
     if ((tid & 63) == 0) red[tid >> 6] = x;
     __syncthreads();
     if (tid == 0) {
+        clear_state = 0;
         const unsigned long long s = static_cast<unsigned long long>(red[0]) + red[1] + red[2] + red[3];
         if (s) atomicAdd(a.count, s);
         if (a.host_out) {
@@ -285,9 +292,13 @@ __global__ __launch_bounds__(256) void k_cluster_probe_big(ClusterArgs a) {
                 a.host_out[1] = c1;
                 __threadfence_system();
                 atomicExch(a.done, 0u);
+                clear_state = a.s_clear && c1 == 0 ? 1u : 0u;
             }
         }
     }
+    __syncthreads();
+    if (clear_state)
+        for (uint32_t i = tid; i < a.s_clear16; i += 256) a.s_clear[i] = make_uint4(0, 0, 0, 0);
 }
 
 // The probe. LDS: the cluster table (cap slots) + a few words. PF: tiles

@@ -539,7 +539,41 @@ def test_deferred_timers(ctx):
     assert set(summed) == set(single)
     for name in ("S.p1.scatter", "probe"):
         assert summed[name] > 1.5 * single[name]   # three joins' worth
+    # PHJ_LEAN_TIMERS: the build side's pass-1 timers are not recorded,
+    # build.big is listed at zero; back-to-back joins reuse S's chunk state
+    # cleared by the previous join's last workgroup
+    q.flags = p.flags | phj.DEFER_TIMERS | phj.LEAN_TIMERS
+    for _ in range(3):
+        assert ctx.join(q).matches == 3_000_000
+    lean = {name: ms for name, ms, _ in ctx.timers_report().timers()}
+    assert not [n for n in lean if n.startswith("R.")] and lean["build.big"] == 0
+    assert {"S.p1.scatter", "build", "probe"} <= set(lean) and lean["S.p1.scatter"] > 1.5 * single["S.p1.scatter"]
     assert ctx.join(p).timers()
+
+
+def test_cleared_chunk_state_between_calls(ctx):
+    """The LDS join's last workgroup clears S's chunk state for the next
+    join's pass 1 (no memset): deferred and plain joins interleaved with an
+    unordered partition of S stay exact, the partition matches the oracle's
+    (the stale-table failure, after which the state is not cleared:
+    test_gpu_chunk_guard.py)."""
+    R, S = O.generate_tables(200_000, 1_500_003, 1.05, 5, threads=4)
+    S[::5, 0] += 200_000
+    expect = O.semijoin_count(R, S)
+    ctx.upload(phj.SIDE_BUILD, R)
+    ctx.upload(phj.SIDE_PROBE, S)
+    p = phj.radix_params((8, 8), hash=phj.HASH_MURMUR3, seed=SEED)
+    q = type(p).from_buffer_copy(p)
+    q.flags = p.flags | phj.DEFER_TIMERS | phj.LEAN_TIMERS
+    for params in (q, q, p, q):
+        assert ctx.join(params).matches == expect
+    u = phj.radix_params((8, 8), hash=phj.HASH_MURMUR3, seed=SEED, stable=False)
+    out, ob = O.partition(S, 1 << 16, True, O.HASH_MURMUR3, SEED, workers=2)
+    k, pay, bounds = ctx.download_partitioned(ctx.partition(phj.SIDE_PROBE, u))
+    assert_same_partitions(k, pay, bounds, out, ob)
+    for params in (q, p):
+        assert ctx.join(params).matches == expect
+    ctx.timers_report()
 
 
 def test_cluster_path_is_default_for_c2_shape(ctx):
