@@ -302,7 +302,9 @@ def main():
     timed_params = params
     if defer:
         timed_params = type(params).from_buffer_copy(params)
-        timed_params.flags = params.flags | phj.DEFER_TIMERS | (0 if args.all_timers else phj.LEAN_TIMERS)
+        # (lean on one device: 7 us faster there, 8 us slower in the W=8 rehearsal's member step)
+        lean = world == 1 and not exchange and not args.all_timers
+        timed_params.flags = params.flags | phj.DEFER_TIMERS | (phj.LEAN_TIMERS if lean else 0)
         ctx.timers_report()   # a clean slate
     results = [ctx.join(timed_params) for _ in range(args.steps)]
     barrier()

@@ -104,11 +104,11 @@ typedef struct phj_join_params {
  * fields partition_ms .. total_ms and the timer list stay zero. A benchmark
  * loop sets it to keep the readout off its timed steps (bench.py). */
 #define PHJ_DEFER_TIMERS 0x4
-/* flags: PHJ_LEAN_TIMERS (one device, with PHJ_DEFER_TIMERS) records only the
- * timers of the critical path's large kernels (the probe side's pass 1, the
- * LDS join's build and probe): every event recorded between two kernels
- * delays the second by ~4 us. The build side's pass-1 and big-cluster timers
- * are not recorded. */
+/* flags: PHJ_LEAN_TIMERS records only the timers of the large kernels (the
+ * probe side's pass 1, the LDS join's build and probe, the exchange): every
+ * event recorded between two kernels delays the second by ~4 us. The build
+ * side's pass-1 timers are not recorded, the big clusters' tables
+ * (`build.big`) are listed at zero. */
 #define PHJ_LEAN_TIMERS 0x8
 #define PHJ_MAX_TIMERS 32
 #define PHJ_TIMER_NAME 24

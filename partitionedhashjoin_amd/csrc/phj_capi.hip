@@ -181,7 +181,7 @@ struct phj_ctx {
     bool count_pin_failed = false, count_pinned = false;
     unsigned long long* split_words = nullptr;  // the LDS probe's {build, probe} clocks (count buffer words 2-3), this join
     bool defer_timers = false;  // the running join has PHJ_DEFER_TIMERS: its timers stay for phj_timers_report
-    bool lean_timers = false;   // ... and PHJ_LEAN_TIMERS: the build side's timers are not recorded
+    bool lean_timers = false;   // PHJ_LEAN_TIMERS: the build side's timers are not recorded
     bool timer_skipped = false; // the open timer was not recorded (timer_end records nothing)
     // the next chunked pass-1 bookkeeping kernel also clears this chunk state
     // (the LDS join: R's, cleared by S's k_pass1_finish_sizes on the same
@@ -2410,7 +2410,7 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
     PHJ_HIP(c, hipSetDevice(c->device));
     std::memset(r, 0, sizeof(*r));
     c->defer_timers = (p->flags & PHJ_DEFER_TIMERS) != 0;
-    c->lean_timers = c->defer_timers && (p->flags & PHJ_LEAN_TIMERS) != 0;
+    c->lean_timers = (p->flags & PHJ_LEAN_TIMERS) != 0;
     c->timer_skipped = false;
     c->count_pinned = false;
     if (!c->defer_timers || c->timers.size() > kMaxTimerRecs) reset_timers(c);

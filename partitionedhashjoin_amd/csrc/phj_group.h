@@ -562,7 +562,7 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
     const int rx = allgather_blocks(G, i, L.elems, rc == PHJ_OK);
     if (rc == PHJ_OK) rc = rx;
     if (rc == PHJ_OK) rc = timer_end(c);
-    if (rc == PHJ_OK) rc = mark(c, &x1);
+    if (rc == PHJ_OK) rc = mark_shared(c, &x1);
     if (p2) {
         b0 = x1;
         const int64_t* codes[kHtSegs];
@@ -577,7 +577,7 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
             if (rc == PHJ_OK) rc = build_ht(c, pl, G.world, codes, bnd, nRall);
         }
         if (rc == PHJ_OK) rc = timer_end(c);
-        if (rc == PHJ_OK) rc = mark(c, &b1);
+        if (rc == PHJ_OK) rc = mark_shared(c, &b1);
     } else if (rc == PHJ_OK) {
         gathered_segments(G, i, L, P, segs.data());
     }
@@ -602,6 +602,10 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
                 const uint32_t* bnd[kHtSegs];
                 gathered_codes(G, i, L, codes, bnd);
                 PHJ_TRY(timer_begin_split(c, total(G.n[PHJ_SIDE_BUILD]) * 8, c->side[PHJ_SIDE_PROBE].n * 8));
+                if (c->lean_timers && c->tune.timers) {   // build.big not timed: listed at zero
+                    const hipEvent_t e = c->timers.back().a;
+                    c->timers.insert(c->timers.end() - 2, TimerRec{"build.big", 0, e, e});
+                }
                 PHJ_TRY(probe_cluster(c, pl, c->side[PHJ_SIDE_PROBE], G.world, codes, bnd));
                 PHJ_TRY(timer_end_split(c));
             } else {
@@ -609,7 +613,7 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
                 PHJ_TRY(probe_ht(c, pl, c->side[PHJ_SIDE_PROBE], false));
                 PHJ_TRY(timer_end(c));
             }
-            PHJ_TRY(mark(c, &p1));
+            PHJ_TRY(mark_shared(c, &p1));
             c->last_fused = false;
             return PHJ_OK;
         }
@@ -797,8 +801,12 @@ int group_join(phj_ctx* shell, const phj_join_params* p, phj_join_result* r, boo
     G.res.assign(G.nlocal(), phj_join_result{});
     // PHJ_DEFER_TIMERS (radix joins): each member keeps its timers for
     // phj_timers_report (a rank context: one member); they accumulate over such joins
-    for (int i = 0; i < G.nlocal(); i++)
+    // PHJ_LEAN_TIMERS: the build side's pass-1 timers are not recorded
+    for (int i = 0; i < G.nlocal(); i++) {
         G.mem[i]->defer_timers = !dry && p->algo == PHJ_ALGO_RADIX && (p->flags & PHJ_DEFER_TIMERS) != 0;
+        G.mem[i]->lean_timers = !dry && p->algo == PHJ_ALGO_RADIX && (p->flags & PHJ_LEAN_TIMERS) != 0;
+        G.mem[i]->timer_skipped = false;
+    }
     G.failed.store(0);
     struct FailOnce {   // an injected failure applies to one join
         Group& G;
