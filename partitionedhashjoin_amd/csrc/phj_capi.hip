@@ -61,6 +61,7 @@ struct Tuning {
     int p1_pipe = 1;      // keys-only pass 1: claims resolved a tile later over pre-allocated chunks (k_chunk_codes_pipe)
     int r_chunk = 1;      // LDS join on one device: R through the chunked code pass, read by tiles ("tile mode")
     int count_pin = 1;    // LDS join: the last workgroup writes the count to pinned host memory (0: a copy back)
+    int p1_tiles1 = 0;    // 1: chunked pass 1's scan + tile lists in one launch (k_chunk_tiles: measured slower, 32 vs 17 us at C2)
     int r_order = 1;      // LDS join: R's pass 1 beside S's (0), after it (1: measured C2 1.69 vs 1.72 ms, S.p1 1.05 vs 1.19), before it (2)
     int p1_kpf = 2;       // ... 1024 x 4: tiles of keys in flight ahead of the one hashed (1 or 2; 2 measured 1.08 -> 1.05 ms)
     int p1_prof = 0;      // PHJ_P1_PROF: the pipelined pass 1's phases to stderr (diagnostics)
@@ -930,9 +931,18 @@ int partition_state(phj_ctx* c, SideState& S, const char* tag, const Plan& pl, b
             c->p1_cleared = c->p1_clear;
             c->p1_clear = nullptr;
         }
-        hipLaunchKernelGGL(k_pass1_finish_sizes, dim3(1), dim3(kFinSizesBlock), 0, c->ks, a.chunk_cursor, pl.nb1, nshards, n, tile2,
-                           static_cast<uint32_t*>(S.bounds1.p), tb2, zero, clr, static_cast<uint32_t>(c->p1_clear_bytes / 16));
-        PHJ_LAUNCHED(c, "k_pass1_finish_sizes");
+        if (c->tune.p1_tiles1) {   // with the tile lists below, one launch
+            uint32_t* ts = static_cast<uint32_t*>(S.tstart.p);
+            hipLaunchKernelGGL(k_chunk_tiles, dim3(pl.nb1), dim3(kBlock), 0, c->ks, a.chunk_cursor, pl.nb1, nshards, n, tile2,
+                               static_cast<uint32_t*>(S.bounds1.p), tb2, static_cast<unsigned long long*>(S.ctab.p), maxch,
+                               pool_stride, static_cast<uint32_t*>(S.tseg2.p), ts, ts + nt2max, zero, clr,
+                               static_cast<uint32_t>(c->p1_clear_bytes / 16));
+            PHJ_LAUNCHED(c, "k_chunk_tiles");
+        } else {
+            hipLaunchKernelGGL(k_pass1_finish_sizes, dim3(1), dim3(kFinSizesBlock), 0, c->ks, a.chunk_cursor, pl.nb1, nshards, n, tile2,
+                               static_cast<uint32_t*>(S.bounds1.p), tb2, zero, clr, static_cast<uint32_t>(c->p1_clear_bytes / 16));
+            PHJ_LAUNCHED(c, "k_pass1_finish_sizes");
+        }
     } else {
         hipLaunchKernelGGL(k_pass1_finish, dim3(1), dim3(kFinBlock), 0, c->ks, a.hist, nt1, pl.nb1, n,
                            pl.npass == 2 ? tile2 : tile, static_cast<uint32_t*>(S.bounds1.p), tb2);
@@ -958,11 +968,13 @@ int partition_state(phj_ctx* c, SideState& S, const char* tag, const Plan& pl, b
             if (chunked) {
                 uint32_t* ts = static_cast<uint32_t*>(S.tstart.p);
                 uint32_t* tc = ts + nt2max;
-                hipLaunchKernelGGL(k_tile_chunks, dim3((pl.nb1 * nshards + kWaves - 1) / kWaves), dim3(kBlock), 0, c->ks, tb2,
-                                   static_cast<uint32_t*>(S.ccur.p), pl.nb1, nshards,
-                                   static_cast<unsigned long long*>(S.ctab.p), maxch, pool_stride, tile2,
-                                   static_cast<uint32_t*>(S.tseg2.p), ts, tc);
-                PHJ_LAUNCHED(c, "k_tile_chunks");
+                if (!c->tune.p1_tiles1) {   // (else written by k_chunk_tiles above)
+                    hipLaunchKernelGGL(k_tile_chunks, dim3((pl.nb1 * nshards + kWaves - 1) / kWaves), dim3(kBlock), 0, c->ks, tb2,
+                                       static_cast<uint32_t*>(S.ccur.p), pl.nb1, nshards,
+                                       static_cast<unsigned long long*>(S.ctab.p), maxch, pool_stride, tile2,
+                                       static_cast<uint32_t*>(S.tseg2.p), ts, tc);
+                    PHJ_LAUNCHED(c, "k_tile_chunks");
+                }
                 S.ctab_dirty = false;
                 b.tile_start = ts;
                 b.tile_cnt = tc;
@@ -2008,6 +2020,7 @@ int ctx_create_device(int device, phj_ctx** out) {
     c->tune.p1_kpf = env_int("PHJ_P1_KPF", 2) == 1 ? 1 : 2;
     c->tune.r_order = std::min(2, std::max(0, env_int("PHJ_R_ORDER", 1)));
     c->tune.count_pin = env_int("PHJ_COUNT_PIN", 1);
+    c->tune.p1_tiles1 = env_int("PHJ_P1_TILES1", 0);
     c->tune.r_chunk = env_int("PHJ_R_CHUNK", 1) != 0;
     c->tune.p1_block = env_int("PHJ_P1_BLOCK", 1024) == 512 ? 512 : 1024;
     c->tune.p1_tps = std::max(1, env_int("PHJ_P1_TPS", static_cast<int>(kTilesPerShard)));

@@ -569,6 +569,10 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
         const uint32_t* bnd[kHtSegs];
         gathered_codes(G, i, L, codes, bnd);
         const uint64_t nRall = total(G.n[PHJ_SIDE_BUILD]);
+        // the probe (aux, behind the tables) needs S's pass 1: the wait goes
+        // before the tables, so the marks between them and the probe are one
+        // event (a wait between them would cost another)
+        if (rc == PHJ_OK && sdone && hipStreamWaitEvent(c->aux, sdone, 0) != hipSuccess) rc = set_err(c, PHJ_ERR_HIP, "wait S");
         if (pl.cluster) {   // only the big clusters' HBM tables; the LDS tables are built in the probe
             if (rc == PHJ_OK) rc = timer_begin(c, "build.big", 0);
             if (rc == PHJ_OK) rc = cluster_big_fill(c, pl, G.world, codes, bnd, nRall);
@@ -594,9 +598,8 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
     // (the S shard's pass 1 went out on the main stream before the exchange)
     auto join_local = [&]() -> int {
         if (p2) {   // on the aux stream, behind the tables
-            c->ks = c->aux;
-            PHJ_HIP(c, hipStreamWaitEvent(c->aux, sdone, 0));
-            PHJ_TRY(mark(c, &t1));
+            c->ks = c->aux;   // (S's pass 1 waited for before the tables)
+            PHJ_TRY(mark_shared(c, &t1));
             if (pl.cluster) {   // one launch: "build" (LDS tables) / "probe" by its clocks
                 const int64_t* codes[kHtSegs];
                 const uint32_t* bnd[kHtSegs];
