@@ -8,6 +8,7 @@
 // once (grow-only) before the timed region; phases are timed with hipEvents
 // on the same stream. Errors never cross the ABI as exceptions: they become
 // negative status codes plus a message (phj_last_error).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -61,6 +62,7 @@ struct Tuning {
     int p1_pipe = 1;      // keys-only pass 1: claims resolved a tile later over pre-allocated chunks (k_chunk_codes_pipe)
     int r_chunk = 1;      // LDS join on one device: R through the chunked code pass, read by tiles ("tile mode")
     int count_pin = 1;    // LDS join: the last workgroup writes the count to pinned host memory (0: a copy back)
+    int ext_timers = 0;   // 1: the large kernels' timers from their own dispatch (hipExtLaunchKernel events; measured no faster)
     int p1_tiles1 = 0;    // 1: chunked pass 1's scan + tile lists in one launch (k_chunk_tiles: measured slower, 32 vs 17 us at C2)
     int r_order = 1;      // LDS join: R's pass 1 beside S's (0), after it (1: measured C2 1.69 vs 1.72 ms, S.p1 1.05 vs 1.19), before it (2)
     int p1_kpf = 2;       // ... 1024 x 4: tiles of keys in flight ahead of the one hashed (1 or 2; 2 measured 1.08 -> 1.05 ms)
@@ -184,6 +186,7 @@ struct phj_ctx {
     bool defer_timers = false;  // the running join has PHJ_DEFER_TIMERS: its timers stay for phj_timers_report
     bool lean_timers = false;   // PHJ_LEAN_TIMERS: the build side's timers are not recorded
     bool timer_skipped = false; // the open timer was not recorded (timer_end records nothing)
+    bool timer_ext = false;     // the open timer's events come from the next launch_ext (timer_end records nothing)
     // the next chunked pass-1 bookkeeping kernel also clears this chunk state
     // (the LDS join: R's, cleared by S's k_pass1_finish_sizes on the same
     // stream), and the pass whose state p1_cleared names skips its memset
@@ -311,7 +314,43 @@ int timer_begin(phj_ctx* c, const char* name, uint64_t bytes) {
     return PHJ_OK;
 }
 
+// A timer whose events the kernel's own dispatch records (launch_ext): no
+// marker packet before or after the kernel (each delays the next kernel ~4 us).
+int timer_begin_ext(phj_ctx* c, const char* name, uint64_t bytes) {
+    if (!c->tune.timers) return PHJ_OK;
+    if (!c->tune.ext_timers) return timer_begin(c, name, bytes);
+    c->timer_skipped = c->lean_timers && (std::strncmp(name, "R.", 2) == 0 || std::strcmp(name, "build.big") == 0);
+    if (c->timer_skipped) return PHJ_OK;
+    TimerRec t{name, bytes, next_event(c), next_event(c)};
+    if (!t.a || !t.b) return set_err(c, PHJ_ERR_HIP, "hipEventCreate failed");
+    c->timers.push_back(t);
+    c->timer_ext = true;
+    return PHJ_OK;
+}
+
+// Launch kfn; after timer_begin_ext (or timer_begin_split_ext) its events are
+// the open timer's (or the split pair's) start and stop.
+int launch_ext(phj_ctx* c, const void* kfn, dim3 grid, dim3 block, void** args, size_t lds, const char* what) {
+    if (!c->timer_ext) {
+        PHJ_HIP(c, hipLaunchKernel(kfn, grid, block, args, lds, c->ks));
+        PHJ_LAUNCHED(c, what);
+        return PHJ_OK;
+    }
+    TimerRec& t = c->timers.back();
+    PHJ_HIP(c, hipExtLaunchKernel(kfn, grid, block, args, lds, c->ks, t.a, t.b, 0));
+    PHJ_LAUNCHED(c, what);
+    if (t.split == 2) c->timers[c->timers.size() - 2].b = t.b;
+    c->last_ev = t.b;   // the kernel's end: later marks may share it
+    c->last_ev_stream = c->ks;
+    c->since_ev = 0;
+    return PHJ_OK;
+}
+
 int timer_end(phj_ctx* c) {
+    if (c->timer_ext) {   // recorded by the launch
+        c->timer_ext = false;
+        return PHJ_OK;
+    }
     if (c->timer_skipped) {
         c->timer_skipped = false;
         return PHJ_OK;
@@ -328,7 +367,23 @@ int timer_begin_split(phj_ctx* c, uint64_t build_bytes, uint64_t probe_bytes) {
     return PHJ_OK;
 }
 
+// timer_begin_split whose events the next launch_ext records (the LDS join's kernel)
+int timer_begin_split_ext(phj_ctx* c, uint64_t build_bytes, uint64_t probe_bytes) {
+    if (!c->tune.timers) return PHJ_OK;
+    if (!c->tune.ext_timers) return timer_begin_split(c, build_bytes, probe_bytes);
+    const hipEvent_t a = next_event(c), b = next_event(c);
+    if (!a || !b) return set_err(c, PHJ_ERR_HIP, "hipEventCreate failed");
+    c->timers.push_back(TimerRec{"build", build_bytes, a, b, 1});
+    c->timers.push_back(TimerRec{"probe", probe_bytes, a, b, 2});
+    c->timer_ext = true;
+    return PHJ_OK;
+}
+
 int timer_end_split(phj_ctx* c) {
+    if (c->timer_ext) {   // recorded by the launch
+        c->timer_ext = false;
+        return PHJ_OK;
+    }
     if (!c->tune.timers) return PHJ_OK;
     PHJ_TRY(mark(c, &c->timers.back().b));
     c->timers[c->timers.size() - 2].b = c->timers.back().b;
@@ -624,7 +679,9 @@ int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const st
         if (a.chunk_cursor == c->p1_cleared) c->p1_cleared = nullptr;   // cleared by the kernel before it
         else if (!zeroed) PHJ_HIP(c, hipMemsetAsync(a.chunk_cursor, 0, chunk_state_bytes(a.nbins), c->ks));
         c->since_ev++;
-        PHJ_TRY(timer_begin(c, sname.c_str(), n * (a.keys_only ? 24 : 32) + (a.out_dig ? n * (a.dig_wide ? 2 : 1) : 0)));
+        const bool p1_prof = c->tune.p1_prof && a.keys_only && c->tune.p1_pipe && BLOCK == 512 && ITEMS == 8 && c->tune.p1_block == 1024;
+        const uint64_t sbytes = n * (a.keys_only ? 24 : 32) + (a.out_dig ? n * (a.dig_wide ? 2 : 1) : 0);
+        PHJ_TRY(p1_prof ? timer_begin(c, sname.c_str(), sbytes) : timer_begin_ext(c, sname.c_str(), sbytes));
         if constexpr (IN_AOS && OUT_AOS && ITEMS <= 8) {
             // persistent: as many workgroups per shard as fit the chip at once
             // (two per CU at 81 KB of LDS), never more than the shard's tiles
@@ -704,8 +761,7 @@ int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const st
                 PHJ_HIP(c, hipMemsetAsync(ak.prof, 0, kP1ProfWords * 8, c->ks));
             }
             void* kargs[] = {&ak, const_cast<uint32_t*>(&ntiles), const_cast<uint32_t*>(&per)};
-            PHJ_HIP(c, hipLaunchKernel(kfn, dim3(slots * a.nshards), dim3(kblock), kargs, lds, c->ks));
-            PHJ_LAUNCHED(c, sname);
+            PHJ_TRY(launch_ext(c, kfn, dim3(slots * a.nshards), dim3(kblock), kargs, lds, sname.c_str()));
             if (prof) {
                 unsigned long long h[kP1ProfWords] = {};
                 PHJ_HIP(c, hipMemcpyAsync(h, ak.prof, sizeof(h), hipMemcpyDeviceToHost, c->ks));
@@ -1592,8 +1648,7 @@ int probe_cluster(phj_ctx* c, const Plan& pl, SideState& PS, int nseg, const int
     const uint32_t want = (PS.nt2 + 7) & ~7u;
     const uint32_t grid = std::max<uint32_t>(8, std::min<uint32_t>(want, static_cast<uint32_t>(per_cu) * c->num_cus) & ~7u);
     void* kargs[] = {&a};
-    PHJ_HIP(c, hipLaunchKernel(kfn, dim3(grid), dim3(B), kargs, lds, c->ks));
-    PHJ_LAUNCHED(c, "k_cluster_probe");
+    PHJ_TRY(launch_ext(c, kfn, dim3(grid), dim3(B), kargs, lds, "k_cluster_probe"));
     if (c->tune.cl_prof) {   // diagnostics (PHJ_CL_PROF): synchronous, to stderr, in microseconds summed over workgroups
         unsigned long long h[kClProfWords] = {};
         PHJ_HIP(c, hipMemcpyAsync(h, a.prof, sizeof(h), hipMemcpyDeviceToHost, c->ks));
@@ -2021,6 +2076,7 @@ int ctx_create_device(int device, phj_ctx** out) {
     c->tune.r_order = std::min(2, std::max(0, env_int("PHJ_R_ORDER", 1)));
     c->tune.count_pin = env_int("PHJ_COUNT_PIN", 1);
     c->tune.p1_tiles1 = env_int("PHJ_P1_TILES1", 0);
+    c->tune.ext_timers = env_int("PHJ_EXT_TIMERS", 0);
     c->tune.r_chunk = env_int("PHJ_R_CHUNK", 1) != 0;
     c->tune.p1_block = env_int("PHJ_P1_BLOCK", 1024) == 512 ? 512 : 1024;
     c->tune.p1_tps = std::max(1, env_int("PHJ_P1_TPS", static_cast<int>(kTilesPerShard)));
@@ -2425,6 +2481,7 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
     c->defer_timers = (p->flags & PHJ_DEFER_TIMERS) != 0;
     c->lean_timers = (p->flags & PHJ_LEAN_TIMERS) != 0;
     c->timer_skipped = false;
+    c->timer_ext = false;
     c->count_pinned = false;
     if (!c->defer_timers || c->timers.size() > kMaxTimerRecs) reset_timers(c);
     if (p->algo == PHJ_ALGO_NO_PARTITIONING) return join_nopart(c, p, r);
@@ -2522,7 +2579,7 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
         PHJ_TRY(phase_mark(&t1));
         // one launch, reported as "build" (the workgroups' table builds in LDS:
         // R's codes read) and "probe" (S's codes read), split by the kernel's own clocks
-        PHJ_TRY(timer_begin_split(c, R.n * 8, S.n * 8));
+        PHJ_TRY(timer_begin_split_ext(c, R.n * 8, S.n * 8));
         if (c->lean_timers && c->tune.timers) {   // build.big not timed: a zero-length record keeps the phase listed
             const hipEvent_t e = c->timers.back().a;
             c->timers.insert(c->timers.end() - 2, TimerRec{"build.big", 0, e, e});

@@ -73,6 +73,7 @@ SCHEDULES = [
     {"PHJ_R_ORDER": "0"},                                       # LDS join: R's pass 1 beside S's
     {"PHJ_R_ORDER": "2"},                                       # ... before it
     {"PHJ_COUNT_PIN": "0"},                                     # LDS join: the count read back by a copy
+    {"PHJ_EXT_TIMERS": "1"},                                    # timers from the kernels' own dispatch (hipExtLaunchKernel)
     {"PHJ_P1_TILES1": "1"},                                     # chunked pass 1: scan and tile lists in one launch
     {"PHJ_P1_TILES1": "1", "PHJ_P1_MIN_TILES": "0"},            # ... whole-tuple chunked pass
     {"PHJ_P1_PROF": "1", "PHJ_CL_PROF": "1"},                   # the phase clocks of pass 1 and of the LDS join's builds
