@@ -70,7 +70,7 @@ def config_params(phj, name):
         "C2: RadixCluster 2-pass 8+8, Murmur3, 10M⋈200M, Zipf s=1.05"
 
 
-def probe_phase(per_step, nR, nS, ms_per_step):
+def probe_phase(per_step, nR, nS, ms_per_step, traffic=None):
     """The north star's probe-phase figure (target >= 60 % of the HBM roofline
     at 1 GPU). SURVEY.md §8(d) prices the probe phase at 16 B per R and per S
     tuple (3.36 GB at 10M⋈200M: >= 60 % means <= 0.70 ms), assuming one fused
@@ -110,6 +110,9 @@ def probe_phase(per_step, nR, nS, ms_per_step):
             "span_ms": span_ms, "frac_survey_def_span": frac(b_def, span_ms),
             "bytes_read": b_read, "achieved_bytes_read": b_read / (ms * 1e-3) / 1e9,
             "frac_bytes_read": frac(b_read, ms),
+            # HBM bytes of the probe kernel's launch from the PMC passes (k_cluster_probe's own
+            # counters; its big-cluster companion is build.big's / not attributed), or null
+            "traffic": (traffic or {}).get("probe"),
             "target_ms_survey_def": b_def / (0.6 * HBM_PEAK_GBS * 1e9) * 1e3,
             "note": ("frac_survey_def is a time target, not a bandwidth: the survey prices the phase at 16 B per "
                      "R and S tuple (a phase that re-reads the tuples); here pass 1 already reduced each tuple to "
@@ -336,11 +339,17 @@ def main():
     # a non-trivial full-size check after the timed region (the default inputs'
     # answer is always |S|): R shifted to [1 + SHIFT, |R| + SHIFT] makes the
     # hottest Zipf keys miss; the join must count exactly the S keys in range
+    # It runs the timed steps' own flags (DEFER|LEAN on one device: the count
+    # polled from pinned host memory, S's chunk state cleared by the previous
+    # join's last workgroup), three joins back to back, then the plain flags
     shift = 3
     generate_shards(ctx, nR, nS, alpha, GEN_SEED, rank, world, start=1 + shift)
     shifted_expect = allsum(ctx.count_in_range(1, 1 + shift, nR))
-    shifted_got = ctx.join(params).matches
-    shifted_ok = shifted_got == shifted_expect and shifted_expect < inrange
+    shifted_runs = [ctx.join(timed_params).matches for _ in range(3)] + [ctx.join(params).matches]
+    if defer:
+        ctx.timers_report()   # (the check's deferred timers are not the bench's)
+    shifted_got = shifted_runs[0]
+    shifted_ok = all(m == shifted_expect for m in shifted_runs) and shifted_expect < inrange
     generate_shards(ctx, nR, nS, alpha, GEN_SEED, rank, world)
 
     if rank == 0:
@@ -349,8 +358,11 @@ def main():
         # own stream beside S, and at N=1 its first timer also spans the wait for
         # the persistent S scatter to free the CUs
         crit = {k: v for k, v in per_step.items() if not k.startswith("R.") and k != "exchange"} or per_step
-        dom_name, (dom_ms, dom_bytes) = max(crit.items(), key=lambda kv: kv[1][0])
-        achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+        if crit:
+            dom_name, (dom_ms, dom_bytes) = max(crit.items(), key=lambda kv: kv[1][0])
+        else:   # no timers recorded (PHJ_TIMERS=0): the roofline is unmeasured
+            dom_name, dom_ms, dom_bytes = None, 0.0, 0
+        achieved = dom_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else None
         value = (nR + nS) * args.steps / elapsed
         out = {
             "metric": "probe+build tuples/sec at 10M⋈200M; achieved HBM GB/s vs roofline, 1/2/4/8 GPU",
@@ -372,14 +384,16 @@ def main():
                        + (" (exchange path)" if exchange and world == 1 else "")},
             "matches": int(matches),
             "expected_matches": inrange,
-            "shifted_check": {"build_start": 1 + shift, "expected": shifted_expect, "matches": shifted_got},
+            "shifted_check": {"build_start": 1 + shift, "expected": shifted_expect, "matches": shifted_got,
+                              "runs": shifted_runs, "flags": int(timed_params.flags), "plain_flags": int(params.flags)},
             "correct": int(matches) == inrange and shifted_ok,
             "exchange_ms": exch / args.steps if exchange else None,
             "roofline": {"bound": "hbm", "kernel": dom_name, "achieved": achieved,
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS if achieved is not None else None,
                          "traffic": traffic.get(dom_name), "algorithmic_bytes": dom_bytes,
                          "ms": dom_ms},
-            "probe_phase": probe_phase(per_step, nR, nS, elapsed * 1e3 / args.steps) if radix else None,
+            "probe_phase": probe_phase(per_step, nR, nS, elapsed * 1e3 / args.steps, traffic) if radix else None,
             "kernels_ms": {k: round(v[0], 4) for k, v in sorted(per_step.items())},
             "kernels_traffic_bytes": {k: int(v) for k, v in sorted(traffic.items())} or None,
         }

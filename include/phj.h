@@ -191,6 +191,22 @@ void phj_shard_range(uint64_t n, int rank, int world, uint64_t *lo, uint64_t *hi
  *    count, or PHJ_ERR_STATE when any rank failed. */
 void phj_exchange_layout(uint64_t max_shard, uint32_t num_partitions, uint64_t *codes_elems,
                          uint64_t *block_elems);
+/* The counting path phj_join takes on one device for params p over a build
+ * side of build_n and a probe side of probe_n rows (default tuning; host
+ * only, no device touched): PHJ_PATH_LDS_JOIN (the clusters' tables built in
+ * LDS, phj_cluster.h), PHJ_PATH_CODE_TABLES (code tables in HBM, the probe
+ * side's pass 2 on chip), PHJ_PATH_PARTITIONED (both sides fully partitioned,
+ * fused or HBM-table join), PHJ_PATH_NO_PARTITIONING; negative: an error code.
+ * The LDS join needs the probe side's keys-only chunked pass 1, whose chunk
+ * pools address slots with 32 bits: above that bound it is declined. Replaces
+ * the choice main() makes between the reference's joins (src/main.cpp:260-276),
+ * refined inside RadixCluster by size. */
+#define PHJ_PATH_NO_PARTITIONING 0
+#define PHJ_PATH_LDS_JOIN 1
+#define PHJ_PATH_CODE_TABLES 2
+#define PHJ_PATH_PARTITIONED 3
+int phj_join_path(const phj_join_params *p, uint64_t build_n, uint64_t probe_n);
+
 /* The segment geometry phj_join's member step uses for radix params p and a
  * global build side of total_build rows (default tuning): the block's codes
  * are grouped by d(c) = (q(c) >> *shift), q = the plan's (sub-)partition
@@ -330,6 +346,15 @@ int phj_probe_pass1(phj_ctx *ctx, const phj_join_params *p, int64_t *keys, uint6
  * PHJ_ERR_STATE (nothing is written through a stale entry) and clears the
  * table; the join after it is exact again. Single-device ctx. */
 int phj_debug_poison_chunk_table(phj_ctx *ctx, int side, const phj_join_params *p, int byte);
+
+/* ---- test hook: poisoned workspace ----
+ * Replaces nothing in the reference. From now on every device buffer the
+ * context (each member of a multi-device or rank context) allocates for its
+ * workspace is filled with `byte` (-1: off) before first use, as memory an
+ * earlier context freed may come back. No join may read a word it did not
+ * write first: the chunk tables, cursors, count pairs and exchange blocks are
+ * cleared or written by the library itself, so every count stays exact. */
+int phj_debug_poison_alloc(phj_ctx *ctx, int byte);
 
 /* ---- test hook: a failing rank ----
  * Replaces nothing in the reference. On a multi-device or rank context, local

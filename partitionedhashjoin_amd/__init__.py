@@ -14,10 +14,12 @@ import ctypes as C
 import numpy as np
 
 from . import _capi
-from ._capi import (ALGO_NO_PARTITIONING, ALGO_RADIX, CTX_EXCHANGE, CTX_LOCAL, HASH_MURMUR3, HASH_XXH3, SIDE_BUILD,
+from ._capi import (ALGO_NO_PARTITIONING, ALGO_RADIX, CTX_EXCHANGE, CTX_LOCAL, HASH_MURMUR3, HASH_XXH3,
+                    PATH_CODE_TABLES, PATH_LDS_JOIN, PATH_NO_PARTITIONING, PATH_PARTITIONED, SIDE_BUILD,
                     SIDE_PROBE, JoinParams, JoinResult, Partitioned, PhjError)
 
-__all__ = ["Context", "shard_range", "exchange_layout", "count_contribution", "count_verdict", "comm_unique_id", "CTX_EXCHANGE", "CTX_LOCAL", "radix_params", "nopart_params", "JoinParams", "JoinResult",
+__all__ = ["Context", "shard_range", "exchange_layout", "join_path", "PATH_LDS_JOIN", "PATH_CODE_TABLES",
+           "PATH_PARTITIONED", "PATH_NO_PARTITIONING", "count_contribution", "count_verdict", "comm_unique_id", "CTX_EXCHANGE", "CTX_LOCAL", "radix_params", "nopart_params", "JoinParams", "JoinResult",
            "Partitioned", "PhjError", "ALGO_RADIX", "ALGO_NO_PARTITIONING", "HASH_XXH3",
            "HASH_MURMUR3", "SIDE_BUILD", "SIDE_PROBE", "DEFAULT_SEED"]
 
@@ -87,6 +89,16 @@ def exchange_geometry(params: JoinParams, total_build: int):
     if rc != 0:
         raise PhjError(rc, "phj_exchange_geometry: radix params required")
     return n.value, sh.value, sb.value, ss.value, bool(cl.value)
+
+
+def join_path(params: JoinParams, build_n: int, probe_n: int) -> int:
+    """The counting path phj_join takes on one device (phj_join_path; host
+    only, default tuning): PATH_LDS_JOIN, PATH_CODE_TABLES, PATH_PARTITIONED
+    or PATH_NO_PARTITIONING."""
+    rc = _capi.load().phj_join_path(C.byref(params), build_n, probe_n)
+    if rc < 0:
+        raise PhjError(rc, "phj_join_path: bad params")
+    return rc
 
 
 def count_contribution(count: int, failed: bool = False) -> np.ndarray:
@@ -303,6 +315,12 @@ class Context:
         """Test hook (phj_debug_poison_chunk_table): leave `side`'s chunk table
         as a stale one would be (every byte = `byte`, marked clean)."""
         self._check(self._L.phj_debug_poison_chunk_table(self._h, side, C.byref(params), byte))
+
+    def debug_poison_alloc(self, byte: int = 0xFF) -> None:
+        """Test hook (phj_debug_poison_alloc): every workspace buffer this
+        context (and each of its members) allocates from now on is filled with
+        `byte` (-1: off), so a read of a word nothing wrote shows."""
+        self._check(self._L.phj_debug_poison_alloc(self._h, byte))
 
     def debug_fail_member(self, member: int) -> None:
         """Test hook (phj_debug_fail_member): local member `member` fails the

@@ -38,13 +38,14 @@ EXPORTED = [
     "phj_partitioned_download", "phj_hash_keys", "phj_timers_report", "phj_join_partitioned_async",
     "phj_prepare", "phj_join_materialize", "phj_joined_rows", "phj_joined_download",
     "phj_ctx_create_ex", "phj_ctx_create_device", "phj_comm_unique_id", "phj_ctx_create_rank",
-    "phj_ctx_info", "phj_shard_range", "phj_probe_pass1", "phj_debug_poison_chunk_table", "phj_debug_fail_member", "phj_debug_exchange_block", "phj_exchange_geometry",
-    "phj_exchange_layout", "phj_count_contribution", "phj_count_verdict",
+    "phj_ctx_info", "phj_shard_range", "phj_probe_pass1", "phj_debug_poison_chunk_table", "phj_debug_poison_alloc", "phj_debug_fail_member", "phj_debug_exchange_block", "phj_exchange_geometry",
+    "phj_exchange_layout", "phj_count_contribution", "phj_count_verdict", "phj_join_path",
 ]
 ABI_VERSION = 2
 CTX_EXCHANGE = 0x1   # phj_ctx_create_ex: the multi-GPU path on one device (RCCL world of one)
 CTX_LOCAL = 0x2      # ... exchange by device copies; devices may repeat (rehearsal on one GPU)
 UNIQUE_ID_BYTES = 128
+PATH_NO_PARTITIONING, PATH_LDS_JOIN, PATH_CODE_TABLES, PATH_PARTITIONED = 0, 1, 2, 3   # phj_join_path
 
 
 class Tuple(C.Structure):
@@ -116,6 +117,7 @@ def load():
         "phj_exchange_layout": (None, [u64, C.c_uint32, C.POINTER(u64), C.POINTER(u64)]),
         "phj_count_contribution": (None, [u64, i, C.POINTER(u64)]),
         "phj_count_verdict": (i, [C.POINTER(u64), C.POINTER(u64)]),
+        "phj_join_path": (i, [C.POINTER(JoinParams), u64, u64]),
         "phj_ctx_destroy": (None, [P]),
         "phj_last_error": (C.c_char_p, [P]),
         "phj_ctx_set_stream": (i, [P, P]),
@@ -135,6 +137,7 @@ def load():
         "phj_hash_keys": (i, [P, i, u64, P, u64, P]),
         "phj_probe_pass1": (i, [P, P, P, u64, P, P, P]),
         "phj_debug_poison_chunk_table": (i, [P, i, P, i]),
+        "phj_debug_poison_alloc": (i, [P, i]),
         "phj_debug_fail_member": (i, [P, i]),
         "phj_debug_exchange_block": (i, [P, i, P, u64]),
         "phj_exchange_geometry": (i, [P, u64, P, P, P, P, P]),

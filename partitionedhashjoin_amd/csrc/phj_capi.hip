@@ -8,7 +8,6 @@
 // once (grow-only) before the timed region; phases are timed with hipEvents
 // on the same stream. Errors never cross the ABI as exceptions: they become
 // negative status codes plus a message (phj_last_error).
-#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -20,6 +19,15 @@
 #include <string>
 #include <unordered_map>
 #include <vector>
+
+// Measurement builds only (scripts/ab_lib.sh, `make prof-lib`): the phase-clock
+// forms of S's pass 1 and of the LDS join's builds, printed to stderr per join.
+#ifndef PHJ_P1_PROF
+#define PHJ_P1_PROF 0
+#endif
+#ifndef PHJ_CL_PROF
+#define PHJ_CL_PROF 0
+#endif
 
 #include "../../include/phj.h"
 #include "phj_cluster.h"
@@ -62,19 +70,11 @@ struct Tuning {
     int p1_pipe = 1;      // keys-only pass 1: claims resolved a tile later over pre-allocated chunks (k_chunk_codes_pipe)
     int r_chunk = 1;      // LDS join on one device: R through the chunked code pass, read by tiles ("tile mode")
     int count_pin = 1;    // LDS join: the last workgroup writes the count to pinned host memory (0: a copy back)
-    int ext_timers = 0;   // 1: the large kernels' timers from their own dispatch (hipExtLaunchKernel events; measured no faster)
-    int p1_tiles1 = 0;    // 1: chunked pass 1's scan + tile lists in one launch (k_chunk_tiles: measured slower, 32 vs 17 us at C2)
     int r_order = 1;      // LDS join: R's pass 1 beside S's (0), after it (1: measured C2 1.69 vs 1.72 ms, S.p1 1.05 vs 1.19), before it (2)
-    int p1_kpf = 2;       // ... 1024 x 4: tiles of keys in flight ahead of the one hashed (1 or 2; 2 measured 1.08 -> 1.05 ms)
-    int p1_prof = 0;      // PHJ_P1_PROF: the pipelined pass 1's phases to stderr (diagnostics)
-    int cl_cnt = 1;       // ... tables built by bucket fill counters (k_cluster_probe CNT; measured build 0.082 -> 0.055 ms at C2)
-    int cl_prof = 0;      // PHJ_CL_PROF: the LDS join's build sections to stderr (diagnostics)
     int p1_block = 1024;  // ... its workgroup: 1024 x 4 codes (16 waves per CU; measured 1.20 -> 1.07 ms at C2) or 512 x 8, the same tile
     int cluster = 1;      // radix join: LDS cluster tables (phj_cluster.h) when the build side's clusters fit
     int cl_cap = static_cast<int>(kClCapMax);   // ... LDS table slots (8192: two workgroups per CU, 16384: one)
     int cl_bits = 0;      // ... clusters = 2^cl_bits (0: the fewest >= 256 whose average fits the table)
-    int cl_pf = 3;        // ... probe: register buffers of tile codes (1-3): PF - 1 tiles in flight beside the one probed
-    bool cl_pre = true;   // ... probe: the next cluster's R codes prefetched during this cluster's tiles
 };
 
 int env_int(const char* name, int dflt) {
@@ -186,7 +186,6 @@ struct phj_ctx {
     bool defer_timers = false;  // the running join has PHJ_DEFER_TIMERS: its timers stay for phj_timers_report
     bool lean_timers = false;   // PHJ_LEAN_TIMERS: the build side's timers are not recorded
     bool timer_skipped = false; // the open timer was not recorded (timer_end records nothing)
-    bool timer_ext = false;     // the open timer's events come from the next launch_ext (timer_end records nothing)
     // the next chunked pass-1 bookkeeping kernel also clears this chunk state
     // (the LDS join: R's, cleared by S's k_pass1_finish_sizes on the same
     // stream), and the pass whose state p1_cleared names skips its memset
@@ -200,6 +199,7 @@ struct phj_ctx {
     size_t s_zeroed_bytes = 0;
     void* s_zero_pending = nullptr;
     size_t s_zero_pending_bytes = 0;
+    int poison = -1;   // phj_debug_poison_alloc: every new workspace buffer is filled with this byte
 };
 
 namespace {
@@ -249,6 +249,10 @@ int ensure(phj_ctx* c, DevBuf& b, size_t bytes) {
         return set_err(c, PHJ_ERR_NOMEM, "hipMalloc(" + std::to_string(rounded) + "): " + hipGetErrorString(e));
     }
     b.bytes = rounded;
+    if (c->poison >= 0) {   // (test hook) no buffer may be read before it is written
+        PHJ_HIP(c, hipMemsetAsync(b.p, c->poison, rounded, c->stream));
+        PHJ_HIP(c, hipStreamSynchronize(c->stream));
+    }
     return PHJ_OK;
 }
 
@@ -314,43 +318,14 @@ int timer_begin(phj_ctx* c, const char* name, uint64_t bytes) {
     return PHJ_OK;
 }
 
-// A timer whose events the kernel's own dispatch records (launch_ext): no
-// marker packet before or after the kernel (each delays the next kernel ~4 us).
-int timer_begin_ext(phj_ctx* c, const char* name, uint64_t bytes) {
-    if (!c->tune.timers) return PHJ_OK;
-    if (!c->tune.ext_timers) return timer_begin(c, name, bytes);
-    c->timer_skipped = c->lean_timers && (std::strncmp(name, "R.", 2) == 0 || std::strcmp(name, "build.big") == 0);
-    if (c->timer_skipped) return PHJ_OK;
-    TimerRec t{name, bytes, next_event(c), next_event(c)};
-    if (!t.a || !t.b) return set_err(c, PHJ_ERR_HIP, "hipEventCreate failed");
-    c->timers.push_back(t);
-    c->timer_ext = true;
-    return PHJ_OK;
-}
-
-// Launch kfn; after timer_begin_ext (or timer_begin_split_ext) its events are
-// the open timer's (or the split pair's) start and stop.
-int launch_ext(phj_ctx* c, const void* kfn, dim3 grid, dim3 block, void** args, size_t lds, const char* what) {
-    if (!c->timer_ext) {
-        PHJ_HIP(c, hipLaunchKernel(kfn, grid, block, args, lds, c->ks));
-        PHJ_LAUNCHED(c, what);
-        return PHJ_OK;
-    }
-    TimerRec& t = c->timers.back();
-    PHJ_HIP(c, hipExtLaunchKernel(kfn, grid, block, args, lds, c->ks, t.a, t.b, 0));
+// Launch kfn on the current launch stream.
+int launch_kernel(phj_ctx* c, const void* kfn, dim3 grid, dim3 block, void** args, size_t lds, const char* what) {
+    PHJ_HIP(c, hipLaunchKernel(kfn, grid, block, args, lds, c->ks));
     PHJ_LAUNCHED(c, what);
-    if (t.split == 2) c->timers[c->timers.size() - 2].b = t.b;
-    c->last_ev = t.b;   // the kernel's end: later marks may share it
-    c->last_ev_stream = c->ks;
-    c->since_ev = 0;
     return PHJ_OK;
 }
 
 int timer_end(phj_ctx* c) {
-    if (c->timer_ext) {   // recorded by the launch
-        c->timer_ext = false;
-        return PHJ_OK;
-    }
     if (c->timer_skipped) {
         c->timer_skipped = false;
         return PHJ_OK;
@@ -367,23 +342,7 @@ int timer_begin_split(phj_ctx* c, uint64_t build_bytes, uint64_t probe_bytes) {
     return PHJ_OK;
 }
 
-// timer_begin_split whose events the next launch_ext records (the LDS join's kernel)
-int timer_begin_split_ext(phj_ctx* c, uint64_t build_bytes, uint64_t probe_bytes) {
-    if (!c->tune.timers) return PHJ_OK;
-    if (!c->tune.ext_timers) return timer_begin_split(c, build_bytes, probe_bytes);
-    const hipEvent_t a = next_event(c), b = next_event(c);
-    if (!a || !b) return set_err(c, PHJ_ERR_HIP, "hipEventCreate failed");
-    c->timers.push_back(TimerRec{"build", build_bytes, a, b, 1});
-    c->timers.push_back(TimerRec{"probe", probe_bytes, a, b, 2});
-    c->timer_ext = true;
-    return PHJ_OK;
-}
-
 int timer_end_split(phj_ctx* c) {
-    if (c->timer_ext) {   // recorded by the launch
-        c->timer_ext = false;
-        return PHJ_OK;
-    }
     if (!c->tune.timers) return PHJ_OK;
     PHJ_TRY(mark(c, &c->timers.back().b));
     c->timers[c->timers.size() - 2].b = c->timers.back().b;
@@ -655,12 +614,12 @@ int scan_u32(phj_ctx* c, uint32_t* data, uint32_t len, uint32_t narrays, uint32_
 
 
 // The pipelined code pass in 1024 x 4 workgroups: KPF tiles of keys in
-// flight (1 or 2); the phase-clock form (PHJ_P1_PROF) at KPF 2.
+// flight (S: 2, measured 1.08 -> 1.05 ms at C2; R: 1); a measurement build
+// (-DPHJ_P1_PROF=1, scripts/ab_lib.sh) runs S's pass in the phase-clock form.
 template <int HK, int DPT>
-const void* pipe1024(int kpf, bool prof) {
-    if (prof) return reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, HK, DPT, 0, true, 2>);
-    return kpf == 1 ? reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, HK, DPT, 0, false, 1>)
-                    : reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, HK, DPT, 0, false, 2>);
+const void* pipe1024(int kpf) {
+    if (kpf == 1) return reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, HK, DPT, 0, false, 1>);
+    return reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, HK, DPT, 0, PHJ_P1_PROF != 0, 2>);
 }
 
 template <int BLOCK, int ITEMS, bool IN_AOS, bool OUT_AOS>
@@ -679,9 +638,8 @@ int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const st
         if (a.chunk_cursor == c->p1_cleared) c->p1_cleared = nullptr;   // cleared by the kernel before it
         else if (!zeroed) PHJ_HIP(c, hipMemsetAsync(a.chunk_cursor, 0, chunk_state_bytes(a.nbins), c->ks));
         c->since_ev++;
-        const bool p1_prof = c->tune.p1_prof && a.keys_only && c->tune.p1_pipe && BLOCK == 512 && ITEMS == 8 && c->tune.p1_block == 1024;
         const uint64_t sbytes = n * (a.keys_only ? 24 : 32) + (a.out_dig ? n * (a.dig_wide ? 2 : 1) : 0);
-        PHJ_TRY(p1_prof ? timer_begin(c, sname.c_str(), sbytes) : timer_begin_ext(c, sname.c_str(), sbytes));
+        PHJ_TRY(timer_begin(c, sname.c_str(), sbytes));
         if constexpr (IN_AOS && OUT_AOS && ITEMS <= 8) {
             // persistent: as many workgroups per shard as fit the chip at once
             // (two per CU at 81 KB of LDS), never more than the shard's tiles
@@ -702,10 +660,9 @@ int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const st
                         // R's pass (LDS join, tile mode: ~10 tiles per workgroup at C2)
                         // keeps one tile in flight, which also gives it a kernel name of
                         // its own in rocprof summaries (S's is the roofline kernel)
-                        const int kpf = prefix.rfind("R.", 0) == 0 ? 1 : c->tune.p1_kpf;
-                        const bool pr = c->tune.p1_prof != 0;
-                        kfn = hk == kMurmur3 ? (dpt == 4 ? pipe1024<kMurmur3, 2>(kpf, pr) : pipe1024<kMurmur3, 1>(kpf, pr))
-                                             : (dpt == 4 ? pipe1024<kXXH3, 2>(kpf, pr) : pipe1024<kXXH3, 1>(kpf, pr));
+                        const int kpf = prefix.rfind("R.", 0) == 0 ? 1 : 2;
+                        kfn = hk == kMurmur3 ? (dpt == 4 ? pipe1024<kMurmur3, 2>(kpf) : pipe1024<kMurmur3, 1>(kpf))
+                                             : (dpt == 4 ? pipe1024<kXXH3, 2>(kpf) : pipe1024<kXXH3, 1>(kpf));
                     } else if (hk == kMurmur3)
                         kfn = dpt == 4 ? reinterpret_cast<const void*>(&k_chunk_codes_pipe<BLOCK, ITEMS, kMurmur3, 4>)
                             : dpt == 2 ? reinterpret_cast<const void*>(&k_chunk_codes_pipe<BLOCK, ITEMS, kMurmur3, 2>)
@@ -754,14 +711,14 @@ int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const st
             if (c->tune.p1_slots > 0) slots = std::min<uint32_t>(per, c->tune.p1_slots);
             if (c->tune.p1_slots < 0) slots = per;   // one tile per workgroup
             PassArgs ak = a;
-            const bool prof = pipe && c->tune.p1_prof && kblock == 1024;
-            if (prof) {   // diagnostics (PHJ_P1_PROF): synchronous, to stderr
+            const bool prof = PHJ_P1_PROF && pipe && kblock == 1024 && prefix.rfind("R.", 0) != 0;
+            if (prof) {   // diagnostics (measurement build, PHJ_P1_PROF): synchronous, to stderr
                 PHJ_TRY(ensure(c, c->cl_prof, 64 * 8));   // words 32.. (the LDS join's are 0..)
                 ak.prof = static_cast<unsigned long long*>(c->cl_prof.p) + 32;
                 PHJ_HIP(c, hipMemsetAsync(ak.prof, 0, kP1ProfWords * 8, c->ks));
             }
             void* kargs[] = {&ak, const_cast<uint32_t*>(&ntiles), const_cast<uint32_t*>(&per)};
-            PHJ_TRY(launch_ext(c, kfn, dim3(slots * a.nshards), dim3(kblock), kargs, lds, sname.c_str()));
+            PHJ_TRY(launch_kernel(c, kfn, dim3(slots * a.nshards), dim3(kblock), kargs, lds, sname.c_str()));
             if (prof) {
                 unsigned long long h[kP1ProfWords] = {};
                 PHJ_HIP(c, hipMemcpyAsync(h, ak.prof, sizeof(h), hipMemcpyDeviceToHost, c->ks));
@@ -859,6 +816,35 @@ int launch_pass(phj_ctx* c, int hk, bool in_aos, bool out_aos, PassArgs a, uint3
 #undef PHJ_PASS_CASES
 }
 
+// Whether partition_state takes the chunked pass 1 for n tuples under plan pl
+// (ko: the keys-only code form of the counting joins). Chunked pass 1
+// (unordered partitions, tile kernels): pass-1 chunks are the pass-2 tiles,
+// every digit's run of a tile fits one workgroup thread (nb1 <= block) and
+// spans at most two chunks (tile1 == tile2), and every pool slot of the
+// shards' pools is a uint32 (the pool bound below).
+// Measured: it pays at 200M tuples (16 chains per digit) and
+// loses to the stable pass below ~100M, where fewer shards (more
+// workgroups per cursor line) or more partial chunks cost more than the
+// histogram read saves; so it starts at p1_min_tiles tiles. The keys-only
+// form for the on-chip probe (half the bytes, three workgroups per CU)
+// wins at every size measured (25M-200M), with shards of p1_ko_tps tiles.
+// use_cluster asks the same of the probe side (the LDS join needs S's codes).
+bool chunked_pass1(const phj_ctx* c, const Plan& pl, uint64_t n64, bool ko) {
+    if (pl.npass != 2 || pl.stable || !c->tune.p1_chunk || n64 == 0 || n64 >= (1ull << 32) - 2 * 4096) return false;
+    const uint64_t n = n64;
+    const TileShape sh = tile_shape(c, pl.nb1);
+    const uint32_t tile = sh.tile;
+    if (tile != tile_shape(c, pl.nb2).tile) return false;
+    if (!ko && (n + tile - 1) / tile < static_cast<uint64_t>(c->tune.p1_min_tiles)) return false;
+    if (pl.nb1 > static_cast<uint32_t>(sh.block) * (ko && sh.block == 512 && tile == 4096 ? 4u : 1u)) return false;
+    if (tile / sh.block > 8) return false;   // registers: the next tile is prefetched
+    if ((3 * (n / tile + kShards) + kShards * pl.nb1) * tile >= (1ull << 32)) return false;
+    const bool pipe = ko && c->tune.p1_pipe && sh.block == 512 && tile == 4096;
+    // the pipelined code pass's pool (pipe_pool_stride per shard)
+    if (pipe && ((kPipeRes + 1) * (n / tile + kShards) + kShards * (3ull * pl.nb1 + 1)) * tile >= (1ull << 32)) return false;
+    return true;
+}
+
 int partition_state(phj_ctx* c, SideState& S, const char* tag, const Plan& pl, bool p1_only,
                     unsigned long long* zero = nullptr, uint32_t max_shards = kShards) {
     c->scan_scratch = &S.partials;
@@ -884,14 +870,7 @@ int partition_state(phj_ctx* c, SideState& S, const char* tag, const Plan& pl, b
     // form for the on-chip probe (half the bytes, three workgroups per CU)
     // wins at every size measured (25M-200M), with shards of p1_ko_tps tiles.
     const bool ko = p1_only;
-    const bool chunked = pl.npass == 2 && !pl.stable && c->tune.p1_chunk && (dcol || p1_only) && p1_aos && n > 0 &&
-                         (ko || nt1 >= static_cast<uint32_t>(c->tune.p1_min_tiles)) &&
-                         tile == tile2 &&
-                         pl.nb1 <= static_cast<uint32_t>(tile_shape(c, pl.nb1).block) * (ko && tile_shape(c, pl.nb1).block == 512 && tile == 4096 ? 4u : 1u) &&
-                         tile / tile_shape(c, pl.nb1).block <= 8 &&   // registers: the next tile is prefetched
-                         (3 * (static_cast<uint64_t>(n) / tile + kShards) + kShards * pl.nb1) * tile < (1ull << 32) &&
-                         (!p1_only || !c->tune.p1_pipe || tile_shape(c, pl.nb1).block != 512 || tile != 4096 ||
-                          ((kPipeRes + 1) * (static_cast<uint64_t>(n) / tile + kShards) + kShards * (3ull * pl.nb1 + 1)) * tile < (1ull << 32));
+    const bool chunked = chunked_pass1(c, pl, n64, ko);
     S.hcoded = chunked && ko;   // k_chunk_codes
     // chains per digit: ~kTilesPerShard tiles each, a power of two <= kShards
     // (max_shards < kShards: R in tile mode takes exactly that many, so a
@@ -987,14 +966,7 @@ int partition_state(phj_ctx* c, SideState& S, const char* tag, const Plan& pl, b
             c->p1_cleared = c->p1_clear;
             c->p1_clear = nullptr;
         }
-        if (c->tune.p1_tiles1) {   // with the tile lists below, one launch
-            uint32_t* ts = static_cast<uint32_t*>(S.tstart.p);
-            hipLaunchKernelGGL(k_chunk_tiles, dim3(pl.nb1), dim3(kBlock), 0, c->ks, a.chunk_cursor, pl.nb1, nshards, n, tile2,
-                               static_cast<uint32_t*>(S.bounds1.p), tb2, static_cast<unsigned long long*>(S.ctab.p), maxch,
-                               pool_stride, static_cast<uint32_t*>(S.tseg2.p), ts, ts + nt2max, zero, clr,
-                               static_cast<uint32_t>(c->p1_clear_bytes / 16));
-            PHJ_LAUNCHED(c, "k_chunk_tiles");
-        } else {
+        {
             hipLaunchKernelGGL(k_pass1_finish_sizes, dim3(1), dim3(kFinSizesBlock), 0, c->ks, a.chunk_cursor, pl.nb1, nshards, n, tile2,
                                static_cast<uint32_t*>(S.bounds1.p), tb2, zero, clr, static_cast<uint32_t>(c->p1_clear_bytes / 16));
             PHJ_LAUNCHED(c, "k_pass1_finish_sizes");
@@ -1024,7 +996,7 @@ int partition_state(phj_ctx* c, SideState& S, const char* tag, const Plan& pl, b
             if (chunked) {
                 uint32_t* ts = static_cast<uint32_t*>(S.tstart.p);
                 uint32_t* tc = ts + nt2max;
-                if (!c->tune.p1_tiles1) {   // (else written by k_chunk_tiles above)
+                {
                     hipLaunchKernelGGL(k_tile_chunks, dim3((pl.nb1 * nshards + kWaves - 1) / kWaves), dim3(kBlock), 0, c->ks, tb2,
                                        static_cast<uint32_t*>(S.ccur.p), pl.nb1, nshards,
                                        static_cast<unsigned long long*>(S.ctab.p), maxch, pool_stride, tile2,
@@ -1444,8 +1416,11 @@ bool use_p2probe(const phj_ctx* c, const Plan& pl, uint64_t nS, uint64_t nR) {
 
 // phj_join takes the LDS join (phj_cluster.h) when the plan's clusters fit:
 // out = the cluster plan. Needs the keys-only chunked pass 1 (512 x 4096 tiles).
+// nS: the probe side (0: not known yet, e.g. the exchange geometry); it must
+// take the keys-only chunked pass 1 under the cluster plan, else (a probe side
+// above the pool's uint32 slot bound, ~2^32 / (kPipeRes + 1) codes per device)
+// the join takes the stable pass 1 and the code tables (use_p2probe).
 bool use_cluster(const phj_ctx* c, const Plan& pl, uint64_t nS, uint64_t nR, Plan& out) {
-    (void)nS;
     if (!c->tune.p1_chunk || pl.stable) return false;
     if (!cluster_plan(c, pl, nR, out)) return false;
     // the chunked pass 1 runs on 512 x 4096 tiles for both of the plan's digit counts
@@ -1453,6 +1428,7 @@ bool use_cluster(const phj_ctx* c, const Plan& pl, uint64_t nS, uint64_t nR, Pla
         const TileShape sh = tile_shape(c, nb);
         if (sh.tile != 4096 || sh.block != 512) return false;
     }
+    if (nS > 0 && !chunked_pass1(c, out, nS, true)) return false;
     return cluster_empty0(out) != 0 && 4 * nR + 2ull * out.nb1 < (1ull << 32);
 }
 
@@ -1618,29 +1594,18 @@ int probe_cluster(phj_ctx* c, const Plan& pl, SideState& PS, int nseg, const int
         c->split_words = a.split;
     }
     constexpr int B = kClBlock, I = kClItems;
-    const size_t lds = static_cast<size_t>(a.cap) * (c->tune.cl_cnt ? 9 : 8);
-    if (c->tune.cl_prof) {
+    const size_t lds = static_cast<size_t>(a.cap) * 9;   // the table + its 16-bit bucket fill counters
+    constexpr bool PR = PHJ_CL_PROF != 0;   // measurement build: the builds' section clocks
+    if (PR) {
         PHJ_TRY(ensure(c, c->cl_prof, 64 * 8));
         a.prof = static_cast<unsigned long long*>(c->cl_prof.p);
         PHJ_HIP(c, hipMemsetAsync(a.prof, 0, kClProfWords * 8, c->ks));
     }
-    // (table builds by fill counters: every prefetch form; by compare-and-swap:
-    // the default form, for comparison)
-    const bool pre = c->tune.cl_pre, pr = c->tune.cl_prof != 0;
-    const int pf = c->tune.cl_pf;
-    // (tile mode, R read by its pass-1 tiles: the default form and the
-    // compare-and-swap and clock forms; segment mode: every form)
-    const void* kfn = RT ? (!c->tune.cl_cnt ? reinterpret_cast<const void*>(&k_cluster_probe<B, I, 3, true, false, false, true>)
-                            : pr           ? reinterpret_cast<const void*>(&k_cluster_probe<B, I, 3, true, true, true, true>)
-                            : pf == 3      ? reinterpret_cast<const void*>(&k_cluster_probe<B, I, 3, true, false, true, true>)
-                                           : reinterpret_cast<const void*>(&k_cluster_probe<B, I, 2, true, false, true, true>))
-                      : !c->tune.cl_cnt ? (pr ? reinterpret_cast<const void*>(&k_cluster_probe<B, I, 3, true, true, false>)
-                                            : reinterpret_cast<const void*>(&k_cluster_probe<B, I, 3, true, false, false>))
-                      : pr            ? reinterpret_cast<const void*>(&k_cluster_probe<B, I, 3, true, true, true>)
-                      : !pre          ? reinterpret_cast<const void*>(&k_cluster_probe<B, I, 2, false, false, true>)
-                      : pf == 2       ? reinterpret_cast<const void*>(&k_cluster_probe<B, I, 2, true, false, true>)
-                      : pf == 3       ? reinterpret_cast<const void*>(&k_cluster_probe<B, I, 3, true, false, true>)
-                                      : reinterpret_cast<const void*>(&k_cluster_probe<B, I, 1, true, false, true>);
+    // three tiles of codes in flight, the next cluster's R codes prefetched
+    // (measured: one / two tiles 0.406 / 0.360 ms against 0.355 at C2; tables by
+    // 64-bit compare-and-swap 0.082 ms of builds against 0.055 by fill counters)
+    const void* kfn = RT ? reinterpret_cast<const void*>(&k_cluster_probe<B, I, 3, true, PR, true>)
+                         : reinterpret_cast<const void*>(&k_cluster_probe<B, I, 3, true, PR, false>);
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, B, lds) != hipSuccess || per_cu < 1) per_cu = 1;
     per_cu = std::max(1, std::min<int>(per_cu, static_cast<int>(160 * 1024 / (lds + 256))));
@@ -1648,8 +1613,8 @@ int probe_cluster(phj_ctx* c, const Plan& pl, SideState& PS, int nseg, const int
     const uint32_t want = (PS.nt2 + 7) & ~7u;
     const uint32_t grid = std::max<uint32_t>(8, std::min<uint32_t>(want, static_cast<uint32_t>(per_cu) * c->num_cus) & ~7u);
     void* kargs[] = {&a};
-    PHJ_TRY(launch_ext(c, kfn, dim3(grid), dim3(B), kargs, lds, "k_cluster_probe"));
-    if (c->tune.cl_prof) {   // diagnostics (PHJ_CL_PROF): synchronous, to stderr, in microseconds summed over workgroups
+    PHJ_TRY(launch_kernel(c, kfn, dim3(grid), dim3(B), kargs, lds, "k_cluster_probe"));
+    if (PR) {   // diagnostics (measurement build): synchronous, to stderr, in microseconds summed over workgroups
         unsigned long long h[kClProfWords] = {};
         PHJ_HIP(c, hipMemcpyAsync(h, a.prof, sizeof(h), hipMemcpyDeviceToHost, c->ks));
         PHJ_HIP(c, hipStreamSynchronize(c->ks));
@@ -2064,19 +2029,11 @@ int ctx_create_device(int device, phj_ctx** out) {
     c->tune.p1_pipe = env_int("PHJ_P1_PIPE", 1) != 0;
     c->tune.cl_cap = env_int("PHJ_CL_CAP", static_cast<int>(kClCapMax)) == 8192 ? 8192 : static_cast<int>(kClCapMax);
     c->tune.cl_bits = std::max(0, std::min(kMaxDigitBits, env_int("PHJ_CL_BITS", 0)));
-    c->tune.cl_pf = std::max(1, std::min(3, env_int("PHJ_CL_PF", 3)));
-    c->tune.cl_pre = env_int("PHJ_CL_PRE", 1) != 0;
     c->tune.p2probe = env_int("PHJ_P2PROBE", 1);
     c->tune.p1_slots = env_int("PHJ_P1_SLOTS", 0);
     c->tune.p1_wpc2 = std::max(0, env_int("PHJ_P1_WPC2", 2));
-    c->tune.cl_prof = env_int("PHJ_CL_PROF", 0);
-    c->tune.cl_cnt = env_int("PHJ_CL_CNT", 1);
-    c->tune.p1_prof = env_int("PHJ_P1_PROF", 0);
-    c->tune.p1_kpf = env_int("PHJ_P1_KPF", 2) == 1 ? 1 : 2;
     c->tune.r_order = std::min(2, std::max(0, env_int("PHJ_R_ORDER", 1)));
     c->tune.count_pin = env_int("PHJ_COUNT_PIN", 1);
-    c->tune.p1_tiles1 = env_int("PHJ_P1_TILES1", 0);
-    c->tune.ext_timers = env_int("PHJ_EXT_TIMERS", 0);
     c->tune.r_chunk = env_int("PHJ_R_CHUNK", 1) != 0;
     c->tune.p1_block = env_int("PHJ_P1_BLOCK", 1024) == 512 ? 512 : 1024;
     c->tune.p1_tps = std::max(1, env_int("PHJ_P1_TPS", static_cast<int>(kTilesPerShard)));
@@ -2170,6 +2127,18 @@ void phj_exchange_layout(uint64_t max_shard, uint32_t num_partitions, uint64_t* 
     const uint64_t cap = (max_shard + 63) / 64 * 64;   // both columns stay 16-B aligned in the gathered buffer
     if (codes_elems) *codes_elems = cap;
     if (block_elems) *block_elems = cap + (static_cast<uint64_t>(num_partitions) + 2) / 2;
+}
+
+int phj_join_path(const phj_join_params* p, uint64_t build_n, uint64_t probe_n) {
+    if (!p) return PHJ_ERR_INVALID;
+    if (p->algo == PHJ_ALGO_NO_PARTITIONING) return PHJ_PATH_NO_PARTITIONING;
+    if (p->algo != PHJ_ALGO_RADIX) return PHJ_ERR_INVALID;
+    phj_ctx tmp;   // default tuning (no device is touched)
+    Plan pl, cpl;
+    if (make_plan(&tmp, p, pl) != PHJ_OK) return PHJ_ERR_INVALID;
+    if (use_cluster(&tmp, pl, probe_n, build_n, cpl)) return PHJ_PATH_LDS_JOIN;
+    refine_plan(&tmp, pl, build_n);
+    return use_p2probe(&tmp, pl, probe_n, build_n) ? PHJ_PATH_CODE_TABLES : PHJ_PATH_PARTITIONED;
 }
 
 int phj_exchange_geometry(const phj_join_params* p, uint64_t total_build, uint32_t* num_segments, uint32_t* shift,
@@ -2481,7 +2450,6 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
     c->defer_timers = (p->flags & PHJ_DEFER_TIMERS) != 0;
     c->lean_timers = (p->flags & PHJ_LEAN_TIMERS) != 0;
     c->timer_skipped = false;
-    c->timer_ext = false;
     c->count_pinned = false;
     if (!c->defer_timers || c->timers.size() > kMaxTimerRecs) reset_timers(c);
     if (p->algo == PHJ_ALGO_NO_PARTITIONING) return join_nopart(c, p, r);
@@ -2579,7 +2547,7 @@ int phj_join(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
         PHJ_TRY(phase_mark(&t1));
         // one launch, reported as "build" (the workgroups' table builds in LDS:
         // R's codes read) and "probe" (S's codes read), split by the kernel's own clocks
-        PHJ_TRY(timer_begin_split_ext(c, R.n * 8, S.n * 8));
+        PHJ_TRY(timer_begin_split(c, R.n * 8, S.n * 8));
         if (c->lean_timers && c->tune.timers) {   // build.big not timed: a zero-length record keeps the phase listed
             const hipEvent_t e = c->timers.back().a;
             c->timers.insert(c->timers.end() - 2, TimerRec{"build.big", 0, e, e});
@@ -2909,6 +2877,15 @@ int phj_debug_poison_chunk_table(phj_ctx* c, int side, const phj_join_params* p,
     PHJ_HIP(c, hipMemsetAsync(S.ctab.p, byte & 0xff, S.ctab.bytes, c->stream));
     PHJ_HIP(c, hipStreamSynchronize(c->stream));
     S.ctab_dirty = false;
+    return PHJ_OK;
+}
+
+int phj_debug_poison_alloc(phj_ctx* c, int byte) {
+    if (!c) return PHJ_ERR_INVALID;
+    const int v = byte < 0 ? -1 : (byte & 0xff);
+    c->poison = v;
+    if (c->group)
+        for (int i = 0; i < c->group->nlocal(); i++) c->group->mem[i]->poison = v;
     return PHJ_OK;
 }
 

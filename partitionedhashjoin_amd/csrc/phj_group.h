@@ -402,8 +402,16 @@ int read_count(Group& G, int i, uint64_t* out, bool pair = false) {
         return PHJ_OK;
     }
     const uint64_t words[2] = {h[0], h[1]};
-    if (phj_count_verdict(words, out) != PHJ_OK)
+    if (phj_count_verdict(words, out) != PHJ_OK) {
+        // some rank failed, this one's own probe perhaps by a pass-1 error
+        // folded into its pair: its chunk tables are cleared before their next
+        // pass either way (as chunk_table_error does on the local path)
+        for (SideState& S : c->side) {
+            S.ctab_dirty = true;
+            S.chunk_check = false;
+        }
         return set_err(c, PHJ_ERR_STATE, std::to_string(h[1]) + " rank(s) failed during the join");
+    }
     return PHJ_OK;
 }
 
@@ -837,7 +845,9 @@ int group_join(phj_ctx* shell, const phj_join_params* p, phj_join_result* r, boo
     // ranks partition by the same function: the LDS join's clusters, or the
     // code tables' refined plan
     Plan cpl;
-    if (use_cluster(G.mem[0], pl, 0, total(G.n[PHJ_SIDE_BUILD]), cpl)) pl = cpl;
+    uint64_t max_s = 0;   // the largest probe shard: every member's S takes the cluster plan's code pass
+    for (uint64_t x : G.n[PHJ_SIDE_PROBE]) max_s = std::max(max_s, x);
+    if (use_cluster(G.mem[0], pl, max_s, total(G.n[PHJ_SIDE_BUILD]), cpl)) pl = cpl;
     else refine_plan(G.mem[0], pl, total(G.n[PHJ_SIDE_BUILD]));
     if (dry) return for_members(shell, G, [&](int i) { return member_prepare_radix(G, i, pl); });
     PHJ_TRY(for_members(shell, G, [&](int i) { return member_radix(G, i, pl, &G.res[i]); }));

@@ -1090,7 +1090,10 @@ void k_chunk_codes(PassArgs a, uint32_t ntiles, uint32_t per) {
 // chain; then kPipeRes chunks per tile of the shard (the ids its starting
 // runs take); then the shard's pool counter.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kPipeRes = 3;
+#ifndef PHJ_PIPE_RES   // (a measurement build may set another reservation)
+#define PHJ_PIPE_RES 3
+#endif
+constexpr uint32_t kPipeRes = PHJ_PIPE_RES;
 __host__ __device__ constexpr uint32_t pipe_pool_stride(uint32_t per, uint32_t nb) {
     return 2 * nb + kPipeRes * per + per + nb + 1;
 }
@@ -1654,88 +1657,6 @@ __global__ __launch_bounds__(kBlock) void k_tile_chunks(const uint32_t* tile_bas
     }
     // the pipelined pass pre-allocates the chunk after a chain's last one
     if (lane == 0 && nch < maxch) tab[nch] = 0;
-    if (bad) atomicOr(sizes + chunk_err_word(nseg), bad);
-}
-
-// After a chunked pass 1, in one launch (the two kernels below in one, no
-// launch between the scan and the tile lists): workgroup s sums the chain
-// sizes of the segments before s itself (coalesced rows of the size table,
-// <= nshards * nseg / kBlock loads per thread) for bounds1[s] and
-// tile_base2[s], then writes segment s's tiles as k_tile_chunks (wave w: the
-// chains of shards w, w + kWaves, ...). Workgroup 0 clears `zero` (four words)
-// and `clr` (clr16 16-B words). nshards <= kShards <= 64.
-__global__ __launch_bounds__(kBlock) void k_chunk_tiles(uint32_t* sizes, uint32_t nseg, uint32_t nshards, uint32_t n,
-                                                        uint32_t T, uint32_t* bounds1, uint32_t* tile_base2,
-                                                        unsigned long long* chunk_tab, uint32_t maxch, uint32_t pool_stride,
-                                                        uint32_t* tile_seg, uint32_t* tile_start, uint32_t* tile_cnt,
-                                                        unsigned long long* zero, uint4* clr, uint32_t clr16) {
-    __shared__ uint32_t red[2][kWaves];
-    const uint32_t s = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    if (s == 0) {
-        if (zero && tid < 4) zero[tid] = 0;   // the on-chip probe's {count, failed} and its clock split
-        if (clr)
-            for (uint32_t i = tid; i < clr16; i += kBlock) clr[i] = make_uint4(0, 0, 0, 0);
-    }
-    // the segments before s: tuples and chunks
-    uint32_t ps = 0, pc = 0;
-    for (uint32_t x = 0; x < nshards; x++)
-        for (uint32_t d = tid; d < s; d += kBlock) {
-            const uint32_t z = sizes[x * nseg + d];
-            ps += z;
-            pc += (z + T - 1) / T;
-        }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        ps += __shfl_xor(ps, o, 64);
-        pc += __shfl_xor(pc, o, 64);
-    }
-    if (lane == 0) {
-        red[0][wave] = ps;
-        red[1][wave] = pc;
-    }
-    // segment s's chains: lane x holds chain x's size, excl its first tile within s
-    const uint32_t z = lane < nshards ? sizes[lane * nseg + s] : 0u;
-    const uint32_t ch = (z + T - 1) / T;
-    uint32_t incl = ch;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o, 64);
-        if (lane >= static_cast<uint32_t>(o)) incl += y;
-    }
-    const uint32_t excl = incl - ch;
-    const uint32_t ch_all = __shfl(incl, 63, 64);   // (every lane active: a shuffle reads inactive lanes as 0)
-    __syncthreads();
-    uint32_t P = 0, C = 0;
-#pragma unroll
-    for (int w = 0; w < kWaves; w++) {
-        P += red[0][w];
-        C += red[1][w];
-    }
-    if (tid == 0) {
-        bounds1[s] = P;
-        tile_base2[s] = C;
-        if (s == nseg - 1) {
-            bounds1[nseg] = n;
-            tile_base2[nseg] = C + ch_all;
-        }
-    }
-    uint32_t bad = 0;
-    for (uint32_t x = wave; x < nshards; x += kWaves) {   // wave-uniform
-        const uint32_t szx = __shfl(z, static_cast<int>(x), 64), nch = (szx + T - 1) / T;
-        const uint32_t t0 = C + __shfl(excl, static_cast<int>(x), 64);
-        unsigned long long* tab = chunk_tab + (static_cast<size_t>(x) * nseg + s) * maxch;
-        for (uint32_t k = lane; k < nch; k += 64) {
-            const unsigned long long v = k < maxch ? tab[k] : 0ull;
-            const uint32_t id = static_cast<uint32_t>(v);
-            const bool ok = k < maxch && (v >> 32) == 1ull && id >= x * pool_stride && id < (x + 1) * pool_stride;
-            tile_seg[t0 + k] = s;
-            tile_start[t0 + k] = ok ? id * T : 0u;
-            tile_cnt[t0 + k] = ok ? min(T, szx - k * T) : 0u;
-            if (!ok) bad |= kChunkErrTable;
-            if (k < maxch) tab[k] = 0;   // the next pass starts from an all-zero table (kPublished)
-        }
-        if (lane == 0 && nch < maxch) tab[nch] = 0;   // the chunk pre-allocated after the chain's last one
-    }
     if (bad) atomicOr(sizes + chunk_err_word(nseg), bad);
 }
 

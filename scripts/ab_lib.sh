@@ -1,6 +1,9 @@
 #!/bin/bash
 # A/B the C2 bench over library builds on one box: scripts/ab_lib.sh LIB1 LIB2 ...
-# (each LIB a libphj_hip.so built beforehand in-tree, e.g. from another commit; PHJ_LIB selects it)
+# (each LIB a libphj_hip.so built beforehand in-tree, e.g. from another commit or with
+#  measurement-only compile flags: `make prof-lib` -> build/libphj_prof.so, the phase-clock
+#  forms of S's pass 1 and of the LDS join (-DPHJ_P1_PROF=1 -DPHJ_CL_PROF=1, stderr per join);
+#  `make build/libphj_res1.so HIPDEFS=-DPHJ_PIPE_RES=1`-style variants the same way; PHJ_LIB selects it)
 set -o pipefail
 mkdir -p gpurun_out
 i=0

@@ -26,14 +26,19 @@ import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
+# one dispatch doing the work of two timers ("build" and "probe")
+SHARED = re.compile(r"phj::k_(join_fused|cluster_probe(?!_big))")
+
 # timer name -> kernel family doing its work (first match wins)
 FAMILIES = [
     (re.compile(r"^R\.p2\.scatter$"), re.compile(r"phj::k_ht_p2")),
     (re.compile(r"\.hist$"), re.compile(r"phj::k_hist")),
     (re.compile(r"\.scatter$"), re.compile(r"phj::k_(scatter|chunk_codes)")),
-    (re.compile(r"^build$"), re.compile(r"phj::k_(build_small|ht_fill|join_fused|cluster_probe)")),
+    # (the LDS join's main kernel, not its big-cluster companion k_cluster_probe_big,
+    # which is dispatched after it: VERDICT r05 weak 2)
+    (re.compile(r"^build$"), re.compile(r"phj::k_(build_small|ht_fill|join_fused|cluster_probe(?!_big))")),
     (re.compile(r"^build\.big$"), re.compile(r"phj::k_cluster_big_fill")),
-    (re.compile(r"^probe$"), re.compile(r"phj::k_(probe|join_fused|cluster_probe)")),
+    (re.compile(r"^probe$"), re.compile(r"phj::k_(probe|join_fused|cluster_probe(?!_big))")),
     (re.compile(r"^np\.build$"), re.compile(r"phj::k_(np_build(?!_overflow)|ht_fill)")),
     (re.compile(r"^np\.probe$"), re.compile(r"phj::k_np_probe")),
 ]
@@ -92,7 +97,7 @@ def attribute(rows, timers):
         if i < 0:
             break
         res[t] = dict(seq[i]["vals"])
-        shared = seq[i] if ("k_join_fused" in seq[i]["name"] or "k_cluster_probe" in seq[i]["name"]) else None
+        shared = seq[i] if SHARED.search(seq[i]["name"]) else None
         i -= 1
     return res
 

@@ -76,6 +76,30 @@ def test_full_size_counts_with_misses(ctx, name, params, alpha):
         assert ctx.join(p1024).matches == expect
 
 
+@pytest.mark.parametrize("alpha", [1.05, 1.25])
+def test_full_size_timed_flags_with_misses(ctx, alpha):
+    """The bench's exact timed configuration: C2 / C5
+    under PHJ_DEFER_TIMERS | PHJ_LEAN_TIMERS, three joins back to back with
+    misses. In that mode the count is polled from pinned host memory written
+    by the LDS join's last workgroup, and S's chunk state for the next join is
+    cleared by that workgroup instead of a memset; each of the three must
+    still equal the device range count and the oracle's semi-join count."""
+    R, S, expect = _workload(ctx, NR, NS, alpha)
+    assert 0.4 * NS < expect < 0.85 * NS
+    assert O.semijoin_count(R, S, threads=THREADS) == expect
+    del R, S
+    timed = phj.radix_params((8, 8), hash=phj.HASH_MURMUR3, seed=SEED)
+    timed.flags |= phj.DEFER_TIMERS | phj.LEAN_TIMERS
+    ctx.timers_report()
+    got = [ctx.join(timed).matches for _ in range(3)]
+    rep = ctx.timers_report()
+    assert got == [expect] * 3, (got, expect)
+    names = [t[0] for t in rep.timers()]
+    assert "probe" in names and "S.p1.scatter" in names
+    # and the plain join after them (its pass 1 starts from the cleared state)
+    assert ctx.join(phj.radix_params((8, 8), hash=phj.HASH_MURMUR3, seed=SEED)).matches == expect
+
+
 def _pair_sums(keys, pays, bounds):
     """Per-partition wrapping sums of two tuple mixes (uint64)."""
     k = keys.view(np.uint64)

@@ -57,26 +57,16 @@ SCHEDULES = [
     {"PHJ_CL_CAP": "8192"},                                     # LDS join: 64 KB tables, two workgroups per CU
     {"PHJ_CL_BITS": "11"},                                      # LDS join: 2048 clusters (two digits per pass-1 thread)
     {"PHJ_CL_BITS": "10", "PHJ_P1_KO_TPS": "4"},                # ... 1024 clusters over 16 shards
-    {"PHJ_CL_PF": "1"},                                         # LDS join probe: one register buffer of codes (no prefetch)
-    {"PHJ_CL_PF": "2"},                                         # ... two
-    {"PHJ_CL_PRE": "0"},                                        # ... each cluster's R codes loaded when its build starts
-    {"PHJ_CL_CNT": "0"},                                        # ... tables built by 64-bit compare-and-swap, not fill counters
-    {"PHJ_CL_CNT": "0", "PHJ_CL_CAP": "8192"},                  # ... in 64 KB tables
+    {"PHJ_CL_CAP": "8192", "PHJ_CL_BITS": "11"},                # ... 64 KB tables over 2048 clusters
     {"PHJ_P1_PIPE": "0"},                                       # keys-only pass 1 resolving its claims in the same tile
     {"PHJ_P1_PIPE": "0", "PHJ_CL_BITS": "11"},                  # ... with four digits per thread
     {"PHJ_P1_BLOCK": "512"},                                    # pipelined pass 1 in 512 x 8 workgroups
     {"PHJ_P1_BLOCK": "512", "PHJ_CL_BITS": "11"},               # ... four digits per thread
-    {"PHJ_P1_KPF": "1"},                                        # ... one tile of keys in flight
-    {"PHJ_P1_KPF": "1", "PHJ_CL_BITS": "11"},                   # ... with two digits per thread
     {"PHJ_R_CHUNK": "0"},                                       # LDS join: R by the stable pass (codes contiguous per cluster)
     {"PHJ_R_CHUNK": "0", "PHJ_CL_BITS": "11"},                  # ... 2048 clusters
     {"PHJ_R_ORDER": "0"},                                       # LDS join: R's pass 1 beside S's
     {"PHJ_R_ORDER": "2"},                                       # ... before it
     {"PHJ_COUNT_PIN": "0"},                                     # LDS join: the count read back by a copy
-    {"PHJ_EXT_TIMERS": "1"},                                    # timers from the kernels' own dispatch (hipExtLaunchKernel)
-    {"PHJ_P1_TILES1": "1"},                                     # chunked pass 1: scan and tile lists in one launch
-    {"PHJ_P1_TILES1": "1", "PHJ_P1_MIN_TILES": "0"},            # ... whole-tuple chunked pass
-    {"PHJ_P1_PROF": "1", "PHJ_CL_PROF": "1"},                   # the phase clocks of pass 1 and of the LDS join's builds
 ]
 
 CASES = [((8, 8), 0, phj.HASH_MURMUR3), ((11, 0), 0, phj.HASH_XXH3), ((1, 0), 1000, phj.HASH_XXH3),

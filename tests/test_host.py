@@ -152,3 +152,32 @@ def test_cli_without_gpu_exits_1(tmp_path):
                         "-f", str(tmp_path / "out.txt")], capture_output=True, text=True)
     assert r.returncode == 1
     assert "No usable HIP device" in r.stderr
+
+
+def test_join_path_declines_lds_join_above_the_pool_bound():
+    """the LDS join needs the probe side's keys-only chunked
+    pass 1, whose chunk pools address slots with 32 bits. Above that bound
+    (about 1.07e9 probe rows with the pipelined pass's reservations) the join
+    must take the code tables (the stable pass 1 and k_probe_ht), not fail.
+    Host-only (phj_join_path: the decision phj_join makes, no device)."""
+    import partitionedhashjoin_amd as phj
+    c2 = phj.radix_params((8, 8), hash=phj.HASH_MURMUR3)
+    nR = 10_000_000
+    assert phj.join_path(c2, nR, 200_000_000) == phj.PATH_LDS_JOIN
+    assert phj.join_path(c2, nR, 0) == phj.PATH_LDS_JOIN
+    # the largest probe side the LDS join takes, found by bisection, then the
+    # rows just above it: every size up to the per-device limit has a path
+    lo, hi = 200_000_000, (1 << 32) - 2 * 4096 - 1
+    assert phj.join_path(c2, nR, hi) == phj.PATH_CODE_TABLES
+    while hi - lo > 1:
+        mid = (lo + hi) // 2
+        if phj.join_path(c2, nR, mid) == phj.PATH_LDS_JOIN:
+            lo = mid
+        else:
+            hi = mid
+    assert 0.5e9 < lo < 2.2e9
+    assert phj.join_path(c2, nR, lo + 1) == phj.PATH_CODE_TABLES
+    # the reference's own -p plans, stable layouts and NoPartitioning
+    assert phj.join_path(phj.radix_params(num_partitions=1024, hash=phj.HASH_XXH3), nR, 200_000_000) == phj.PATH_LDS_JOIN
+    assert phj.join_path(phj.radix_params((8, 8), stable=True), nR, 1000) != phj.PATH_LDS_JOIN
+    assert phj.join_path(phj.nopart_params(), nR, 200_000_000) == phj.PATH_NO_PARTITIONING

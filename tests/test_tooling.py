@@ -66,6 +66,27 @@ def test_fused_join_is_one_dispatch_for_build_and_probe():
     assert got["S.p1.hist"]["FETCH_SIZE"] == 4
 
 
+def test_lds_join_traffic_is_the_main_kernel_not_its_big_companion():
+    """`build` / `probe` took k_cluster_probe_big's
+    counters (a 7.9 us launch dispatched after the LDS join) instead of
+    k_cluster_probe's."""
+    join = ["void phj::k_chunk_codes_pipe<1024, 4, 1, 1, 0, false, 2>(phj::PassArgs, unsigned int, unsigned int)",
+            "phj::k_pass1_finish_sizes(...)", "phj::k_tile_chunks(...)",
+            "void phj::k_chunk_codes_pipe<1024, 4, 1, 1, 0, false, 1>(phj::PassArgs, unsigned int, unsigned int)",
+            "phj::k_pass1_finish_sizes(...)", "phj::k_tile_chunks(...)",
+            "phj::k_cluster_big_fill(phj::ClusterArgs)",
+            "void phj::k_cluster_probe<1024, 4, 3, true, false, true, true>(phj::ClusterArgs)",
+            "phj::k_cluster_probe_big(phj::ClusterArgs)"]
+    names = join + join
+    timers = ["S.p1.scatter", "R.p1.scatter", "build.big", "build", "probe"]   # (pmc_probe.py: every timer)
+    got = pmc.attribute(_rows(names), timers)
+    off = len(join)
+    assert got["build"] == got["probe"] == {"FETCH_SIZE": float(off + 7)}
+    assert got["build.big"]["FETCH_SIZE"] == off + 6
+    assert got["R.p1.scatter"]["FETCH_SIZE"] == off + 3
+    assert got["S.p1.scatter"]["FETCH_SIZE"] == off + 0
+
+
 def test_sweep_writes_generate_sh_figure_layout(tmp_path):
     # scripts/sweep.py writes the reference's figure.dat layout (generate.sh:66-82):
     # one column per run, rows NumberOfPartitions / Partition / Build / Probe
