@@ -1091,8 +1091,11 @@ void k_chunk_codes(PassArgs a, uint32_t ntiles, uint32_t per) {
 // runs take); then the shard's pool counter.
 // ---------------------------------------------------------------------------
 #ifndef PHJ_PIPE_RES   // (a measurement build may set another reservation)
-#define PHJ_PIPE_RES 3
+#define PHJ_PIPE_RES 1
 #endif
+// (1: the pool's reservation per tile; chunks a tile starts beyond it come from
+// the shard's pool counter. Measured against 3: S's pass +0.009 ms at C2, the
+// pool 9.6 -> 4.8 GB and the LDS join's probe-side bound 1.02e9 -> 2.0e9 rows.)
 constexpr uint32_t kPipeRes = PHJ_PIPE_RES;
 __host__ __device__ constexpr uint32_t pipe_pool_stride(uint32_t per, uint32_t nb) {
     return 2 * nb + kPipeRes * per + per + nb + 1;
@@ -1293,11 +1296,16 @@ void k_chunk_codes_pipe(PassArgs a, uint32_t ntiles, uint32_t per) {
             }
             ptick(2);
             if (live) {   // claims of every digit (0 adds too): resolved next iteration
+                // (a thread past the plan's digits claims 0 from its own sink word:
+                // with fewer digits than threads, clamping them onto the last digit
+                // serialised up to 768 returning atomics per tile on one cursor)
 #pragma unroll
                 for (int j = 0; j < DPT; j++) {
-                    const uint32_t d = min(d0 + j, nb - 1);
-                    v0[j] = atomicAdd(curs + d, d0 + j < nb ? c[j] : 0u);
-                    hint[j] = __hip_atomic_load(hints + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const bool real = d0 + j < nb;
+                    uint32_t* cw = real ? curs + d0 + j : reinterpret_cast<uint32_t*>(ssink);
+                    unsigned long long* hw = real ? hints + d0 + j : reinterpret_cast<unsigned long long*>(ssink);
+                    v0[j] = atomicAdd(cw, real ? c[j] : 0u);
+                    hint[j] = __hip_atomic_load(hw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
             if (tid == 0) {
