@@ -42,6 +42,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2", choices=["c2", "c4", "c5"],
                     help="c2: radix 8+8 murmur3 s=1.05; c4: no-partitioning xxh3; c5: radix s=1.25")
+    ap.add_argument("--skew", type=float, default=None, help="Zipf skew of S (default: the config's)")
     ap.add_argument("--primary", type=int, default=NR)
     ap.add_argument("--secondary", type=int, default=NS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -260,6 +261,9 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     nR, nS = args.primary, args.secondary
     params, alpha, workload = config_params(phj, args.config)
+    if args.skew is not None:
+        alpha = args.skew
+        workload += f" (skew overridden: {alpha})"
     # the join is one C call per step on this rank's context: a single-device
     # phj_join at N=1; at N>1 (or --exchange) the multi-GPU member step of
     # csrc/phj_group.h (R partition + RCCL all-gather of the build keys beside

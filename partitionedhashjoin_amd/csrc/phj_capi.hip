@@ -2902,11 +2902,11 @@ int phj_debug_exchange_block(phj_ctx* c, int member, int64_t* out, uint64_t elem
     if (!c->group) return set_err(c, PHJ_ERR_STATE, "phj_debug_exchange_block takes a multi-device or rank context");
     Group& G = *c->group;
     if (member < 0 || member >= G.nlocal()) return set_err(c, PHJ_ERR_INVALID, "no such local member");
-    const DevBuf& b = G.buf[member].send;
-    if (!b.p || b.bytes < elems * 8) return set_err(c, PHJ_ERR_STATE, "no exchange block of that size");
+    const DevBuf& b = G.buf[member].recv;
+    if (!b.p || b.bytes < static_cast<size_t>(G.world) * elems * 8) return set_err(c, PHJ_ERR_STATE, "no exchange block of that size");
     PHJ_HIP(c, hipSetDevice(G.mem[member]->device));
     PHJ_HIP(c, hipStreamSynchronize(G.mem[member]->aux));
-    PHJ_HIP(c, hipMemcpy(out, b.p, elems * 8, hipMemcpyDeviceToHost));
+    PHJ_HIP(c, hipMemcpy(out, own_block(G, member, elems), elems * 8, hipMemcpyDeviceToHost));
     return PHJ_OK;
 }
 

@@ -209,7 +209,10 @@ PackLayout pack_layout(uint64_t maxn, uint32_t P) {
 enum class Xchg { kRccl, kLocal };
 
 struct MemberBufs {
-    DevBuf send, recv, cnt, full;
+    // recv: the gathered blocks of every rank; a member packs its own block in
+    // place, at its global rank's offset (an in-place all-gather: no send
+    // buffer, no copy of its own block)
+    DevBuf recv, cnt, full;
     hipEvent_t packed = nullptr;
     bool rehearsal_packed = false;   // PHJ_REHEARSE: this member's block is packed (members > 0 pack once)
     // local NoPartitioning exchange: this member's R shard, published before the
@@ -267,7 +270,7 @@ void group_destroy(Group* G) {
         (void)hipStreamSynchronize(c->aux);
         if (i < G->comm.size() && G->comm[i]) (void)rccl().CommDestroy(G->comm[i]);
         MemberBufs& B = G->buf[i];
-        for (DevBuf* b : {&B.send, &B.recv, &B.cnt, &B.full}) free_buf(*b);
+        for (DevBuf* b : {&B.recv, &B.cnt, &B.full}) free_buf(*b);
         if (B.packed) (void)hipEventDestroy(B.packed);
     }
     for (phj_ctx* c : G->mem) phj_ctx_destroy(c);
@@ -297,6 +300,11 @@ int exchange_sizes(phj_ctx* shell, Group& G, int side) {
     return PHJ_OK;
 }
 
+// Member i's own exchange block: its global rank's slot of the gathered buffer.
+int64_t* own_block(Group& G, int i, uint64_t elems) {
+    return static_cast<int64_t*>(G.buf[i].recv.p) + static_cast<size_t>(G.rank0 + i) * elems;
+}
+
 uint64_t total(const std::vector<uint64_t>& v) {
     uint64_t t = 0;
     for (uint64_t x : v) t += x;
@@ -305,8 +313,8 @@ uint64_t total(const std::vector<uint64_t>& v) {
 
 // ---- the radix join step of one member ----
 
-// All-gather of `elems` int64 per rank from B.send into B.recv, on the member's
-// current launch stream (aux). `ok` = this member packed its block; with the
+// All-gather of `elems` int64 per rank into B.recv (in place: each rank's block
+// is already at its slot, own_block), on the member's current launch stream (aux). `ok` = this member packed its block; with the
 // local exchange every member reaches the barrier even after an error, and
 // nobody copies when any member failed (its block may not exist).
 // With RCCL a member that failed before the collective still takes part in it
@@ -331,11 +339,12 @@ int allgather_blocks(Group& G, int i, uint64_t elems, bool ok, bool receive = tr
     MemberBufs& B = G.buf[i];
     if (G.kind == Xchg::kRccl) {
         if (!G.comm[i]) return set_err(c, PHJ_ERR_STATE, "RCCL communicator aborted by an earlier failure");
-        if (!B.send.p || !B.recv.p || B.send.bytes < elems * 8 || B.recv.bytes < static_cast<size_t>(G.world) * elems * 8)
+        if (!B.recv.p || B.recv.bytes < static_cast<size_t>(G.world) * elems * 8)
             return abort_comm(G, i, ok ? set_err(c, PHJ_ERR_STATE, "exchange buffers missing") : PHJ_ERR_STATE);
-        if (!ok && hipMemsetAsync(B.send.p, 0, elems * 8, c->ks) != hipSuccess)
+        int64_t* mine = own_block(G, i, elems);
+        if (!ok && hipMemsetAsync(mine, 0, elems * 8, c->ks) != hipSuccess)
             return abort_comm(G, i, PHJ_ERR_STATE);   // cannot send a valid empty segment
-        PHJ_NCCL(c, rccl().AllGather(B.send.p, B.recv.p, elems, ncclInt64, G.comm[i], c->ks));
+        PHJ_NCCL(c, rccl().AllGather(mine, B.recv.p, elems, ncclInt64, G.comm[i], c->ks));
         c->since_ev++;
         return ok ? PHJ_OK : PHJ_ERR_STATE;
     }
@@ -345,13 +354,15 @@ int allgather_blocks(Group& G, int i, uint64_t elems, bool ok, bool receive = tr
     if (G.failed.load()) return ok ? set_err(c, PHJ_ERR_STATE, "another member failed") : PHJ_ERR_STATE;
     if (!receive) return PHJ_OK;
     for (int h = 0; h < G.nlocal(); h++) {
+        if (h == i) continue;   // (its own block is packed in place)
         phj_ctx* ch = G.mem[h];
         char* dst = static_cast<char*>(B.recv.p) + static_cast<size_t>(h) * elems * 8;
+        const void* src = own_block(G, h, elems);   // (a peer writes only its other slots)
         PHJ_HIP(c, hipStreamWaitEvent(c->ks, G.buf[h].packed, 0));
         if (ch->device == c->device)
-            PHJ_HIP(c, hipMemcpyAsync(dst, G.buf[h].send.p, elems * 8, hipMemcpyDeviceToDevice, c->ks));
+            PHJ_HIP(c, hipMemcpyAsync(dst, src, elems * 8, hipMemcpyDeviceToDevice, c->ks));
         else
-            PHJ_HIP(c, hipMemcpyPeerAsync(dst, c->device, G.buf[h].send.p, ch->device, elems * 8, c->ks));
+            PHJ_HIP(c, hipMemcpyPeerAsync(dst, c->device, src, ch->device, elems * 8, c->ks));
     }
     c->since_ev++;
     return PHJ_OK;
@@ -435,7 +446,6 @@ int member_alloc_radix(Group& G, int i, const Plan& pl, bool p2) {
     phj_ctx* c = G.mem[i];
     MemberBufs& B = G.buf[i];
     const PackLayout L = member_layout(G, pl, p2);
-    PHJ_TRY(ensure(c, B.send, L.elems * 8));
     PHJ_TRY(ensure(c, B.recv, static_cast<size_t>(G.world) * L.elems * 8));
     PHJ_TRY(ensure(c, B.cnt, cnt_bytes(G)));
     if (!B.packed) PHJ_HIP(c, hipEventCreateWithFlags(&B.packed, hipEventDisableTiming));
@@ -552,15 +562,15 @@ int member_radix(Group& G, int i, const Plan& pl, phj_join_result* r) {
     if (rc == PHJ_OK && hipStreamWaitEvent(c->aux, t0, 0) != hipSuccess) rc = set_err(c, PHJ_ERR_HIP, "wait t0");
     if (p2) {   // the R shard as codes in partition order, straight into the exchange block
         if (rc == PHJ_OK)
-            rc = partition_build(c, pl, static_cast<int64_t*>(B.send.p),
-                                 reinterpret_cast<uint32_t*>(static_cast<int64_t*>(B.send.p) + L.maxn));
+            rc = partition_build(c, pl, own_block(G, i, L.elems),
+                                 reinterpret_cast<uint32_t*>(own_block(G, i, L.elems) + L.maxn));
     } else {
         if (rc == PHJ_OK) rc = partition_side(c, PHJ_SIDE_BUILD, pl);
         if (rc == PHJ_OK && R.n &&
-            hipMemcpyAsync(B.send.p, R.view.keys, R.n * 8, hipMemcpyDeviceToDevice, c->ks) != hipSuccess)
+            hipMemcpyAsync(own_block(G, i, L.elems), R.view.keys, R.n * 8, hipMemcpyDeviceToDevice, c->ks) != hipSuccess)
             rc = set_err(c, PHJ_ERR_HIP, "pack keys");
         if (rc == PHJ_OK &&
-            hipMemcpyAsync(static_cast<int64_t*>(B.send.p) + L.maxn, R.view.bounds, (static_cast<size_t>(P) + 1) * 4,
+            hipMemcpyAsync(own_block(G, i, L.elems) + L.maxn, R.view.bounds, (static_cast<size_t>(P) + 1) * 4,
                            hipMemcpyDeviceToDevice, c->ks) != hipSuccess)
             rc = set_err(c, PHJ_ERR_HIP, "pack bounds");
         c->since_ev += 2;

@@ -14,6 +14,15 @@ bench.py's cpu_baseline) over the same relations (the host generator equals
 the CLI's, generate.sh's default relations), into <out>_<skew>_cpu.dat.
 
     python scripts/sweep.py --skew 1.05 1.25 --gpus 1 --cpu --out profiles/r02_sweep_cli
+
+With --rehearse-worlds W..., the GPU-count axis is also REHEARSED ON ONE GPU
+(for boxes with one MI355X): the CLI's multi-device step with W members on
+device 0 (--devices 0,..,0 --exchange local) and PHJ_REHEARSE=1, so members
+1..W-1 only feed the exchange (device copies standing in for the RCCL
+all-gather) and the reported phases are member 0's, i.e. one rank's device
+work at world size W (the radix columns; the NoPartitioning step has no
+rehearsal form). Written to <out>_<skew>_rehearsed_w<W>.dat and one
+<out>_<skew>_gpu_axis.json (per column: the total per W, labelled).
 """
 import argparse
 import json
@@ -47,11 +56,12 @@ def write_figure(path, table):
         f.write("\n".join(" ".join(r) for r in figure_rows(table)) + "\n")
 
 
-def run(args, unit):
+def run(args, unit, env=None):
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "r.txt")
         cmd = [CLI, *args, "-u", unit, "--log", "error", "-o", "file", "--filename", out]
-        subprocess.run(cmd, check=True, capture_output=True, text=True, timeout=600)
+        subprocess.run(cmd, check=True, capture_output=True, text=True, timeout=600,
+                       env=None if env is None else dict(os.environ, **env))
         with open(out) as f:
             return json.load(f)
 
@@ -88,6 +98,8 @@ def main():
     ap.add_argument("--seed", type=int, default=20240601)
     ap.add_argument("--cpu", action="store_true", help="also time the CPU columns (oracle restatement)")
     ap.add_argument("--cpu-threads", type=int, default=15)
+    ap.add_argument("--rehearse-worlds", type=int, nargs="*", default=[],
+                    help="GPU-count axis rehearsed on one GPU (W members on device 0, PHJ_REHEARSE=1)")
     ap.add_argument("--out", default="sweep")
     a = ap.parse_args()
     common = ["--primary", str(a.primary), "--secondary", str(a.secondary), "--generate", a.generate,
@@ -107,6 +119,30 @@ def main():
             with open(base + ".json", "w") as f:
                 json.dump({"skew": skew, "gpus": g, "unit": a.unit, "primary": a.primary, "secondary": a.secondary,
                            "runs": table}, f, indent=1)
+        if a.rehearse_worlds:
+            axis = {}
+            for W in a.rehearse_worlds:
+                table = {}
+                for name, args, _p in columns():
+                    if _p is None:   # (PHJ_REHEARSE quiets the radix member step only)
+                        continue
+                    res = run(args + common + ["--skew", str(skew), "--devices", ",".join(["0"] * W),
+                                               "--exchange", "local"], a.unit, env={"PHJ_REHEARSE": "1"})
+                    r = res["results"]
+                    table[name] = {"partition": int(r["partition"]), "build": int(r["build"]),
+                                   "probe": int(r["probe"]), **{k: v for k, v in res.get("device", {}).items()}}
+                    axis.setdefault(name, {})[W] = table[name].get("device_total_us",
+                                                                   table[name]["partition"] + table[name]["build"] +
+                                                                   table[name]["probe"])
+                    print(f"skew {skew} rehearsed W={W} {name:16s} {r['partition']:>8s} {r['build']:>8s} "
+                          f"{r['probe']:>8s}", flush=True)
+                write_figure(f"{a.out}_{skew}_rehearsed_w{W}.dat", table)
+            with open(f"{a.out}_{skew}_gpu_axis.json", "w") as f:
+                json.dump({"skew": skew, "unit": a.unit, "primary": a.primary, "secondary": a.secondary,
+                           "label": "rehearsed on one GPU: W members on device 0 (PHJ_REHEARSE=1), member 0's "
+                                    "device time = one rank's work at world size W; the exchange is device "
+                                    "copies, not RCCL over xGMI",
+                           "total_by_world": axis}, f, indent=1)
         if a.cpu:
             table = cpu_table(a.primary, a.secondary, skew, a.seed, a.unit, a.cpu_threads)
             write_figure(f"{a.out}_{skew}_cpu.dat", table)
