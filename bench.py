@@ -277,16 +277,23 @@ def main():
 
     radix = params.algo == phj.ALGO_RADIX
 
-    def step():
-        return ctx.join(params)
-
-    for _ in range(args.warmup):
-        step()
-
     def barrier():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
+
+    # the warm-up steps run the timed steps' own flags (below)
+    defer = args.timers_deferred and params.algo == phj.ALGO_RADIX
+    timed_params = params
+    if defer:
+        timed_params = type(params).from_buffer_copy(params)
+        # (lean on one device: 7 us faster there, 8 us slower in the W=8 rehearsal's member step)
+        lean = world == 1 and not exchange and not args.all_timers
+        timed_params.flags = params.flags | phj.DEFER_TIMERS | (phj.LEAN_TIMERS if lean else 0)
+    for _ in range(args.warmup):
+        ctx.join(timed_params)
+    if defer:
+        ctx.timers_report()   # a clean slate
 
     barrier()
     t0 = time.perf_counter()
@@ -305,14 +312,6 @@ def main():
     # inside them and summed by timers_report after the loop
     # (at N>1 each rank's context has one member: the same, per rank); one
     # device: PHJ_LEAN_TIMERS also leaves R's pass-1 timer out (--all-timers)
-    defer = args.timers_deferred and params.algo == phj.ALGO_RADIX
-    timed_params = params
-    if defer:
-        timed_params = type(params).from_buffer_copy(params)
-        # (lean on one device: 7 us faster there, 8 us slower in the W=8 rehearsal's member step)
-        lean = world == 1 and not exchange and not args.all_timers
-        timed_params.flags = params.flags | phj.DEFER_TIMERS | (phj.LEAN_TIMERS if lean else 0)
-        ctx.timers_report()   # a clean slate
     results = [ctx.join(timed_params) for _ in range(args.steps)]
     barrier()
     elapsed = time.perf_counter() - t0

@@ -285,6 +285,20 @@ hipEvent_t next_event(phj_ctx* c) {
     return c->evpool[c->evnext++];
 }
 
+// phj_prepare: events for this many timer marks created up front (deferred
+// timers keep every join's marks until phj_timers_report, ~4 per join under
+// PHJ_LEAN_TIMERS: 64 joins' worth), so no hipEventCreate runs inside a timed loop
+constexpr size_t kPrepEvents = 256;
+int reserve_events(phj_ctx* c, size_t n) {
+    while (c->evpool.size() < n) {
+        hipEvent_t e = new_event();
+        if (!e) return set_err(c, PHJ_ERR_HIP, "hipEventCreate failed");
+        c->evpool.push_back(e);
+    }
+    if (c->timers.capacity() < n) c->timers.reserve(n);
+    return PHJ_OK;
+}
+
 int mark(phj_ctx* c, hipEvent_t* out) {
     *out = next_event(c);
     if (!*out) return set_err(c, PHJ_ERR_HIP, "hipEventCreate failed");
@@ -622,6 +636,35 @@ const void* pipe1024(int kpf) {
     return reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, HK, DPT, 0, PHJ_P1_PROF != 0, 2>);
 }
 
+// Workgroups per CU of kernel kfn at `block` threads and `lds` bytes of dynamic
+// LDS, as the runtime reports it (0 if it cannot), cached per host thread: the
+// query reads the kernel's attributes through the runtime, host time before
+// every launch of a join otherwise.
+int occupancy(const void* kfn, int block, size_t lds) {
+    struct Key {
+        const void* f;
+        int b;
+        size_t l;
+        bool operator==(const Key& o) const { return f == o.f && b == o.b && l == o.l; }
+    };
+    struct Hash {
+        size_t operator()(const Key& k) const {
+            return std::hash<const void*>()(k.f) ^ (static_cast<size_t>(k.b) << 20) ^ (k.l * 0x9E3779B97F4A7C15ull);
+        }
+    };
+    thread_local std::unordered_map<Key, int, Hash> cache;
+    const Key k{kfn, block, lds};
+    auto it = cache.find(k);
+    if (it != cache.end()) return it->second;
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kfn, block, lds) != hipSuccess) {
+        (void)hipGetLastError();
+        occ = 0;
+    }
+    cache.emplace(k, occ);
+    return occ;
+}
+
 template <int BLOCK, int ITEMS, bool IN_AOS, bool OUT_AOS>
 int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const std::string& prefix,
                   uint64_t n, uint32_t hist_len) {
@@ -690,15 +733,7 @@ int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const st
                                      : reinterpret_cast<const void*>(&k_scatter_chunked<BLOCK, ITEMS, kXXH3, 3>);
             // workgroups per CU: what the LDS and the kernel's registers allow
             // (cached per kernel and LDS size; one cache per worker thread)
-            thread_local std::unordered_map<const void*, std::pair<size_t, int>> occ_cache;
-            int occ = 0;
-            auto hit = occ_cache.find(kfn);
-            if (hit != occ_cache.end() && hit->second.first == lds) {
-                occ = hit->second.second;
-            } else {
-                if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kfn, kblock, lds) != hipSuccess || occ < 1) occ = 1;
-                occ_cache[kfn] = {lds, occ};
-            }
+            const int occ = std::max(1, occupancy(kfn, kblock, lds));
             const uint32_t fit = std::max<uint32_t>(1, std::min<uint32_t>(static_cast<uint32_t>(occ), static_cast<uint32_t>(160 * 1024 / lds)));
             uint32_t slots = std::max<uint32_t>(1, std::min<uint32_t>(per, fit * c->num_cus / a.nshards));
             // keys-only (the on-chip join): PHJ_P1_WPC2 half-workgroups per CU, not
@@ -1108,8 +1143,7 @@ int build_and_probe(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned*
         const void* kfn = pl.hk == kMurmur3 ? reinterpret_cast<const void*>(&k_join_fused<kMurmur3, kFusedKPL, kFusedTcap>)
                                             : reinterpret_cast<const void*>(&k_join_fused<kXXH3, kFusedKPL, kFusedTcap>);
         int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, kBlock, 0) != hipSuccess || per_cu < 1)
-            per_cu = 2;
+        if ((per_cu = occupancy(kfn, kBlock, 0)) < 1) per_cu = 2;
         const size_t wblocks = (nslots + kWaves - 1) / kWaves;
         const uint32_t grid = static_cast<uint32_t>(
             std::max<size_t>(1, std::min<size_t>(wblocks, static_cast<size_t>(per_cu) * c->num_cus)));
@@ -1280,7 +1314,7 @@ int build_and_probe(phj_ctx* c, const Plan& pl, int nseg, const phj_partitioned*
         else kfn = reinterpret_cast<const void*>(&k_probe_wave<kXXH3, kProbeWaveKPL, kProbeWaveTcap>);
     }
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, kBlock, 0) != hipSuccess || per_cu < 1) per_cu = 2;
+    if ((per_cu = occupancy(kfn, kBlock, 0)) < 1) per_cu = 2;
     const size_t item_blocks = wave_probe ? (item_bound + kWaves - 1) / kWaves : item_bound;
     const uint32_t pgrid = static_cast<uint32_t>(
         std::max<size_t>(1, std::min<size_t>(item_blocks, static_cast<size_t>(per_cu) * c->num_cus)));
@@ -1461,7 +1495,7 @@ int probe_ht(phj_ctx* c, const Plan& pl, SideState& PS, bool clear = true) {
     // persistent: as many workgroups as fit the chip at once (a multiple of 8:
     // XCD x owns tiles [x, x + 1) * ntiles / 8), never many more than tiles
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, B, lds) != hipSuccess || per_cu < 1) per_cu = 2;
+    if ((per_cu = occupancy(kfn, B, lds)) < 1) per_cu = 2;
     per_cu = std::min<int>(per_cu, static_cast<int>(160 * 1024 / lds));
     const uint32_t want = (PS.nt2 + 7) & ~7u;
     const uint32_t grid = std::max<uint32_t>(8, std::min<uint32_t>(want, static_cast<uint32_t>(per_cu) * c->num_cus) & ~7u);
@@ -1607,7 +1641,7 @@ int probe_cluster(phj_ctx* c, const Plan& pl, SideState& PS, int nseg, const int
     const void* kfn = RT ? reinterpret_cast<const void*>(&k_cluster_probe<B, I, 3, true, PR, true>)
                          : reinterpret_cast<const void*>(&k_cluster_probe<B, I, 3, true, PR, false>);
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, B, lds) != hipSuccess || per_cu < 1) per_cu = 1;
+    if ((per_cu = occupancy(kfn, B, lds)) < 1) per_cu = 1;
     per_cu = std::max(1, std::min<int>(per_cu, static_cast<int>(160 * 1024 / (lds + 256))));
     // persistent, a multiple of 8 (XCD-grouped ranges), never many more than tiles
     const uint32_t want = (PS.nt2 + 7) & ~7u;
@@ -1749,7 +1783,7 @@ int join_nopart_ct(phj_ctx* c, const phj_join_params* p, phj_join_result* r) {
         const void* kfn = p->hash == PHJ_HASH_MURMUR3 ? reinterpret_cast<const void*>(&k_np_probe_ct<kMurmur3, IT>)
                                                       : reinterpret_cast<const void*>(&k_np_probe_ct<kXXH3, IT>);
         int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, 256, 0) != hipSuccess || per_cu < 1) per_cu = 8;
+        if ((per_cu = occupancy(kfn, 256, 0)) < 1) per_cu = 8;
         const uint64_t want = (S.n + 256ull * IT - 1) / (256ull * IT);
         const uint32_t grid = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(want, static_cast<uint64_t>(per_cu) * c->num_cus)));
         const auto* S_rel = reinterpret_cast<const longlong2*>(S.rel);
@@ -2657,6 +2691,7 @@ int phj_prepare(phj_ctx* c, const phj_join_params* p) {
     }
     (void)hipGetLastError();
     PHJ_HIP(c, hipSetDevice(c->device));
+    PHJ_TRY(reserve_events(c, kPrepEvents));
     struct DryScope {
         phj_ctx* c;
         ~DryScope() { c->dry = false; }

@@ -477,6 +477,7 @@ void gathered_codes(const Group& G, int i, const PackLayout& L, const int64_t** 
 int member_prepare_radix(Group& G, int i, const Plan& pl) {
     phj_ctx* c = G.mem[i];
     PHJ_HIP(c, hipSetDevice(c->device));
+    PHJ_TRY(reserve_events(c, kPrepEvents));
     const bool p2 = member_p2(G, c, pl);
     PHJ_TRY(member_alloc_radix(G, i, pl, p2));
     struct DryScope {
