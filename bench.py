@@ -348,7 +348,11 @@ def main():
     shift = 3
     generate_shards(ctx, nR, nS, alpha, GEN_SEED, rank, world, start=1 + shift)
     shifted_expect = allsum(ctx.count_in_range(1, 1 + shift, nR))
-    shifted_runs = [ctx.join(timed_params).matches for _ in range(3)] + [ctx.join(params).matches]
+    shifted_runs, shifted_ms = [], []   # (host wall time per join: the misses' probe cost)
+    for p in [timed_params] * 3 + [params]:
+        t_join = time.perf_counter()
+        shifted_runs.append(ctx.join(p).matches)
+        shifted_ms.append(round((time.perf_counter() - t_join) * 1e3, 4))
     if defer:
         ctx.timers_report()   # (the check's deferred timers are not the bench's)
     shifted_got = shifted_runs[0]
@@ -388,7 +392,8 @@ def main():
             "matches": int(matches),
             "expected_matches": inrange,
             "shifted_check": {"build_start": 1 + shift, "expected": shifted_expect, "matches": shifted_got,
-                              "runs": shifted_runs, "flags": int(timed_params.flags), "plain_flags": int(params.flags)},
+                              "runs": shifted_runs, "wall_ms": shifted_ms, "flags": int(timed_params.flags),
+                              "plain_flags": int(params.flags)},
             "correct": int(matches) == inrange and shifted_ok,
             "exchange_ms": exch / args.steps if exchange else None,
             "roofline": {"bound": "hbm", "kernel": dom_name, "achieved": achieved,

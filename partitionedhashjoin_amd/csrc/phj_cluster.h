@@ -314,7 +314,14 @@ __global__ __launch_bounds__(256) void k_cluster_probe_big(ClusterArgs a) {
 // set test: a probe stops at the first match either way); a bucket's attempts
 // are at most the cluster's codes (<= lim < 2^16), so a counter never carries
 // into its neighbour.
-template <int BLOCK, int ITEMS, int PF = 1, bool PRE = true, bool PROF = false, bool TM = false>
+__host__ __device__ constexpr size_t cluster_lds_bytes(uint32_t cap) { return static_cast<size_t>(cap) * 9; }
+// ASMW: the S codes' loads in inline assembly, each step waiting for exactly its
+// own tile (the compiler, merging the build and staging paths, waited for
+// every load in flight, s_waitcnt vmcnt(0), before every tile's table reads)
+#ifndef PHJ_CL_ASM
+#define PHJ_CL_ASM 1
+#endif
+template <int BLOCK, int ITEMS, int PF = 1, bool PRE = true, bool PROF = false, bool TM = false, bool ASMW = PHJ_CL_ASM != 0>
 __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
     constexpr int CPL = kClCapMax * 3 / 4 / BLOCK;   // R codes per lane at the limit
     extern __shared__ __attribute__((aligned(16))) uint64_t tab[];   // [cap] + cap / 4 words of fill counters
@@ -349,7 +356,9 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
         // retires in issue order, and one conditional load made the compiler
         // wait for everything in flight. The metadata loads are vector loads (a
         // scalar load would be waited for by every LDS access: lgkmcnt counts both).
-        int64_t key[PF][ITEMS];
+        typedef long long v2i __attribute__((ext_vector_type(2)));
+        // the tiles' codes, two per 16-B load (kv[f][i / 2] holds items i, i + 1)
+        v2i kv[PF][ITEMS / 2];
         uint32_t vm[PF], dq[PF];
         // tile metadata staged in LDS, MR tiles at a time (refilled behind a
         // barrier every MR tiles): the loop's only global loads are then the
@@ -368,7 +377,7 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
             __syncthreads();
             mbase = base;
         };
-        auto load = [&](uint32_t t, int64_t* k, uint32_t& m, uint32_t& dd) {
+        auto load = [&](uint32_t t, v2i* k, uint32_t& m, uint32_t& dd) {
             if (t - mbase >= MR && t < t_hi) stage(t);   // workgroup-uniform
             const uint32_t j = min(t, t_hi - 1) - mbase;
             dd = smeta[0][j];
@@ -381,21 +390,25 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
             // lanes past the tile's codes at its last pair, which they share
             // with a valid lane (masked off: a chain's last, partial chunk is
             // not read whole; ~15 % of the bytes at C2)
-            typedef long long v2i __attribute__((ext_vector_type(2)));
             const v2i* src = reinterpret_cast<const v2i*>(a.s_codes + lo);
             const uint32_t last = c ? (c - 1) / 2 : 0u;
 #pragma unroll
             for (int i = 0; i < ITEMS; i += 2) {
                 const uint32_t e = 2 * ((i / 2) * BLOCK + tid);
-                const v2i v = __builtin_nontemporal_load(src + min((i / 2) * BLOCK + tid, last));
-                k[i] = v.x;
-                k[i + 1] = v.y;
+                const v2i* ptr = src + min((i / 2) * BLOCK + tid, last);
+                if constexpr (ASMW) {
+                    // issued outside the compiler's wait model: the step waits for
+                    // exactly this tile (CLW below)
+                    __asm__ volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(k[i / 2]) : "v"(ptr));
+                } else {
+                    k[i / 2] = __builtin_nontemporal_load(ptr);
+                }
                 m |= (e < c ? (1u << i) : 0u) | (e + 1 < c ? (2u << i) : 0u);
             }
         };
         stage(t_lo);
 #pragma unroll
-        for (int f = 0; f < PF; f++) load(t_lo + f, key[f], vm[f], dq[f]);   // tiles t_lo .. t_lo + PF - 1
+        for (int f = 0; f < PF; f++) load(t_lo + f, kv[f], vm[f], dq[f]);   // tiles t_lo .. t_lo + PF - 1
         uint32_t cur = 0xffffffffu, bmask = 0;
         bool big = false;
         uint64_t e = 0;
@@ -490,6 +503,7 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
             // every load of the build path complete (s_waitcnt vmcnt(0)): else
             // the compiler, merging this path with the no-build one, makes the
             // next step wait for every load in flight on both
+            // (leaving it to the compiler measured the same: r06c_ab_nodrain.txt)
             __builtin_amdgcn_s_waitcnt(0xF70);
             if (PROF) {
                 __syncthreads();
@@ -523,13 +537,26 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
         auto step = [&](int f) -> bool {
             const uint32_t cvm = vm[f], d = dq[f];
             if (d != cur) build(d);   // workgroup-uniform
+            if constexpr (ASMW) {
+                // this tile's loads: every step issues ITEMS / 2 loads, so at most
+                // (PF - 1) * ITEMS / 2 issued after them may stay in flight (any
+                // other load issued since only makes the wait longer, never short)
+                static_assert(ITEMS == 4, "two 16-B loads per tile");
+                __asm__ volatile("s_waitcnt vmcnt(%2)" : "+v"(kv[f][0]), "+v"(kv[f][1]) : "n"((PF - 1) * ITEMS / 2));
+            }
+            int64_t key[ITEMS];
+#pragma unroll
+            for (int i = 0; i < ITEMS; i += 2) {
+                key[i] = kv[f][i / 2].x;
+                key[i + 1] = kv[f][i / 2].y;
+            }
             if (!big) {   // LDS: every item's home bucket read, then the walks
                 ulonglong2 v[ITEMS];
 #pragma unroll
-                for (int i = 0; i < ITEMS; i++) v[i] = tb[static_cast<uint32_t>(static_cast<uint64_t>(key[f][i]) >> kHtBucketShift) & bmask];
+                for (int i = 0; i < ITEMS; i++) v[i] = tb[static_cast<uint32_t>(static_cast<uint64_t>(key[i]) >> kHtBucketShift) & bmask];
 #pragma unroll
                 for (int i = 0; i < ITEMS; i++) {
-                    const uint64_t cc = static_cast<uint64_t>(key[f][i]);
+                    const uint64_t cc = static_cast<uint64_t>(key[i]);
                     bool hit = v[i].x == cc || v[i].y == cc;
                     if ((cvm >> i) & 1u) {
                         if (!hit && v[i].y != e) {
@@ -549,7 +576,7 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
             // into other registers would put a move at the loop's back edge,
             // which waits for the refill): tile t + PF's codes; tiles t + 1 ..
             // t + PF - 1 were in flight during this tile's probe
-            load(t + PF, key[f], vm[f], dq[f]);
+            load(t + PF, kv[f], vm[f], dq[f]);
             return ++t < t_hi;
         };
         bool more = true;
@@ -559,6 +586,10 @@ __global__ __launch_bounds__(BLOCK) void k_cluster_probe(ClusterArgs a) {
                 more = step(f);
                 if (!more) break;
             }
+        }
+        if constexpr (ASMW) {   // the loads past the range land before their registers are reused
+#pragma unroll
+            for (int f = 0; f < PF; f++) __asm__ volatile("s_waitcnt vmcnt(0)" : "+v"(kv[f][0]), "+v"(kv[f][1]));
         }
     }
     uint32_t x = hits;

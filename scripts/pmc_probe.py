@@ -20,7 +20,9 @@ import partitionedhashjoin_amd as phj
 alpha = 1.25 if args.config == "c5" else 1.05
 params = phj.nopart_params() if args.config == "c4" else phj.radix_params((8, 8))
 c = phj.Context(0)
-c.generate_sequential(0, args.primary, 1)
+# PMC_BUILD_START: R = [start, start + |R|) (4: the bench's shifted-R check, the
+# three hottest Zipf keys absent from R)
+c.generate_sequential(0, args.primary, int(os.environ.get("PMC_BUILD_START", "1")))
 c.generate_zipf(1, args.secondary, alpha, 1, args.primary, 20240601)
 c.count_in_range(1, 1, args.primary)
 for _ in range(args.steps):
