@@ -13,7 +13,7 @@
 #   rehearse         per-rank W = 1, 2, 4, 8 rehearsal on one GPU (scripts/rehearse_world.py)
 #   pmc              counter calibration + probe / pass-1 PMC passes at C2, C5, C4
 #   traces           kernel timelines of a C2 step and a rehearsed W=8 member step
-#   sweep            the reference's partition-count sweep through the CLI (scripts/sweep.py)
+#   sweep            the reference's partition-count sweep through the CLI + the rehearsed GPU-count axis (scripts/sweep.py)
 set -o pipefail
 TAG=${1:?usage: round_measure.sh TAG STEP...}
 shift
@@ -76,7 +76,7 @@ for step in "$@"; do
       python3 scripts/trace_summary.py ${O}_c2trace --step-kernel "k_cluster_probe<" > ${O}_c2trace.txt 2>&1
       tail -30 ${O}_c2trace.txt ;;
     sweep)
-      timeout -k 10 900 python scripts/sweep.py --skew 1.05 1.25 --out ${O}_sweep_cli > ${O}_sweep.log 2>&1 || { echo "sweep failed"; tail -5 ${O}_sweep.log; exit 9; }
+      timeout -k 10 900 python scripts/sweep.py --skew 1.05 1.25 --rehearse-worlds 1 2 4 8 --out ${O}_sweep_cli > ${O}_sweep.log 2>&1 || { echo "sweep failed"; tail -5 ${O}_sweep.log; exit 9; }
       tail -24 ${O}_sweep.log ;;
     *) echo "unknown step $step"; exit 10 ;;
   esac
