@@ -13,6 +13,7 @@
 #   rehearse         per-rank W = 1, 2, 4, 8 rehearsal on one GPU (scripts/rehearse_world.py)
 #   pmc              counter calibration + probe / pass-1 PMC passes at C2, C5, C4
 #   traces           kernel timelines of a C2 step and a rehearsed W=8 member step
+#   counters         rocprofv3 -L on the box (which memory-side counters exist)
 #   sweep            the reference's partition-count sweep through the CLI + the rehearsed GPU-count axis (scripts/sweep.py)
 set -o pipefail
 TAG=${1:?usage: round_measure.sh TAG STEP...}
@@ -64,6 +65,7 @@ for step in "$@"; do
           --group FETCH_SIZE --group WRITE_SIZE \
           --group TCC_HIT_sum,TCC_MISS_sum,TCC_EA0_RDREQ_sum \
           --group TCC_EA0_RDREQ_32B_sum,TCC_REQ_sum \
+          --group TCC_EA0_RDREQ_DRAM_sum,TCC_EA0_RDREQ_sum \
           --group SQ_WAVES,SQ_WAVE_CYCLES,SQ_WAIT_ANY,SQ_BUSY_CYCLES,SQ_INSTS_VALU,SQ_INSTS_LDS,SQ_WAIT_INST_ANY,SQ_INSTS_SALU \
           --group SQ_ACTIVE_INST_VALU,SQ_ACTIVE_INST_LDS,SQ_ACTIVE_INST_VMEM,SQ_LDS_BANK_CONFLICT,SQ_INSTS_VMEM_RD,SQ_INSTS_VMEM_WR,SQ_WAIT_INST_LDS,SQ_ACTIVE_INST_ANY \
           > ${O}_pmc_${cfg}_$kf.jsonl 2> ${O}_pmc_${cfg}_$kf.err || { echo "pmc $cfg $k failed"; tail -20 ${O}_pmc_${cfg}_$kf.err; exit 7; }
@@ -75,6 +77,10 @@ for step in "$@"; do
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$GRAFT_REPO_ROOT/${O}_c2trace" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-traffic > "$GRAFT_REPO_ROOT/${O}_c2trace.log" 2>&1) || { echo "rocprof c2 failed"; tail -5 ${O}_c2trace.log; exit 8; }
       python3 scripts/trace_summary.py ${O}_c2trace --step-kernel "k_cluster_probe<" > ${O}_c2trace.txt 2>&1
       tail -30 ${O}_c2trace.txt ;;
+    counters)
+      # the counters this box's rocprofv3 offers (a MALL / data-fabric split for C4?)
+      timeout -k 10 120 rocprofv3 -L > ${O}_counters.txt 2>&1 || { echo "rocprofv3 -L failed"; tail -5 ${O}_counters.txt; exit 11; }
+      grep -i -E "mall|dram|_df|gmi|ea0_rd" ${O}_counters.txt | head -30 ;;
     sweep)
       timeout -k 10 900 python scripts/sweep.py --skew 1.05 1.25 --rehearse-worlds 1 2 4 8 --out ${O}_sweep_cli > ${O}_sweep.log 2>&1 || { echo "sweep failed"; tail -5 ${O}_sweep.log; exit 9; }
       tail -24 ${O}_sweep.log ;;
