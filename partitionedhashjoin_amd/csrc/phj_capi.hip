@@ -72,7 +72,6 @@ struct Tuning {
     int count_pin = 1;    // LDS join: the last workgroup writes the count to pinned host memory (0: a copy back)
     int r_order = 1;      // LDS join: R's pass 1 beside S's (0), after it (1: measured C2 1.69 vs 1.72 ms, S.p1 1.05 vs 1.19), before it (2)
     int p1_block = 1024;  // ... its workgroup: 1024 x 4 codes (16 waves per CU; measured 1.20 -> 1.07 ms at C2) or 512 x 8, the same tile
-    int p1_wide = 0;      // ... the probe side's pass over 8192-code tiles (1024 x 8: the per-tile scan, claims and chunk protocol over twice the codes): 1 from 2^24 codes, 2 at every size (measured C2 1.608 -> 1.639 ms: off)
     int cluster = 1;      // radix join: LDS cluster tables (phj_cluster.h) when the build side's clusters fit
     int cl_cap = static_cast<int>(kClCapMax);   // ... LDS table slots (8192: two workgroups per CU, 16384: one)
     int cl_bits = 0;      // ... clusters = 2^cl_bits (0: the fewest >= 256 whose average fits the table)
@@ -636,14 +635,6 @@ const void* pipe1024(int kpf) {
     if (kpf == 1) return reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, HK, DPT, 0, false, 1>);
     return reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 4, HK, DPT, 0, PHJ_P1_PROF != 0, 2>);
 }
-// the wide form (PassArgs::wide): 1024 x 8 codes per tile, kWideKpf tiles of keys in flight
-#ifndef PHJ_WIDE_KPF
-#define PHJ_WIDE_KPF 1
-#endif
-template <int HK, int DPT>
-const void* pipe_wide() {
-    return reinterpret_cast<const void*>(&k_chunk_codes_pipe<1024, 8, HK, DPT, 0, PHJ_P1_PROF != 0, PHJ_WIDE_KPF>);
-}
 
 // Workgroups per CU of kernel kfn at `block` threads and `lds` bytes of dynamic
 // LDS, as the runtime reports it (0 if it cannot), cached per host thread: the
@@ -695,12 +686,10 @@ int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const st
         if constexpr (IN_AOS && OUT_AOS && ITEMS <= 8) {
             // persistent: as many workgroups per shard as fit the chip at once
             // (two per CU at 81 KB of LDS), never more than the shard's tiles
-            const bool pipe = a.keys_only && c->tune.p1_pipe && BLOCK == 512 && ITEMS == 8;
-            const bool wide = pipe && a.wide;   // 8192-code tiles (partition_state decided, chunks of that size)
-            const uint32_t TT = wide ? kWideTile : static_cast<uint32_t>(T);
-            const uint32_t ntiles = static_cast<uint32_t>((n + TT - 1) / TT);
+            const uint32_t ntiles = static_cast<uint32_t>((n + T - 1) / T);
             const uint32_t per = (ntiles + a.nshards - 1) / a.nshards;
-            const size_t lds = pipe ? chunk_pipe_lds_bytes(TT, a.nbins) : a.keys_only ? chunk_codes_lds_bytes(T, a.nbins) : sc_lds;
+            const bool pipe = a.keys_only && c->tune.p1_pipe && BLOCK == 512 && ITEMS == 8;
+            const size_t lds = pipe ? chunk_pipe_lds_bytes(T, a.nbins) : a.keys_only ? chunk_codes_lds_bytes(T, a.nbins) : sc_lds;
             const void* kfn = nullptr;
             int kblock = BLOCK;
             // keys only, written as hash codes (the on-chip probe): k_chunk_codes;
@@ -709,10 +698,7 @@ int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const st
             if (a.keys_only && pipe) {
                 if constexpr (BLOCK == 512 && ITEMS == 8) {
                     const int dpt = a.nbins > 2 * BLOCK ? 4 : a.nbins > BLOCK ? 2 : 1;
-                    if (wide) {   // 16 waves per CU, 8 codes per thread
-                        kblock = 1024;
-                        kfn = hk == kMurmur3 ? pipe_wide<kMurmur3, 1>() : pipe_wide<kXXH3, 1>();   // nb1 <= 1024 (wide_pass1)
-                    } else if (c->tune.p1_block == 1024) {   // 16 waves per CU, 4 codes per thread
+                    if (c->tune.p1_block == 1024) {   // 16 waves per CU, 4 codes per thread
                         kblock = 1024;
                         // R's pass (LDS join, tile mode: ~10 tiles per workgroup at C2)
                         // keeps one tile in flight, which also gives it a kernel name of
@@ -761,7 +747,6 @@ int launch_pass_t(phj_ctx* c, int hk, const PassArgs& a, uint32_t grid, const st
             if (c->tune.p1_slots < 0) slots = per;   // one tile per workgroup
             PassArgs ak = a;
             const bool prof = PHJ_P1_PROF && pipe && kblock == 1024 && prefix.rfind("R.", 0) != 0;
-            if (pipe && lds > 160 * 1024) return set_err(c, PHJ_ERR_INVALID, "pipelined code pass: LDS above 160 KB");
             if (prof) {   // diagnostics (measurement build, PHJ_P1_PROF): synchronous, to stderr
                 PHJ_TRY(ensure(c, c->cl_prof, 64 * 8));   // words 32.. (the LDS join's are 0..)
                 ak.prof = static_cast<unsigned long long*>(c->cl_prof.p) + 32;
@@ -879,16 +864,7 @@ int launch_pass(phj_ctx* c, int hk, bool in_aos, bool out_aos, PassArgs a, uint3
 // form for the on-chip probe (half the bytes, three workgroups per CU)
 // wins at every size measured (25M-200M), with shards of p1_ko_tps tiles.
 // use_cluster asks the same of the probe side (the LDS join needs S's codes).
-// The probe side's pipelined code pass over kWideTile-code tiles (chunks of
-// that size, listed as 4096-code tiles for the consumers): one digit per
-// thread and its LDS (two 64 KB sorted tiles) within the CU's 160 KB; from
-// 2^24 codes (a few tiles per workgroup below that), PHJ_P1_WIDE=2 at every size.
-bool wide_pass1(const phj_ctx* c, const Plan& pl, uint64_t n, bool ko) {
-    return ko && c->tune.p1_wide && c->tune.p1_pipe && c->tune.p1_block == 1024 && pl.nb1 <= 1024 &&
-           chunk_pipe_lds_bytes(kWideTile, pl.nb1) <= 160 * 1024 && (c->tune.p1_wide == 2 || n >= (1ull << 24));
-}
-
-bool chunked_pass1(const phj_ctx* c, const Plan& pl, uint64_t n64, bool ko, bool probe_side = false) {
+bool chunked_pass1(const phj_ctx* c, const Plan& pl, uint64_t n64, bool ko) {
     if (pl.npass != 2 || pl.stable || !c->tune.p1_chunk || n64 == 0 || n64 >= (1ull << 32) - 2 * 4096) return false;
     const uint64_t n = n64;
     const TileShape sh = tile_shape(c, pl.nb1);
@@ -899,9 +875,8 @@ bool chunked_pass1(const phj_ctx* c, const Plan& pl, uint64_t n64, bool ko, bool
     if (tile / sh.block > 8) return false;   // registers: the next tile is prefetched
     if ((3 * (n / tile + kShards) + kShards * pl.nb1) * tile >= (1ull << 32)) return false;
     const bool pipe = ko && c->tune.p1_pipe && sh.block == 512 && tile == 4096;
-    // the pipelined code pass's pool (pipe_pool_stride per shard, chunks of ct)
-    const uint64_t ct = probe_side && pipe && wide_pass1(c, pl, n, ko) ? kWideTile : tile;
-    if (pipe && ((kPipeRes + 1) * (n / ct + kShards) + kShards * (3ull * pl.nb1 + 1)) * ct >= (1ull << 32)) return false;
+    // the pipelined code pass's pool (pipe_pool_stride per shard)
+    if (pipe && ((kPipeRes + 1) * (n / tile + kShards) + kShards * (3ull * pl.nb1 + 1)) * tile >= (1ull << 32)) return false;
     return true;
 }
 
@@ -912,14 +887,8 @@ int partition_state(phj_ctx* c, SideState& S, const char* tag, const Plan& pl, b
     const uint64_t n64 = S.n;
     if (n64 >= (1ull << 32) - 2 * 4096) return set_err(c, PHJ_ERR_RANGE, "relation above 2^32 tuples per device");
     const uint32_t n = static_cast<uint32_t>(n64);
+    const uint32_t tile = tile_shape(c, pl.nb1).tile;
     const uint32_t tile2 = pl.npass == 2 ? tile_shape(c, pl.nb2).tile : 0;
-    const bool probe_side = &S == &c->side[PHJ_SIDE_PROBE];
-    const bool ko = p1_only;
-    const bool chunked = chunked_pass1(c, pl, n64, ko, probe_side);
-    // pass 1's tile (and chunk): the wide code pass on the probe side, else the tile kernels'
-    const bool wide = chunked && probe_side && c->tune.p1_pipe && tile_shape(c, pl.nb1).block == 512 &&
-                      tile_shape(c, pl.nb1).tile == 4096 && wide_pass1(c, pl, n64, ko);
-    const uint32_t tile = wide ? kWideTile : static_cast<uint32_t>(tile_shape(c, pl.nb1).tile);
     const uint32_t nt1 = (n + tile - 1) / tile;
     const bool p1_aos = pl.npass == 2;
     // pass 1 leaves the pass-2 digit in a column (tile kernels only)
@@ -935,14 +904,15 @@ int partition_state(phj_ctx* c, SideState& S, const char* tag, const Plan& pl, b
     // histogram read saves; so it starts at p1_min_tiles tiles. The keys-only
     // form for the on-chip probe (half the bytes, three workgroups per CU)
     // wins at every size measured (25M-200M), with shards of p1_ko_tps tiles.
+    const bool ko = p1_only;
+    const bool chunked = chunked_pass1(c, pl, n64, ko);
     S.hcoded = chunked && ko;   // k_chunk_codes
     // chains per digit: ~kTilesPerShard tiles each, a power of two <= kShards
     // (max_shards < kShards: R in tile mode takes exactly that many, so a
     // cluster below the LDS limit has at most max_shards + lim / tile runs)
     uint32_t nshards = 1;
-    // (wide tiles: half as many per shard, the same codes)
     const uint32_t tps = max_shards < kShards ? std::max<uint32_t>(1, (nt1 + max_shards - 1) / max_shards)
-                                              : static_cast<uint32_t>(ko ? c->tune.p1_ko_tps : c->tune.p1_tps) / (wide ? 2u : 1u);
+                                              : static_cast<uint32_t>(ko ? c->tune.p1_ko_tps : c->tune.p1_tps);
     while (nshards < max_shards && static_cast<uint64_t>(nshards) * tps < nt1) nshards <<= 1;
     // pool of pass-1 chunks, one region per shard: a shard takes at most
     // `per` tiles, each with two chunks reserved up front (k_scatter_chunked, k_chunk_codes;
@@ -950,7 +920,7 @@ int partition_state(phj_ctx* c, SideState& S, const char* tag, const Plan& pl, b
     // chains' other starts (each chain wastes at most one partial chunk)
     const uint32_t per = (nt1 + nshards - 1) / nshards;
     // (the pipelined code pass: 2 static chunks per chain, kPipeRes per tile, then its counter)
-    const bool pipe = ko && c->tune.p1_pipe && tile_shape(c, pl.nb1).block == 512 && (tile == 4096 || wide);
+    const bool pipe = ko && c->tune.p1_pipe && tile_shape(c, pl.nb1).block == 512 && tile == 4096;
     const uint32_t pool_stride = pipe ? pipe_pool_stride(per, pl.nb1) : 3 * per + pl.nb1;
     const uint32_t maxch = per + 1;   // chunks of one chain (every tuple of a shard in one digit)
     const size_t slots1 = chunked ? static_cast<size_t>(nshards) * pool_stride * tile : n;
@@ -1019,7 +989,6 @@ int partition_state(phj_ctx* c, SideState& S, const char* tag, const Plan& pl, b
         a.maxch = maxch;
         a.pool_stride = pool_stride;
         a.nshards = nshards;
-        a.wide = wide ? 1u : 0u;
         S.ctab_dirty = n > 0;   // until k_tile_chunks has cleared what pass 1 publishes
         S.chunk_check = n > 0;
     }
@@ -1065,7 +1034,7 @@ int partition_state(phj_ctx* c, SideState& S, const char* tag, const Plan& pl, b
                 {
                     hipLaunchKernelGGL(k_tile_chunks, dim3((pl.nb1 * nshards + kWaves - 1) / kWaves), dim3(kBlock), 0, c->ks, tb2,
                                        static_cast<uint32_t*>(S.ccur.p), pl.nb1, nshards,
-                                       static_cast<unsigned long long*>(S.ctab.p), maxch, pool_stride, tile2, tile,
+                                       static_cast<unsigned long long*>(S.ctab.p), maxch, pool_stride, tile2,
                                        static_cast<uint32_t*>(S.tseg2.p), ts, tc);
                     PHJ_LAUNCHED(c, "k_tile_chunks");
                 }
@@ -1493,7 +1462,7 @@ bool use_cluster(const phj_ctx* c, const Plan& pl, uint64_t nS, uint64_t nR, Pla
         const TileShape sh = tile_shape(c, nb);
         if (sh.tile != 4096 || sh.block != 512) return false;
     }
-    if (nS > 0 && !chunked_pass1(c, out, nS, true, true)) return false;
+    if (nS > 0 && !chunked_pass1(c, out, nS, true)) return false;
     return cluster_empty0(out) != 0 && 4 * nR + 2ull * out.nb1 < (1ull << 32);
 }
 
@@ -1659,7 +1628,7 @@ int probe_cluster(phj_ctx* c, const Plan& pl, SideState& PS, int nseg, const int
         c->split_words = a.split;
     }
     constexpr int B = kClBlock, I = kClItems;
-    const size_t lds = cluster_lds_bytes(a.cap);   // the table + its 16-bit bucket fill counters + displaced bits
+    const size_t lds = cluster_lds_bytes(a.cap);   // the table + its 16-bit bucket fill counters
     constexpr bool PR = PHJ_CL_PROF != 0;   // measurement build: the builds' section clocks
     if (PR) {
         PHJ_TRY(ensure(c, c->cl_prof, 64 * 8));
@@ -2101,7 +2070,6 @@ int ctx_create_device(int device, phj_ctx** out) {
     c->tune.count_pin = env_int("PHJ_COUNT_PIN", 1);
     c->tune.r_chunk = env_int("PHJ_R_CHUNK", 1) != 0;
     c->tune.p1_block = env_int("PHJ_P1_BLOCK", 1024) == 512 ? 512 : 1024;
-    c->tune.p1_wide = std::min(2, std::max(0, env_int("PHJ_P1_WIDE", 0)));
     c->tune.p1_tps = std::max(1, env_int("PHJ_P1_TPS", static_cast<int>(kTilesPerShard)));
     c->tune.p1_min_tiles = std::max(0, env_int("PHJ_P1_MIN_TILES", 32768));
     c->tune.p1_ko_tps = std::max(1, env_int("PHJ_P1_KO_TPS", 1024));

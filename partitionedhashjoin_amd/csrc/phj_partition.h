@@ -139,9 +139,7 @@ struct PassArgs {
     unsigned long long* sink;   // k_chunk_codes: [kSinkGroups][BLOCK] words the stores past the tile target (never read)
     DigitFn f;
     unsigned long long* prof;   // k_chunk_codes_pipe PROF: clocks of its phases, kP1ProfWords (diagnostics)
-    uint32_t wide;              // the pipelined code pass over kWideTile-code tiles (chunks), 1024 x 8
 };
-constexpr uint32_t kWideTile = 8192;
 constexpr int kP1ProfWords = 16;
 
 // Workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md,
@@ -1642,13 +1640,10 @@ __global__ __launch_bounds__(kBlock) void k_tile_seg(const uint32_t* tile_base, 
 // shard x's pool (a stale table) becomes an empty tile and sets the pass's
 // error word (the consumers read no slot through it). Entry nch (the chunk
 // k_chunk_codes_pipe pre-allocates after a chain's last one) is cleared too.
-// CT: the pass's chunk (a multiple of T): each chunk is listed as CT / T tiles
-// of T slots (the wide code pass's 8192-slot chunks as two 4096-code tiles,
-// so the consumers keep their tile); a chain's tiles are ceil(size / T) either way.
 __global__ __launch_bounds__(kBlock) void k_tile_chunks(const uint32_t* tile_base, uint32_t* sizes,
                                                         uint32_t nseg, uint32_t nshards,
                                                         unsigned long long* chunk_tab, uint32_t maxch,
-                                                        uint32_t pool_stride, uint32_t T, uint32_t CT, uint32_t* tile_seg,
+                                                        uint32_t pool_stride, uint32_t T, uint32_t* tile_seg,
                                                         uint32_t* tile_start, uint32_t* tile_cnt) {
     const uint32_t w = blockIdx.x * kWaves + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (w >= nseg * nshards) return;
@@ -1657,23 +1652,20 @@ __global__ __launch_bounds__(kBlock) void k_tile_chunks(const uint32_t* tile_bas
     uint32_t before = (z + T - 1) / T;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) before += __shfl_xor(before, o, 64);
-    const uint32_t szx = sizes[x * nseg + s], nt = (szx + T - 1) / T, nch = (szx + CT - 1) / CT, sub = CT / T;
+    const uint32_t szx = sizes[x * nseg + s], nch = (szx + T - 1) / T;
     const uint32_t t0 = tile_base[s] + before;
     unsigned long long* tab = chunk_tab + (static_cast<size_t>(x) * nseg + s) * maxch;
     uint32_t bad = 0;
-    for (uint32_t k = lane; k < nt; k += 64) {
-        const uint32_t kc = k / sub;   // the tile's chunk
-        const unsigned long long v = kc < maxch ? tab[kc] : 0ull;
+    for (uint32_t k = lane; k < nch; k += 64) {
+        const unsigned long long v = k < maxch ? tab[k] : 0ull;
         const uint32_t id = static_cast<uint32_t>(v);
-        const bool ok = kc < maxch && (v >> 32) == 1ull && id >= x * pool_stride && id < (x + 1) * pool_stride;
+        const bool ok = k < maxch && (v >> 32) == 1ull && id >= x * pool_stride && id < (x + 1) * pool_stride;
         tile_seg[t0 + k] = s;
-        tile_start[t0 + k] = ok ? id * CT + (k - kc * sub) * T : 0u;
+        tile_start[t0 + k] = ok ? id * T : 0u;
         tile_cnt[t0 + k] = ok ? min(T, szx - k * T) : 0u;
         if (!ok) bad |= kChunkErrTable;
+        if (k < maxch) tab[k] = 0;   // the next pass starts from an all-zero table (kPublished)
     }
-    // the next pass starts from an all-zero table (kPublished); every entry
-    // above was read (and its value used) before these stores are issued
-    for (uint32_t k = lane; k < nch && k < maxch; k += 64) tab[k] = 0;
     // the pipelined pass pre-allocates the chunk after a chain's last one
     if (lane == 0 && nch < maxch) tab[nch] = 0;
     if (bad) atomicOr(sizes + chunk_err_word(nseg), bad);

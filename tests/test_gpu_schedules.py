@@ -62,9 +62,6 @@ SCHEDULES = [
     {"PHJ_P1_PIPE": "0", "PHJ_CL_BITS": "11"},                  # ... with four digits per thread
     {"PHJ_P1_BLOCK": "512"},                                    # pipelined pass 1 in 512 x 8 workgroups
     {"PHJ_P1_BLOCK": "512", "PHJ_CL_BITS": "11"},               # ... four digits per thread
-    {"PHJ_P1_WIDE": "2"},                                       # probe side's pass 1 over 8192-code tiles at every size
-    {"PHJ_P1_WIDE": "2", "PHJ_P1_KO_TPS": "4"},                 # ... over 16 shards
-    {"PHJ_P1_WIDE": "1"},                                       # ... from 2^24 codes
     {"PHJ_R_CHUNK": "0"},                                       # LDS join: R by the stable pass (codes contiguous per cluster)
     {"PHJ_R_CHUNK": "0", "PHJ_CL_BITS": "11"},                  # ... 2048 clusters
     {"PHJ_R_ORDER": "0"},                                       # LDS join: R's pass 1 beside S's
